@@ -1,0 +1,100 @@
+#!/usr/bin/env python3
+"""Regenerate the committed golden fixtures from the REFERENCE built by oracle/Makefile.ref.
+
+TEST INFRASTRUCTURE.  Runs in the development container only (needs /root/reference):
+
+  tests/golden/ref_vectors.json  primitive vectors printed by oracle/_ref/ref_golden (field ops,
+                                 pubkeys, hash160 02/03/04, XXH64, bloom sizing/fill, group
+                                 walk, BSGS baby tables at small M)
+  tests/golden/ref_e2e.json      end-to-end hit sets of oracle/_ref/keyhunt (the reference CLI) on
+                                 known-answer windows, parsed from the
+                                 KEYFOUNDKEYFOUND.txt it writes.
+
+Usage:  python oracle/make_golden.py [--vectors] [--e2e]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import re
+import shutil
+import subprocess
+import tempfile
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+DATA = os.path.join(REPO, "tests", "golden", "data")
+REF_BIN = os.path.join(HERE, "_ref", "keyhunt")
+REF_GOLDEN = os.path.join(HERE, "_ref", "ref_golden")
+
+# (name, argv after the binary, timeout s).  Windows from SURVEY.md 8c.
+E2E_RUNS = [
+    ("address_1to32_2p20", ["-m", "address", "-f", "1to32.txt", "-r", "1:100000", "-n", "0x100000", "-t", "8"], 300),
+    ("rmd160_1to32_compress_2p20", ["-m", "rmd160", "-f", "1to32.rmd", "-l", "compress", "-r", "1:100000", "-n", "0x100000", "-t", "8"], 300),
+    ("xpoint_1to63_65_2p20", ["-m", "xpoint", "-f", "1to63_65.txt", "-r", "1:100000", "-n", "0x100000", "-t", "8"], 300),
+    ("rmd160_66_window", ["-m", "rmd160", "-f", "66.rmd", "-l", "compress", "-r", "2832ed74f2b000000:2832ed74f2bffffff", "-n", "0x100000", "-t", "8"], 600),
+    ("address_66_window", ["-m", "address", "-f", "66.txt", "-l", "compress", "-r", "2832ed74f2b400000:2832ed74f2b7fffff", "-n", "0x100000", "-t", "8"], 600),
+    ("rmd160_64_window", ["-m", "rmd160", "-f", "64.rmd", "-l", "compress", "-r", "f7051f27b0000000:f7051f27b0ffffff", "-n", "0x100000", "-t", "8"], 600),
+    ("xpoint_63_window", ["-m", "xpoint", "-f", "63.pub", "-r", "7cce5efdac000000:7cce5efdacffffff", "-n", "0x100000", "-t", "8"], 600),
+    ("bsgs_120_window", ["-m", "bsgs", "-f", "120.txt", "-r", "b10f22572c497a836e9d0000000000:b10f22572c497a836edd0000000000", "-t", "8"], 300),
+    ("bsgs_125_window", ["-m", "bsgs", "-f", "125.txt", "-r", "1c533b6bb7f0804e0995fe0000000000:1c533b6bb7f0804e09963e0000000000", "-t", "8"], 300),
+    ("bsgs_130_window", ["-m", "bsgs", "-f", "130.txt", "-r", "33e7665705359f04f28b8880000000000:33e7665705359f04f28b8c80000000000", "-t", "8"], 300),
+    ("bsgs_63_window", ["-m", "bsgs", "-f", "63.pub", "-r", "7cce5a0000000000:7cce9a0000000000", "-t", "8"], 300),
+    ("bsgs_test120_b120", ["-m", "bsgs", "-f", "test120.txt", "-b", "120", "-t", "8"], 300),
+    ("bsgs_63_small_n_k4", ["-m", "bsgs", "-f", "63.pub", "-n", "0x1000000", "-k", "4", "-r", "7cce5efdac000000:7cce5efdad000000", "-t", "8"], 300),
+]
+
+
+def gen_vectors() -> None:
+    subprocess.run(["make", "-s", "-C", HERE, "-f", "Makefile.ref", "-j8"], check=True)
+    out = subprocess.run([REF_GOLDEN], check=True, capture_output=True, text=True).stdout
+    doc = json.loads(out)
+    doc["_generator"] = "oracle/_ref/ref_golden (oracle/ref_golden.cpp linked against the reference's own sources)"
+    with open(os.path.join(REPO, "tests", "golden", "ref_vectors.json"), "w") as f:
+        json.dump(doc, f, indent=1)
+
+
+def parse_keyfound(text: str) -> list[dict]:
+    hits = []
+    for m in re.finditer(r"Private Key: ([0-9a-f]+)\npubkey: ([0-9a-f]+)\nAddress (\S+)\nrmd160 ([0-9a-f]+)", text):
+        hits.append({"key": m.group(1), "pubkey": m.group(2), "address": m.group(3), "rmd160": m.group(4)})
+    for m in re.finditer(r"Key found privkey ([0-9a-f]+)\nPublickey ([0-9a-f]+)", text):
+        hits.append({"key": m.group(1), "pubkey": m.group(2)})
+    return hits
+
+
+def gen_e2e(only: list[str] | None = None) -> None:
+    subprocess.run(["make", "-s", "-C", HERE, "-f", "Makefile.ref", "-j8"], check=True)
+    path = os.path.join(REPO, "tests", "golden", "ref_e2e.json")
+    results = json.load(open(path)) if os.path.exists(path) else {}
+    for name, argv, tmo in E2E_RUNS:
+        if only and name not in only:
+            continue
+        with tempfile.TemporaryDirectory() as td:
+            for fn in os.listdir(DATA):
+                shutil.copy(os.path.join(DATA, fn), td)
+            p = subprocess.run(["timeout", str(tmo), REF_BIN] + argv + ["-q"], cwd=td, capture_output=True, text=True)
+            kf = os.path.join(td, "KEYFOUNDKEYFOUND.txt")
+            text = open(kf).read() if os.path.exists(kf) else ""
+            hits = parse_keyfound(text)
+            results[name] = {"argv": argv, "exit": p.returncode, "hits": sorted(hits, key=lambda h: int(h["key"], 16)),
+                             "stdout_hit_lines": [ln.strip() for ln in p.stdout.split("\n") if "Hit!" in ln or "Key found" in ln]}
+            print(f"{name}: exit={p.returncode} hits={len(hits)}", flush=True)
+    results["_generator"] = "oracle/make_golden.py running oracle/_ref/keyhunt (reference CLI built from its sources)"
+    with open(path, "w") as f:
+        json.dump(results, f, indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--vectors", action="store_true")
+    ap.add_argument("--e2e", action="store_true")
+    ap.add_argument("--only", nargs="*")
+    a = ap.parse_args()
+    if not a.vectors and not a.e2e:
+        a.vectors = a.e2e = True
+    if a.vectors:
+        gen_vectors()
+    if a.e2e:
+        gen_e2e(a.only)
