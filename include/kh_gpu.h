@@ -1,0 +1,146 @@
+/*
+ * kh_gpu.h -- C ABI of the MI355X keyhunt engine (libkh_gpu.so).
+ *
+ * The reference (naanprofit/keyhunt) has no plugin API: its hot path is file-static C++ driven by
+ * globals.  The seams this ABI replaces are the bodies of its worker threads:
+ *
+ *   kh_scan            <- thread_process, one N_SEQUENTIAL_MAX chunk      keyhunt.cpp:3265-3861
+ *                         (group walk 3349-3461, hash160/xpoint probes 3475-3830, bloom_check +
+ *                          searchbinary 3065-3089, parity fix-up 3619-3636)
+ *   kh_set_targets     <- readFileAddress/forceReadFileAddress/...XPoint  keyhunt.cpp:7239-7490
+ *                         + initBloomFilter 7605-7626 + _sort 1359-1364
+ *   kh_bsgs_setup      <- BSGS parameter block                            keyhunt.cpp:1454-1842
+ *   kh_bsgs_build      <- thread_bPload / thread_bPload_2blooms + bsgs_sort keyhunt.cpp:5284-5644, 2466-2503
+ *   kh_bsgs_scan       <- thread_process_bsgs (sequential), bases of 2N   keyhunt.cpp:4549-4888
+ *                         with bsgs_secondcheck / bsgs_thirdcheck          keyhunt.cpp:5151-5248
+ *
+ * Conventions: plain C types only; 256-bit scalars and coordinates are 32-byte BIG-endian
+ * (Int::Get32Bytes); every call returns 0 on success or a negative KH_E* code (never exits);
+ * calls on one context are not re-entrant, contexts on different devices are independent;
+ * the host owns every buffer passed in, the library owns device memory inside the context.
+ * The engine never falls back to the CPU: if the HIP code object cannot run, calls fail.
+ */
+#ifndef KH_GPU_H
+#define KH_GPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KH_ABI_VERSION 1
+
+/* error codes */
+#define KH_OK 0
+#define KH_E_ARG -1        /* invalid argument */
+#define KH_E_HIP -2        /* HIP runtime error (see kh_last_error) */
+#define KH_E_NOMEM -3      /* device or host allocation failed */
+#define KH_E_STATE -4      /* call out of order (e.g. scan before targets) */
+#define KH_E_OVERFLOW -5   /* caller's output array too small (count is still reported) */
+#define KH_E_BSGS_N -6     /* BSGS: n has no exact square root / sqrt(n) not a multiple of 1024 */
+#define KH_E_RANGE -7      /* BSGS: range smaller than N ("[E] the given range is small") */
+
+/* scan modes (-m) and search kinds (-l) */
+#define KH_MODE_ADDRESS 0  /* -m address / -m rmd160: hash160 probes */
+#define KH_MODE_XPOINT 1   /* -m xpoint: X[0..20) probes */
+#define KH_SEARCH_COMPRESS 0
+#define KH_SEARCH_UNCOMPRESS 1
+#define KH_SEARCH_BOTH 2   /* reference default (FLAGSEARCH = 2) */
+
+/* hit kinds */
+#define KH_KIND_02 0       /* hash160(02||X) matched */
+#define KH_KIND_03 1       /* hash160(03||X) matched */
+#define KH_KIND_04 2       /* hash160(04||X||Y) matched */
+#define KH_KIND_XPOINT 3   /* X[0..20) matched */
+
+typedef struct kh_ctx kh_ctx;
+
+/* one confirmed hit of kh_scan: the private key as the reference would print it */
+typedef struct {
+  uint8_t key[32];      /* big-endian; already negated (n - k) where the reference negates */
+  uint64_t offset;      /* key offset from the chunk start (before negation) */
+  uint32_t kind;        /* KH_KIND_* */
+  uint32_t compressed;  /* 1 -> writekey(true, ...), 0 -> writekey(false, ...) */
+} kh_hit;
+
+/* BSGS parameters exactly as the reference derives them */
+typedef struct {
+  uint64_t n;           /* BSGS_N (rounded down to a multiple of M) */
+  uint64_t m, m2, m3;   /* bsgs_m, bsgs_m2, bsgs_m3 */
+  uint64_t aux;         /* bsgs_aux = N / M */
+  uint64_t cycles;      /* ceil(aux / 1024) 1024-point groups per base */
+  uint64_t bloom_bits[3], bloom_bytes[3];  /* per shard, layers 1..3 */
+  uint32_t bloom_hashes[3];
+  uint32_t pad;
+} kh_bsgs_info;
+
+/* one key found by kh_bsgs_scan */
+typedef struct {
+  uint32_t target;      /* index into the targets given to kh_bsgs_set_targets */
+  uint32_t pad;
+  uint8_t key[32];      /* big-endian private key */
+} kh_bsgs_found;
+
+/* ---- context ------------------------------------------------------------------------------ */
+int kh_device_count(int *count);
+int kh_open(int device, kh_ctx **out);
+int kh_close(kh_ctx *ctx);
+const char *kh_strerror(int code);
+const char *kh_last_error(kh_ctx *ctx);
+int kh_abi_version(void);
+/* lanes per walk launch (0 = automatic); groups (of 1024 points) per lane per launch (0 = auto) */
+int kh_set_geometry(kh_ctx *ctx, uint32_t lanes, uint32_t groups_per_launch);
+int kh_synchronize(kh_ctx *ctx);
+
+/* ---- address / rmd160 / xpoint ------------------------------------------------------------ */
+/* rows: n x 20 bytes (hash160s, or X[0..20) for xpoint), any order.  bloom_items: the element
+ * count the reference sizes its bloom with (numberItems), 0 -> n.  Sorts the table, builds the
+ * reference-layout bloom (bloom_init2(max(10000, items), 1e-6)) and uploads both. */
+int kh_set_targets(kh_ctx *ctx, const uint8_t *rows, uint64_t n, uint64_t bloom_items);
+/* Scan keys start + i*stride, i in [0, n_keys) (n_keys a multiple of 1024; stride NULL -> 1).
+ * Returns the confirmed hits in the order one reference thread prints them. */
+int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride[32], uint64_t n_keys, uint32_t mode,
+            uint32_t search, kh_hit *hits, uint32_t cap, uint32_t *n_hits);
+
+/* ---- BSGS --------------------------------------------------------------------------------- */
+int kh_bsgs_setup(kh_ctx *ctx, uint64_t n, uint64_t k, kh_bsgs_info *info);
+int kh_bsgs_build(kh_ctx *ctx);                  /* baby-step blooms + sorted bP table on the GPU */
+/* targets: n x {x[32], y[32]} affine points (big-endian) */
+int kh_bsgs_set_targets(kh_ctx *ctx, const uint8_t *xy, uint32_t n);
+/* Walk n_bases bases start, start + 2N, ... for every target not yet found.  Keys already found
+ * are skipped (like bsgs_found[]).  found: keys found by THIS call. */
+int kh_bsgs_scan(kh_ctx *ctx, const uint8_t start[32], uint64_t n_bases, kh_bsgs_found *found, uint32_t cap,
+                 uint32_t *n_found);
+int kh_bsgs_reset_found(kh_ctx *ctx);
+/* first-level bloom candidates seen so far (for stats / parity tests) */
+int kh_bsgs_candidates(kh_ctx *ctx, uint64_t *count);
+
+/* ---- measurement -------------------------------------------------------------------------- */
+/* Accumulated device time of walk launches of one kind since the last reset, measured with
+ * HIP events on the context's stream.  kind: 0 address/rmd160, 1 xpoint, 2 bsgs giant,
+ * 3 bsgs build, 4 lane setup (scalar mult). */
+int kh_kernel_time(kh_ctx *ctx, uint32_t kind, uint64_t *launches, double *ms, uint64_t *points);
+int kh_kernel_time_reset(kh_ctx *ctx);
+
+/* ---- parity hooks (used by tests/) -------------------------------------------------------- */
+/* k*G for n scalars (big-endian 32 B each) -> n x {x,y} (big-endian), through the lane-setup kernel */
+int kh_pubkeys(kh_ctx *ctx, const uint8_t *scalars, uint32_t n, uint8_t *xy);
+/* X (and Y if out_y) of points start + i*stride, i < n_points (multiple of 1024), via the walk */
+int kh_walk_points(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride[32], uint64_t n_points,
+                   uint8_t *out_x, uint8_t *out_y);
+/* per input point: hash160(02||X), hash160(03||X), hash160(04||X||Y) -> 60 bytes */
+int kh_hash160(kh_ctx *ctx, const uint8_t *xy, uint32_t n, uint8_t *out60);
+/* field ops on the device: per pair (a,b) -> mul, sqr(a), inv(a), add, sub (5 x 32 B) */
+int kh_field_ops(kh_ctx *ctx, const uint8_t *a, const uint8_t *b, uint32_t n, uint8_t *out160);
+/* bloom_check of n items (len 20 or 32) against the target bloom (layer 0) or BSGS layer 1..3 */
+int kh_bloom_check(kh_ctx *ctx, uint32_t layer, const uint8_t *items, uint32_t n, uint32_t len, uint8_t *out);
+/* copy a bloom back: layer 0 = target bloom, 1..3 = BSGS layers (256 shards concatenated, unpadded) */
+int kh_get_bloom(kh_ctx *ctx, uint32_t layer, uint8_t *buf, uint64_t cap, uint64_t *bytes);
+/* sorted bP table as the reference's 16-byte bsgs_xvalue rows {value[6], pad[2], index u64 LE} */
+int kh_get_bsgs_table(kh_ctx *ctx, uint8_t *buf, uint64_t cap_rows, uint64_t *rows);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KH_GPU_H */

@@ -1,0 +1,1284 @@
+// kh_capi.cpp -- implementation of include/kh_gpu.h.
+//
+// Host side of the MI355X engine: device memory layout, lane partitioning, launches, the
+// reference-exact host steps around the kernels (bloom sizing, table sort + searchbinary,
+// compressed-key parity fix-up, BSGS second/third check), and event timing.  Every scan and
+// build runs on the GPU kernels in kh_kernels.hip; there is no CPU fallback.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+#include <algorithm>
+#include <array>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "kh_gpu.h"
+#include "kh_kernels.h"
+#include "kh_math.h"
+
+using namespace kh;
+
+// ==============================================================================================
+// 256-bit scalars (mod n) on the host
+// ==============================================================================================
+namespace {
+
+typedef unsigned __int128 u128;
+struct u256 {
+  uint64_t v[4];
+};
+const u256 ORDER_N = {{0xBFD25E8CD0364141ULL, 0xBAAEDCE6AF48A03BULL, 0xFFFFFFFFFFFFFFFEULL, 0xFFFFFFFFFFFFFFFFULL}};
+
+u256 u256_from_be(const uint8_t b[32]) {
+  u256 r;
+  for (int i = 0; i < 4; i++) {
+    uint64_t w = 0;
+    for (int j = 0; j < 8; j++) w = (w << 8) | b[(3 - i) * 8 + j];
+    r.v[i] = w;
+  }
+  return r;
+}
+void u256_to_be(uint8_t b[32], const u256 &a) {
+  for (int i = 0; i < 4; i++)
+    for (int j = 0; j < 8; j++) b[(3 - i) * 8 + j] = (uint8_t)(a.v[i] >> (56 - 8 * j));
+}
+u256 u256_from_u128(u128 x) { return u256{{(uint64_t)x, (uint64_t)(x >> 64), 0, 0}}; }
+u256 u256_u64(uint64_t x) { return u256{{x, 0, 0, 0}}; }
+int u256_cmp(const u256 &a, const u256 &b) {
+  for (int i = 3; i >= 0; i--) {
+    if (a.v[i] < b.v[i]) return -1;
+    if (a.v[i] > b.v[i]) return 1;
+  }
+  return 0;
+}
+bool u256_is_zero(const u256 &a) { return (a.v[0] | a.v[1] | a.v[2] | a.v[3]) == 0; }
+uint64_t u256_add_raw(u256 &r, const u256 &a, const u256 &b) {
+  u128 c = 0;
+  for (int i = 0; i < 4; i++) {
+    c += (u128)a.v[i] + b.v[i];
+    r.v[i] = (uint64_t)c;
+    c >>= 64;
+  }
+  return (uint64_t)c;
+}
+uint64_t u256_sub_raw(u256 &r, const u256 &a, const u256 &b) {
+  uint64_t br = 0;
+  for (int i = 0; i < 4; i++) {
+    u128 t = (u128)a.v[i] - b.v[i] - br;
+    r.v[i] = (uint64_t)t;
+    br = (uint64_t)(t >> 64) & 1;
+  }
+  return br;
+}
+u256 sc_reduce(u256 a) {
+  while (u256_cmp(a, ORDER_N) >= 0) u256_sub_raw(a, a, ORDER_N);
+  return a;
+}
+u256 sc_add(const u256 &a, const u256 &b) {
+  u256 r;
+  uint64_t c = u256_add_raw(r, a, b);
+  if (c || u256_cmp(r, ORDER_N) >= 0) u256_sub_raw(r, r, ORDER_N);
+  return r;
+}
+u256 sc_neg(const u256 &a) {
+  if (u256_is_zero(a)) return a;
+  u256 r;
+  u256_sub_raw(r, ORDER_N, a);
+  return r;
+}
+u256 sc_sub(const u256 &a, const u256 &b) { return sc_add(a, sc_neg(b)); }
+// a * m mod n for a < n, m < 2^64
+u256 sc_mul_u64(const u256 &a, uint64_t m) {
+  u256 r = u256_u64(0), x = a;
+  while (m) {
+    if (m & 1) r = sc_add(r, x);
+    x = sc_add(x, x);
+    m >>= 1;
+  }
+  return r;
+}
+void u256_to_limbs(uint32_t out[8], const u256 &a) {
+  for (int i = 0; i < 4; i++) {
+    out[2 * i] = (uint32_t)a.v[i];
+    out[2 * i + 1] = (uint32_t)(a.v[i] >> 32);
+  }
+}
+fe fe_of(const u256 &a) {
+  fe r;
+  u256_to_limbs(r.d, a);
+  return r;
+}
+u256 u256_of(const fe &a) {
+  u256 r;
+  for (int i = 0; i < 4; i++) r.v[i] = (uint64_t)a.d[2 * i] | ((uint64_t)a.d[2 * i + 1] << 32);
+  return r;
+}
+
+// ==============================================================================================
+// libbloom2 sizing, exactly as bloom/bloom.cpp:154-187 computes it (long double, bpe as double)
+// ==============================================================================================
+bloom_desc bloom_size(uint64_t entries) {
+  long double num = -logl((long double)0.000001);
+  long double denom = 0.480453013918201;
+  double bpe = (double)(num / denom);
+  long double allbits = (long double)entries * bpe;
+  bloom_desc d;
+  memset(&d, 0, sizeof d);
+  d.bits = (uint64_t)allbits;
+  d.bytes = d.bits / 8 + ((d.bits % 8) ? 1 : 0);
+  d.hashes = (uint32_t)(uint8_t)ceil(0.693147180559945 * bpe);
+  d.recip = ~0ULL / d.bits;
+  d.stride = d.bytes;
+  return d;
+}
+// keyhunt's entry count rule: initBloomFilter uses max(10000, items) (keyhunt.cpp:7608)
+uint64_t bloom_entries(uint64_t items) { return items <= 10000 ? 10000 : items; }
+
+void host_bloom_hash(const uint8_t *buf, int len, uint64_t &a, uint64_t &b) {
+  if (len == 32) {
+    uint64_t in[4];
+    for (int k = 0; k < 4; k++) {
+      uint64_t v = 0;
+      for (int q = 7; q >= 0; q--) v = (v << 8) | buf[8 * k + q];
+      in[k] = v;
+    }
+    a = xxh64_32(in, KH_BLOOM_SEED);
+    b = xxh64_32(in, a);
+  } else {
+    uint32_t w[5];
+    for (int k = 0; k < 5; k++)
+      w[k] = (uint32_t)buf[4 * k] | ((uint32_t)buf[4 * k + 1] << 8) | ((uint32_t)buf[4 * k + 2] << 16) |
+             ((uint32_t)buf[4 * k + 3] << 24);
+    a = xxh64_20(w, KH_BLOOM_SEED);
+    b = xxh64_20(w, a);
+  }
+}
+void host_bloom_add(uint8_t *bf, const bloom_desc &d, const uint8_t *buf, int len) {
+  uint64_t a, b;
+  host_bloom_hash(buf, len, a, b);
+  uint64_t h = a;
+  for (uint32_t i = 0; i < d.hashes; i++) {
+    uint64_t x = h % d.bits;
+    bf[x >> 3] |= (uint8_t)(1u << (x & 7));
+    h += b;
+  }
+}
+bool host_bloom_check(const uint8_t *bf, const bloom_desc &d, const uint8_t *buf, int len) {
+  uint64_t a, b;
+  host_bloom_hash(buf, len, a, b);
+  uint64_t h = a;
+  for (uint32_t i = 0; i < d.hashes; i++) {
+    uint64_t x = h % d.bits;
+    if (!((bf[x >> 3] >> (x & 7)) & 1)) return false;
+    h += b;
+  }
+  return true;
+}
+
+// searchbinary (keyhunt.cpp:3065-3089): the reference's own midpoint loop
+bool searchbinary(const uint8_t *rows, int64_t n, const uint8_t *key, int width, int key_off) {
+  int64_t half = n, min = 0, max = n, cur = 0;
+  while (half >= 1) {
+    half = (max - min) / 2;
+    int c = memcmp(key + key_off, rows + (cur + half) * width, width);
+    if (c == 0) return true;
+    if (c < 0)
+      max = max - half;
+    else
+      min = min + half;
+    cur = min;
+  }
+  return false;
+}
+
+// ==============================================================================================
+// host EC with the comb table (the same table the setup kernel reads)
+// ==============================================================================================
+ge G_POINT() {
+  ge g;
+  const uint64_t gx[4] = {0x59F2815B16F81798ULL, 0x029BFCDB2DCE28D9ULL, 0x55A06295CE870B07ULL, 0x79BE667EF9DCBBACULL};
+  const uint64_t gy[4] = {0x9C47D08FFB10D4B8ULL, 0xFD17B448A6855419ULL, 0x5DA4FBFC0E1108A8ULL, 0x483ADA7726A3C465ULL};
+  fe_from_u64(g.x, gx);
+  fe_from_u64(g.y, gy);
+  return g;
+}
+
+struct comb_table {
+  std::vector<ge> t;  // 32 * 256 (entry v = 0 unused)
+  void build() {
+    t.assign(32 * 256, ge{});
+    ge base = G_POINT();
+    for (int j = 0; j < 32; j++) {
+      t[j * 256 + 1] = base;
+      ge_double(t[j * 256 + 2], base);
+      for (int v = 3; v < 256; v++) ge_add(t[j * 256 + v], t[j * 256 + v - 1], base);
+      if (j < 31) {
+        ge b = base;
+        for (int k = 0; k < 8; k++) ge_double(b, b);
+        base = b;
+      }
+    }
+  }
+  // k*G (k reduced mod n, k != 0); returns false for k == 0
+  bool mult(ge &r, const u256 &k_in) const {
+    u256 k = sc_reduce(k_in);
+    if (u256_is_zero(k)) return false;
+    gej acc;
+    acc.inf = true;
+    for (int j = 0; j < 32; j++) {
+      uint32_t v = (uint32_t)(k.v[j >> 3] >> ((j & 7) * 8)) & 0xFF;
+      if (v) gej_add_ge(acc, t[j * 256 + v]);
+    }
+    gej_to_ge(r, acc);
+    return true;
+  }
+};
+
+// Montgomery-trick batch inversion (IntGroup::ModInv); zero elements are skipped (left 0)
+void batch_inv(std::vector<fe> &a) {
+  size_t n = a.size();
+  std::vector<fe> pre(n);
+  fe acc;
+  fe_set_u32(acc, 1);
+  for (size_t i = 0; i < n; i++) {
+    if (!fe_is_zero(a[i])) fe_mul(acc, acc, a[i]);
+    pre[i] = acc;
+  }
+  fe inv;
+  fe_inv(inv, acc);
+  for (size_t i = n; i-- > 0;) {
+    if (fe_is_zero(a[i])) continue;
+    fe prev;
+    if (i == 0)
+      fe_set_u32(prev, 1);
+    else
+      prev = pre[i - 1];
+    fe t;
+    fe_mul(t, inv, prev);
+    fe_mul(inv, inv, a[i]);
+    a[i] = t;
+  }
+}
+
+struct timing {
+  uint64_t launches = 0, points = 0;
+  double ms = 0;
+};
+
+}  // namespace
+
+// ==============================================================================================
+// context
+// ==============================================================================================
+struct kh_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  comb_table comb;
+  uint32_t *d_comb = nullptr;
+
+  // lanes
+  uint32_t lanes_max = 1u << 18;
+  uint32_t groups_per_launch = 0;
+  uint32_t lanes_alloc = 0;
+  uint32_t *d_cx = nullptr, *d_cy = nullptr, *d_scalars = nullptr;
+  uint4 *d_scratch = nullptr;
+  std::vector<uint32_t> h_scalars;
+
+  // walk delta tables: key -> device table ((H+1) x 16 words)
+  std::vector<std::pair<std::string, uint32_t *>> tables;
+
+  // hits
+  uint32_t hit_cap = 1u << 16;
+  uint32_t *d_hit_count = nullptr;
+  kh_dev_hit *d_hits = nullptr;
+  std::vector<kh_dev_hit> h_hits;
+
+  // address targets
+  std::vector<uint8_t> rows;  // sorted, 20 B each
+  uint64_t n_rows = 0;
+  bloom_desc tbd{};
+  std::vector<uint8_t> h_tbloom;
+  uint8_t *d_tbloom = nullptr;
+
+  // bsgs
+  bool bsgs_ready = false, bsgs_built = false;
+  kh_bsgs_info info{};
+  bloom_desc bd[3]{};
+  uint8_t *d_bl[3] = {nullptr, nullptr, nullptr};
+  std::vector<uint8_t> h_bl[3];  // layers 2 and 3 on the host for refinement (index 1, 2)
+  std::vector<uint8_t> h_rows;   // sorted 16-byte bsgs_xvalue rows
+  std::vector<ge> amp2, amp3;
+  std::vector<ge> targets;
+  std::vector<uint8_t> found;
+  uint64_t candidates = 0;
+
+  // timing
+  hipEvent_t ev_a = nullptr, ev_b = nullptr;
+  timing tm[5];
+
+  ~kh_ctx();
+};
+
+#define HIPCHK(ctx, call)                                                                    \
+  do {                                                                                       \
+    hipError_t e_ = (call);                                                                  \
+    if (e_ != hipSuccess) {                                                                  \
+      (ctx)->err = std::string(#call) + ": " + hipGetErrorString(e_);                        \
+      return KH_E_HIP;                                                                       \
+    }                                                                                        \
+  } while (0)
+
+kh_ctx::~kh_ctx() {
+  (void)hipSetDevice(device);
+  if (stream) (void)hipStreamSynchronize(stream);
+  (void)hipFree(d_comb);
+  (void)hipFree(d_cx);
+  (void)hipFree(d_cy);
+  (void)hipFree(d_scalars);
+  (void)hipFree(d_scratch);
+  for (auto &t : tables) (void)hipFree(t.second);
+  (void)hipFree(d_hit_count);
+  (void)hipFree(d_hits);
+  (void)hipFree(d_tbloom);
+  for (int i = 0; i < 3; i++) (void)hipFree(d_bl[i]);
+  if (ev_a) (void)hipEventDestroy(ev_a);
+  if (ev_b) (void)hipEventDestroy(ev_b);
+  if (stream) (void)hipStreamDestroy(stream);
+}
+
+namespace {
+
+int ensure_lanes(kh_ctx *c, uint32_t L) {
+  if (L <= c->lanes_alloc) return KH_OK;
+  (void)hipFree(c->d_cx);
+  (void)hipFree(c->d_cy);
+  (void)hipFree(c->d_scalars);
+  (void)hipFree(c->d_scratch);
+  c->d_cx = c->d_cy = c->d_scalars = nullptr;
+  c->d_scratch = nullptr;
+  c->lanes_alloc = 0;
+  HIPCHK(c, hipMalloc(&c->d_cx, (size_t)L * 32));
+  HIPCHK(c, hipMalloc(&c->d_cy, (size_t)L * 32));
+  HIPCHK(c, hipMalloc(&c->d_scalars, (size_t)L * 32));
+  HIPCHK(c, hipMalloc(&c->d_scratch, (size_t)L * KH_WALK_H * 32));
+  c->lanes_alloc = L;
+  return KH_OK;
+}
+
+// delta table T[i] = (i+1)*D, i < H, and T[H] = 2H*D, for D = d*G (d a scalar, may be "negative")
+int get_table(kh_ctx *c, const u256 &d, const uint32_t **out) {
+  uint8_t be[32];
+  u256_to_be(be, d);
+  std::string key((const char *)be, 32);
+  for (auto &t : c->tables)
+    if (t.first == key) {
+      *out = t.second;
+      return KH_OK;
+    }
+  const int H = KH_WALK_H;
+  std::vector<uint32_t> h((size_t)(H + 1) * 16);
+  ge D;
+  if (!c->comb.mult(D, d)) {
+    c->err = "delta scalar is 0";
+    return KH_E_ARG;
+  }
+  ge cur = D;
+  for (int i = 0; i < H; i++) {
+    if (i == 1) ge_double(cur, D);
+    if (i >= 2) ge_add(cur, cur, D);
+    memcpy(&h[(size_t)i * 16], cur.x.d, 32);
+    memcpy(&h[(size_t)i * 16 + 8], cur.y.d, 32);
+  }
+  ge d2;
+  ge_double(d2, cur);  // 2H * D
+  memcpy(&h[(size_t)H * 16], d2.x.d, 32);
+  memcpy(&h[(size_t)H * 16 + 8], d2.y.d, 32);
+  uint32_t *dev = nullptr;
+  HIPCHK(c, hipMalloc(&dev, h.size() * 4));
+  HIPCHK(c, hipMemcpy(dev, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+  c->tables.push_back({key, dev});
+  *out = dev;
+  return KH_OK;
+}
+
+// Lane centres: C_g = [Q +] s_g*G.  s: L scalars (already reduced, non-zero)
+int run_setup(kh_ctx *c, const std::vector<u256> &s, const ge *q) {
+  uint32_t L = (uint32_t)s.size();
+  int r = ensure_lanes(c, L);
+  if (r) return r;
+  c->h_scalars.resize((size_t)L * 8);
+  for (uint32_t g = 0; g < L; g++) u256_to_limbs(&c->h_scalars[(size_t)g * 8], s[g]);
+  HIPCHK(c, hipMemcpyAsync(c->d_scalars, c->h_scalars.data(), (size_t)L * 32, hipMemcpyHostToDevice, c->stream));
+  setup_args A;
+  memset(&A, 0, sizeof A);
+  A.scalars = c->d_scalars;
+  A.comb = c->d_comb;
+  A.L = L;
+  A.cx = c->d_cx;
+  A.cy = c->d_cy;
+  uint32_t *dq = nullptr;
+  if (q) {
+    HIPCHK(c, hipMalloc(&dq, 64));
+    HIPCHK(c, hipMemcpyAsync(dq, q->x.d, 32, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(dq + 8, q->y.d, 32, hipMemcpyHostToDevice, c->stream));
+    A.q = dq;
+    A.has_q = 1;
+  }
+  HIPCHK(c, hipEventRecord(c->ev_a, c->stream));
+  HIPCHK(c, launch_setup(A, c->stream));
+  HIPCHK(c, hipEventRecord(c->ev_b, c->stream));
+  HIPCHK(c, hipEventSynchronize(c->ev_b));
+  float ms = 0;
+  (void)hipEventElapsedTime(&ms, c->ev_a, c->ev_b);
+  c->tm[4].launches++;
+  c->tm[4].ms += ms;
+  c->tm[4].points += L;
+  if (dq) (void)hipFree(dq);
+  return KH_OK;
+}
+
+struct job_geom {
+  uint32_t L;
+  uint64_t gpl;  // groups per lane in the job
+};
+// lanes cover total_groups groups; gpl must divide `gpl_divides` when non-zero
+job_geom plan(kh_ctx *c, uint64_t total_groups, uint64_t gpl_divides) {
+  job_geom g;
+  uint64_t gpl = (total_groups + c->lanes_max - 1) / c->lanes_max;
+  if (gpl == 0) gpl = 1;
+  if (gpl_divides) {
+    while (gpl < gpl_divides && gpl_divides % gpl) gpl++;
+    if (gpl > gpl_divides) gpl = gpl_divides;
+  }
+  g.gpl = gpl;
+  g.L = (uint32_t)((total_groups + gpl - 1) / gpl);
+  return g;
+}
+
+// walk all lanes through `gpl` groups in launches of groups_per_launch; kind = timing slot
+int run_walk(kh_ctx *c, int mode, int kind, walk_args A, uint64_t gpl, uint32_t default_gpl_launch) {
+  uint32_t per = c->groups_per_launch ? c->groups_per_launch : default_gpl_launch;
+  for (uint64_t gb = 0; gb < gpl; gb += per) {
+    A.group_base = gb;
+    A.groups = (uint32_t)std::min<uint64_t>(per, gpl - gb);
+    HIPCHK(c, hipEventRecord(c->ev_a, c->stream));
+    HIPCHK(c, launch_walk(mode, A, c->stream));
+    HIPCHK(c, hipEventRecord(c->ev_b, c->stream));
+    HIPCHK(c, hipEventSynchronize(c->ev_b));
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, c->ev_a, c->ev_b);
+    c->tm[kind].launches++;
+    c->tm[kind].ms += ms;
+    c->tm[kind].points += (uint64_t)A.L * A.groups * 2 * KH_WALK_H;
+  }
+  return KH_OK;
+}
+
+int fetch_hits(kh_ctx *c, uint32_t &n) {
+  uint32_t cnt = 0;
+  HIPCHK(c, hipMemcpyAsync(&cnt, c->d_hit_count, 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (cnt > c->hit_cap) {
+    c->err = "device hit buffer overflow";
+    return KH_E_OVERFLOW;
+  }
+  c->h_hits.resize(cnt);
+  if (cnt) {
+    HIPCHK(c, hipMemcpyAsync(c->h_hits.data(), c->d_hits, (size_t)cnt * sizeof(kh_dev_hit), hipMemcpyDeviceToHost,
+                             c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
+  n = cnt;
+  return KH_OK;
+}
+
+}  // namespace
+
+// ==============================================================================================
+// C ABI
+// ==============================================================================================
+extern "C" {
+
+int kh_abi_version(void) { return KH_ABI_VERSION; }
+
+const char *kh_strerror(int code) {
+  switch (code) {
+    case KH_OK: return "ok";
+    case KH_E_ARG: return "invalid argument";
+    case KH_E_HIP: return "HIP runtime error";
+    case KH_E_NOMEM: return "out of memory";
+    case KH_E_STATE: return "call out of order";
+    case KH_E_OVERFLOW: return "output buffer too small";
+    case KH_E_BSGS_N: return "BSGS n has no exact square root or sqrt(n) is not a multiple of 1024";
+    case KH_E_RANGE: return "the given range is small";
+    default: return "unknown error";
+  }
+}
+
+const char *kh_last_error(kh_ctx *ctx) { return ctx ? ctx->err.c_str() : "no context"; }
+
+int kh_device_count(int *count) {
+  if (!count) return KH_E_ARG;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+  *count = n;
+  return KH_OK;
+}
+
+int kh_open(int device, kh_ctx **out) {
+  if (!out) return KH_E_ARG;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return KH_E_HIP;
+  kh_ctx *c = new kh_ctx();
+  c->device = device;
+  auto fail = [&](int r) {
+    delete c;
+    return r;
+  };
+  if (hipSetDevice(device) != hipSuccess) return fail(KH_E_HIP);
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return fail(KH_E_HIP);
+  if (hipEventCreate(&c->ev_a) != hipSuccess || hipEventCreate(&c->ev_b) != hipSuccess) return fail(KH_E_HIP);
+  c->comb.build();
+  std::vector<uint32_t> h((size_t)32 * 256 * 16, 0);
+  for (int i = 0; i < 32 * 256; i++) {
+    if (i % 256 == 0) continue;
+    memcpy(&h[(size_t)i * 16], c->comb.t[i].x.d, 32);
+    memcpy(&h[(size_t)i * 16 + 8], c->comb.t[i].y.d, 32);
+  }
+  if (hipMalloc(&c->d_comb, h.size() * 4) != hipSuccess) return fail(KH_E_NOMEM);
+  if (hipMemcpy(c->d_comb, h.data(), h.size() * 4, hipMemcpyHostToDevice) != hipSuccess) return fail(KH_E_HIP);
+  if (hipMalloc(&c->d_hit_count, 4) != hipSuccess) return fail(KH_E_NOMEM);
+  if (hipMalloc(&c->d_hits, (size_t)c->hit_cap * sizeof(kh_dev_hit)) != hipSuccess) return fail(KH_E_NOMEM);
+  *out = c;
+  return KH_OK;
+}
+
+int kh_close(kh_ctx *ctx) {
+  delete ctx;
+  return KH_OK;
+}
+
+int kh_set_geometry(kh_ctx *ctx, uint32_t lanes, uint32_t groups_per_launch) {
+  if (!ctx) return KH_E_ARG;
+  ctx->lanes_max = lanes ? lanes : (1u << 18);
+  ctx->groups_per_launch = groups_per_launch;
+  return KH_OK;
+}
+
+int kh_synchronize(kh_ctx *ctx) {
+  if (!ctx) return KH_E_ARG;
+  (void)hipSetDevice(ctx->device);
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  return KH_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// address / rmd160 / xpoint
+// ---------------------------------------------------------------------------------------------
+int kh_set_targets(kh_ctx *ctx, const uint8_t *rows, uint64_t n, uint64_t bloom_items) {
+  if (!ctx || (!rows && n)) return KH_E_ARG;
+  (void)hipSetDevice(ctx->device);
+  std::vector<std::array<uint8_t, 20>> v(n);
+  for (uint64_t i = 0; i < n; i++) memcpy(v[i].data(), rows + i * 20, 20);
+  std::sort(v.begin(), v.end(), [](const std::array<uint8_t, 20> &a, const std::array<uint8_t, 20> &b) {
+    return memcmp(a.data(), b.data(), 20) < 0;
+  });
+  ctx->rows.resize(n * 20);
+  for (uint64_t i = 0; i < n; i++) memcpy(&ctx->rows[i * 20], v[i].data(), 20);
+  ctx->n_rows = n;
+  ctx->tbd = bloom_size(bloom_entries(bloom_items ? bloom_items : n));
+  ctx->h_tbloom.assign(ctx->tbd.bytes, 0);
+  for (uint64_t i = 0; i < n; i++) host_bloom_add(ctx->h_tbloom.data(), ctx->tbd, &ctx->rows[i * 20], 20);
+  (void)hipFree(ctx->d_tbloom);
+  ctx->d_tbloom = nullptr;
+  HIPCHK(ctx, hipMalloc(&ctx->d_tbloom, ctx->tbd.bytes + 4));
+  HIPCHK(ctx, hipMemcpy(ctx->d_tbloom, ctx->h_tbloom.data(), ctx->tbd.bytes, hipMemcpyHostToDevice));
+  return KH_OK;
+}
+
+int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride_be[32], uint64_t n_keys, uint32_t mode,
+            uint32_t search, kh_hit *hits, uint32_t cap, uint32_t *n_hits) {
+  if (!ctx || !start || !n_hits || (n_keys % (2 * KH_WALK_H)) || n_keys == 0) return KH_E_ARG;
+  if (mode > KH_MODE_XPOINT || search > KH_SEARCH_BOTH) return KH_E_ARG;
+  if (!ctx->d_tbloom) return KH_E_STATE;
+  (void)hipSetDevice(ctx->device);
+  const int H = KH_WALK_H;
+  u256 st = sc_reduce(u256_from_be(start));
+  u256 stride = stride_be ? sc_reduce(u256_from_be(stride_be)) : u256_u64(1);
+  if (u256_is_zero(stride)) return KH_E_ARG;
+  const uint32_t *tab = nullptr;
+  int r = get_table(ctx, stride, &tab);
+  if (r) return r;
+
+  uint64_t total_groups = n_keys / (2 * H);
+  job_geom jg = plan(ctx, total_groups, 0);
+  std::vector<u256> s(jg.L);
+  for (uint32_t g = 0; g < jg.L; g++) {
+    u128 off = (u128)g * jg.gpl * (2 * H) + H;
+    u256 o = sc_reduce(u256_from_u128(off));
+    if (u256_cmp(stride, u256_u64(1)) != 0) {
+      // o * stride mod n (o < 2^128): double-and-add over the bits of o
+      u256 acc = u256_u64(0), x = stride;
+      for (int b = 0; b < 128; b++) {
+        if ((off >> b) & 1) acc = sc_add(acc, x);
+        x = sc_add(x, x);
+      }
+      o = acc;
+    }
+    s[g] = sc_add(st, o);
+    if (u256_is_zero(s[g])) {
+      ctx->err = "lane centre scalar is 0 mod n";
+      return KH_E_ARG;
+    }
+  }
+  r = run_setup(ctx, s, nullptr);
+  if (r) return r;
+
+  int km = mode == KH_MODE_XPOINT ? KM_XPOINT
+         : search == KH_SEARCH_COMPRESS ? KM_H160C
+         : search == KH_SEARCH_UNCOMPRESS ? KM_H160U
+                                          : KM_H160B;
+  walk_args A;
+  memset(&A, 0, sizeof A);
+  A.tab = tab;
+  A.cx = ctx->d_cx;
+  A.cy = ctx->d_cy;
+  A.scratch = ctx->d_scratch;
+  A.L = jg.L;
+  A.lane_stride = jg.gpl * 2 * H;
+  A.n_points = n_keys;
+  A.bloom = ctx->d_tbloom;
+  A.bd = ctx->tbd;
+  A.hit_count = ctx->d_hit_count;
+  A.hits = ctx->d_hits;
+  A.hit_cap = ctx->hit_cap;
+  HIPCHK(ctx, hipMemsetAsync(ctx->d_hit_count, 0, 4, ctx->stream));
+  r = run_walk(ctx, km, mode == KH_MODE_XPOINT ? 1 : 0, A, jg.gpl, 2);
+  if (r) return r;
+  uint32_t nd = 0;
+  r = fetch_hits(ctx, nd);
+  if (r) return r;
+
+  // confirm each bloom hit against the sorted table and resolve the key (keyhunt.cpp:3619-3636)
+  std::vector<kh_dev_hit> dh(ctx->h_hits.begin(), ctx->h_hits.begin() + nd);
+  std::sort(dh.begin(), dh.end(), [](const kh_dev_hit &a, const kh_dev_hit &b) {
+    return a.idx != b.idx ? a.idx < b.idx : a.kind < b.kind;
+  });
+  std::vector<kh_hit> out;
+  for (auto &h : dh) {
+    u256 k = sc_add(st, sc_reduce(u256_from_u128((u128)h.idx)));
+    if (u256_cmp(stride, u256_u64(1)) != 0) {
+      u256 acc = u256_u64(0), x = stride;
+      for (int b = 0; b < 64; b++) {
+        if ((h.idx >> b) & 1) acc = sc_add(acc, x);
+        x = sc_add(x, x);
+      }
+      k = sc_add(st, acc);
+    }
+    ge P;
+    if (!ctx->comb.mult(P, k)) continue;
+    uint8_t probe[20];
+    uint32_t w[5];
+    bool compressed = false;
+    if (h.kind == KH_KIND_02 || h.kind == KH_KIND_03) {
+      hash160_comp(P.x, 2 + h.kind, w);
+      compressed = true;
+    } else if (h.kind == KH_KIND_04) {
+      hash160_uncomp(P.x, P.y, w);
+    } else {
+      for (int j = 0; j < 5; j++) w[j] = bswap32(P.x.d[7 - j]);
+    }
+    memcpy(probe, w, 20);
+    if (!searchbinary(ctx->rows.data(), (int64_t)ctx->n_rows, probe, 20, 0)) continue;
+    kh_hit o;
+    memset(&o, 0, sizeof o);
+    u256 kr = k;
+    if (compressed) {
+      uint32_t odd = P.y.d[0] & 1;
+      if (odd != (h.kind == KH_KIND_03 ? 1u : 0u)) kr = sc_neg(k);
+    }
+    u256_to_be(o.key, kr);
+    o.offset = h.idx;
+    o.kind = h.kind;
+    o.compressed = compressed ? 1 : 0;
+    out.push_back(o);
+  }
+  *n_hits = (uint32_t)out.size();
+  if (hits)
+    for (uint32_t i = 0; i < out.size() && i < cap; i++) hits[i] = out[i];
+  return out.size() > cap ? KH_E_OVERFLOW : KH_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// BSGS
+// ---------------------------------------------------------------------------------------------
+int kh_bsgs_setup(kh_ctx *ctx, uint64_t n, uint64_t k, kh_bsgs_info *info) {
+  if (!ctx || !k) return KH_E_ARG;
+  (void)hipSetDevice(ctx->device);
+  // keyhunt.cpp:1454-1661
+  uint64_t m = (uint64_t)sqrtl((long double)n);
+  while (m * m > n) m--;
+  while ((m + 1) * (m + 1) <= n) m++;
+  if (m * m != n || m % 1024) return KH_E_BSGS_N;
+  m *= k;
+  uint64_t m2 = m / 32 + (m % 32 ? 1 : 0);
+  uint64_t m3 = m2 / 32 + (m2 % 32 ? 1 : 0);
+  uint64_t aux = n / m;
+  if (n % m) n = m * aux;
+  kh_bsgs_info &I = ctx->info;
+  memset(&I, 0, sizeof I);
+  I.n = n;
+  I.m = m;
+  I.m2 = m2;
+  I.m3 = m3;
+  I.aux = aux;
+  I.cycles = aux / 1024 + (aux % 1024 ? 1 : 0);
+  uint64_t it[3];
+  it[0] = (m / 256 > 10000) ? (m / 256 + (m % 256 ? 1 : 0)) : 1000;
+  it[1] = (m2 / 256 > 1000) ? (m2 / 256 + (m2 % 256 ? 1 : 0)) : 1000;
+  it[2] = (m3 / 256 > 1000) ? (m3 / 256 + (m3 % 256 ? 1 : 0)) : 1000;
+  for (int l = 0; l < 3; l++) {
+    ctx->bd[l] = bloom_size(bloom_entries(it[l]));
+    ctx->bd[l].stride = (ctx->bd[l].bytes + 255) & ~255ULL;
+    I.bloom_bits[l] = ctx->bd[l].bits;
+    I.bloom_bytes[l] = ctx->bd[l].bytes;
+    I.bloom_hashes[l] = ctx->bd[l].hashes;
+  }
+  for (int l = 0; l < 3; l++) {
+    (void)hipFree(ctx->d_bl[l]);
+    ctx->d_bl[l] = nullptr;
+    size_t bytes = 256 * ctx->bd[l].stride + 4;
+    HIPCHK(ctx, hipMalloc(&ctx->d_bl[l], bytes));
+    HIPCHK(ctx, hipMemset(ctx->d_bl[l], 0, bytes));
+  }
+  // AMP2[i] = -(M2 + 2i*M2)G, AMP3[i] = -(M3 + 2i*M3)G  (keyhunt.cpp:1818-1842)
+  ctx->amp2.resize(32);
+  ctx->amp3.resize(32);
+  for (int i = 0; i < 32; i++) {
+    ge a;
+    ctx->comb.mult(a, u256_u64(m2 * (2 * (uint64_t)i + 1)));
+    fe_neg(a.y, a.y);
+    ctx->amp2[i] = a;
+    ctx->comb.mult(a, u256_u64(m3 * (2 * (uint64_t)i + 1)));
+    fe_neg(a.y, a.y);
+    ctx->amp3[i] = a;
+  }
+  ctx->bsgs_ready = true;
+  ctx->bsgs_built = false;
+  ctx->candidates = 0;
+  if (info) *info = I;
+  return KH_OK;
+}
+
+int kh_bsgs_build(kh_ctx *ctx) {
+  if (!ctx) return KH_E_ARG;
+  if (!ctx->bsgs_ready) return KH_E_STATE;
+  (void)hipSetDevice(ctx->device);
+  const int H = KH_WALK_H;
+  const kh_bsgs_info &I = ctx->info;
+  const uint32_t *tab = nullptr;
+  int r = get_table(ctx, u256_u64(1), &tab);
+  if (r) return r;
+  uint64_t total_groups = (I.m + 2 * H - 1) / (2 * H);
+  job_geom jg = plan(ctx, total_groups, 0);
+  std::vector<u256> s(jg.L);
+  for (uint32_t g = 0; g < jg.L; g++) s[g] = u256_u64(1 + (uint64_t)g * jg.gpl * 2 * H + H);  // baby i <-> key i+1
+  r = run_setup(ctx, s, nullptr);
+  if (r) return r;
+  uint64_t *d_key = nullptr;
+  uint32_t *d_val = nullptr;
+  HIPCHK(ctx, hipMalloc(&d_key, I.m3 * 8));
+  HIPCHK(ctx, hipMalloc(&d_val, I.m3 * 4));
+  walk_args A;
+  memset(&A, 0, sizeof A);
+  A.tab = tab;
+  A.cx = ctx->d_cx;
+  A.cy = ctx->d_cy;
+  A.scratch = ctx->d_scratch;
+  A.L = jg.L;
+  A.lane_stride = jg.gpl * 2 * H;
+  A.n_points = I.m;
+  A.bl1 = ctx->d_bl[0];
+  A.bl2 = ctx->d_bl[1];
+  A.bl3 = ctx->d_bl[2];
+  A.bd = ctx->bd[0];
+  A.bd2 = ctx->bd[1];
+  A.bd3 = ctx->bd[2];
+  A.m2 = I.m2;
+  A.m3 = I.m3;
+  A.rows_key = d_key;
+  A.rows_val = d_val;
+  r = run_walk(ctx, KM_BUILD, 3, A, jg.gpl, 4);
+  if (r) {
+    (void)hipFree(d_key);
+    (void)hipFree(d_val);
+    return r;
+  }
+  // bsgs_sort (keyhunt.cpp:4412-4508): order rows by the 6 value bytes (ties by index)
+  std::vector<uint64_t> keys(I.m3);
+  std::vector<uint32_t> vals(I.m3);
+  HIPCHK(ctx, hipMemcpy(keys.data(), d_key, I.m3 * 8, hipMemcpyDeviceToHost));
+  HIPCHK(ctx, hipMemcpy(vals.data(), d_val, I.m3 * 4, hipMemcpyDeviceToHost));
+  (void)hipFree(d_key);
+  (void)hipFree(d_val);
+  std::vector<uint64_t> order(I.m3);
+  for (uint64_t i = 0; i < I.m3; i++) order[i] = i;
+  std::sort(order.begin(), order.end(), [&](uint64_t a, uint64_t b) {
+    return keys[a] != keys[b] ? keys[a] < keys[b] : vals[a] < vals[b];
+  });
+  ctx->h_rows.assign(I.m3 * 16, 0);
+  for (uint64_t i = 0; i < I.m3; i++) {
+    uint64_t kk = keys[order[i]];
+    uint8_t *row = &ctx->h_rows[i * 16];
+    for (int b = 0; b < 6; b++) row[b] = (uint8_t)(kk >> (40 - 8 * b));
+    uint64_t idx = vals[order[i]];
+    memcpy(row + 8, &idx, 8);
+  }
+  // layers 2 and 3 on the host for the refinement steps
+  for (int l = 1; l < 3; l++) {
+    ctx->h_bl[l].resize(256 * ctx->bd[l].stride);
+    HIPCHK(ctx, hipMemcpy(ctx->h_bl[l].data(), ctx->d_bl[l], ctx->h_bl[l].size(), hipMemcpyDeviceToHost));
+  }
+  ctx->bsgs_built = true;
+  return KH_OK;
+}
+
+int kh_bsgs_set_targets(kh_ctx *ctx, const uint8_t *xy, uint32_t n) {
+  if (!ctx || (!xy && n)) return KH_E_ARG;
+  ctx->targets.resize(n);
+  for (uint32_t i = 0; i < n; i++) {
+    fe_from_be(ctx->targets[i].x, xy + 64 * i);
+    fe_from_be(ctx->targets[i].y, xy + 64 * i + 32);
+  }
+  ctx->found.assign(n, 0);
+  return KH_OK;
+}
+
+int kh_bsgs_reset_found(kh_ctx *ctx) {
+  if (!ctx) return KH_E_ARG;
+  std::fill(ctx->found.begin(), ctx->found.end(), 0);
+  return KH_OK;
+}
+
+int kh_bsgs_candidates(kh_ctx *ctx, uint64_t *count) {
+  if (!ctx || !count) return KH_E_ARG;
+  *count = ctx->candidates;
+  return KH_OK;
+}
+
+namespace {
+
+bool rows_search(const kh_ctx *c, const uint8_t x32[32], uint64_t &idx) {
+  // bsgs_searchbinary (keyhunt.cpp:4510-4544), no bucket cache
+  const uint8_t *rows = c->h_rows.data();
+  int64_t n = (int64_t)c->info.m3, min = 0, max = n, cur = 0, half = n;
+  while (half >= 1) {
+    half = (max - min) / 2;
+    const uint8_t *row = rows + (cur + half) * 16;
+    int cmp = memcmp(x32 + 16, row, 6);
+    if (cmp == 0) {
+      memcpy(&idx, row + 8, 8);
+      return true;
+    }
+    if (cmp < 0)
+      max = max - half;
+    else
+      min = min + half;
+    cur = min;
+  }
+  return false;
+}
+
+// S + A[i] for i < 32, X only, one batched inversion.  AddDirect with dx == 0 yields
+// x = -S.x - A.x in the reference (inverse of 0 is 0); reproduced.
+void add32_x(const ge &S, const std::vector<ge> &A, fe out[32]) {
+  std::vector<fe> dx(32);
+  for (int i = 0; i < 32; i++) fe_sub(dx[i], A[i].x, S.x);
+  batch_inv(dx);
+  for (int i = 0; i < 32; i++) {
+    fe dy, s, x;
+    fe_sub(dy, A[i].y, S.y);
+    fe_mul(s, dy, dx[i]);
+    fe_sqr(x, s);
+    fe_sub(x, x, S.x);
+    fe_sub(x, x, A[i].x);
+    out[i] = x;
+  }
+}
+
+// bsgs_thirdcheck (keyhunt.cpp:5186-5248)
+bool third_check(const kh_ctx *c, const u256 &base_key, uint32_t a, const ge &Q, u256 &key) {
+  const kh_bsgs_info &I = c->info;
+  u256 base3 = sc_add(base_key, sc_reduce(u256_from_u128((u128)a * 2 * I.m2)));
+  ge bp;
+  if (!c->comb.mult(bp, base3)) return false;
+  fe_neg(bp.y, bp.y);
+  ge S;
+  ge_add(S, Q, bp);
+  fe xs[32];
+  add32_x(S, c->amp3, xs);
+  for (int i = 0; i < 32; i++) {
+    uint8_t xr[32];
+    fe_to_be(xr, xs[i]);
+    u256 calc = u256_u64(i == 0 ? I.m3 : (uint64_t)i * 2 * I.m3 + I.m3);
+    if (host_bloom_check(c->h_bl[2].data() + (size_t)xr[0] * c->bd[2].stride, c->bd[2], xr, 32)) {
+      uint64_t j;
+      if (rows_search(c, xr, j)) {
+        for (int sgn = 0; sgn < 2; sgn++) {
+          u256 jj = u256_u64(j + 1);
+          u256 k = sgn == 0 ? sc_add(calc, jj) : sc_sub(calc, jj);
+          k = sc_add(k, base3);
+          ge chk;
+          if (c->comb.mult(chk, k) && fe_eq(chk.x, Q.x)) {
+            key = k;
+            return true;
+          }
+        }
+      }
+    } else if (fe_eq(S.x, c->amp3[i].x)) {
+      key = sc_add(calc, base3);
+      return true;
+    }
+  }
+  return false;
+}
+
+// bsgs_secondcheck (keyhunt.cpp:5151-5184)
+bool second_check(const kh_ctx *c, const u256 &base, uint64_t a, const ge &Q, u256 &key) {
+  const kh_bsgs_info &I = c->info;
+  u256 base_key = sc_add(base, sc_reduce(u256_from_u128((u128)a * 2 * I.m)));
+  ge bp;
+  if (!c->comb.mult(bp, base_key)) return false;
+  fe_neg(bp.y, bp.y);
+  ge S;
+  ge_add(S, Q, bp);
+  fe xs[32];
+  add32_x(S, c->amp2, xs);
+  for (int i = 0; i < 32; i++) {
+    uint8_t xr[32];
+    fe_to_be(xr, xs[i]);
+    if (host_bloom_check(c->h_bl[1].data() + (size_t)xr[0] * c->bd[1].stride, c->bd[1], xr, 32))
+      if (third_check(c, base_key, (uint32_t)i, Q, key)) return true;
+  }
+  return false;
+}
+
+}  // namespace
+
+int kh_bsgs_scan(kh_ctx *ctx, const uint8_t start[32], uint64_t n_bases, kh_bsgs_found *found, uint32_t cap,
+                 uint32_t *n_found) {
+  if (!ctx || !start || !n_found) return KH_E_ARG;
+  if (!ctx->bsgs_built) return KH_E_STATE;
+  (void)hipSetDevice(ctx->device);
+  *n_found = 0;
+  const int H = KH_WALK_H;
+  const kh_bsgs_info &I = ctx->info;
+  const uint64_t A_pts = I.cycles * 1024;  // giant points walked per base (cycles x 1024)
+  u256 st = sc_reduce(u256_from_be(start));
+  // GSn[i] = -(i+1)*2M*G  (keyhunt.cpp:1797-1816)
+  const uint32_t *tab = nullptr;
+  int r = get_table(ctx, sc_neg(u256_u64(2 * I.m)), &tab);
+  if (r) return r;
+  uint32_t nf = 0;
+  int rc = KH_OK;
+  for (uint32_t tgt = 0; tgt < ctx->targets.size(); tgt++) {
+    if (ctx->found[tgt]) continue;
+    const ge &Q = ctx->targets[tgt];
+    // giant points of this call: t in [0, n_bases*A); t -> base b = t / A, a = t % A.
+    // A lane's run of gpl groups never crosses a base: gpl divides `cycles`.
+    uint64_t total_groups = n_bases * I.cycles;
+    bool done = false;
+    uint64_t g0 = 0;  // first group of this round
+    while (g0 < total_groups && !done) {
+      uint64_t round_groups = std::min<uint64_t>(total_groups - g0, (uint64_t)ctx->lanes_max * I.cycles);
+      job_geom jg = plan(ctx, round_groups, I.cycles);
+      uint64_t t_round = g0 * 2 * H;
+      std::vector<u256> s(jg.L);
+      for (uint32_t g = 0; g < jg.L; g++) {
+        uint64_t t0 = t_round + (uint64_t)g * jg.gpl * 2 * H;
+        uint64_t b = t0 / A_pts, a0 = t0 % A_pts;
+        // centre key: base_b + M + 2M*(a0 + H); lane centre = Q - key*G
+        u256 kb = sc_add(st, sc_reduce(u256_from_u128((u128)b * 2 * I.n)));
+        kb = sc_add(kb, sc_reduce(u256_from_u128((u128)I.m + (u128)2 * I.m * (a0 + H))));
+        s[g] = sc_neg(kb);
+      }
+      r = run_setup(ctx, s, &Q);
+      if (r) return r;
+      walk_args Aw;
+      memset(&Aw, 0, sizeof Aw);
+      Aw.tab = tab;
+      Aw.cx = ctx->d_cx;
+      Aw.cy = ctx->d_cy;
+      Aw.scratch = ctx->d_scratch;
+      Aw.L = jg.L;
+      Aw.lane_stride = jg.gpl * 2 * H;
+      Aw.n_points = round_groups * 2 * H;
+      Aw.bloom = ctx->d_bl[0];
+      Aw.bd = ctx->bd[0];
+      Aw.hit_count = ctx->d_hit_count;
+      Aw.hits = ctx->d_hits;
+      Aw.hit_cap = ctx->hit_cap;
+      HIPCHK(ctx, hipMemsetAsync(ctx->d_hit_count, 0, 4, ctx->stream));
+      r = run_walk(ctx, KM_BSGS, 2, Aw, jg.gpl, 8);
+      if (r) return r;
+      uint32_t nd = 0;
+      r = fetch_hits(ctx, nd);
+      if (r) return r;
+      std::vector<kh_dev_hit> dh(ctx->h_hits.begin(), ctx->h_hits.begin() + nd);
+      std::sort(dh.begin(), dh.end(), [](const kh_dev_hit &x, const kh_dev_hit &y) { return x.idx < y.idx; });
+      ctx->candidates += nd;
+      for (auto &h : dh) {
+        uint64_t t = t_round + h.idx;
+        uint64_t b = t / A_pts, a = t % A_pts;
+        u256 base = sc_add(st, sc_reduce(u256_from_u128((u128)b * 2 * I.n)));
+        u256 key;
+        if (second_check(ctx, base, a, Q, key)) {
+          ctx->found[tgt] = 1;
+          if (found && nf < cap) {
+            found[nf].target = tgt;
+            found[nf].pad = 0;
+            u256_to_be(found[nf].key, key);
+          }
+          nf++;
+          done = true;
+          break;
+        }
+      }
+      g0 += round_groups;
+    }
+  }
+  *n_found = nf;
+  return nf > cap ? KH_E_OVERFLOW : rc;
+}
+
+// ---------------------------------------------------------------------------------------------
+// measurement
+// ---------------------------------------------------------------------------------------------
+int kh_kernel_time(kh_ctx *ctx, uint32_t kind, uint64_t *launches, double *ms, uint64_t *points) {
+  if (!ctx || kind > 4) return KH_E_ARG;
+  if (launches) *launches = ctx->tm[kind].launches;
+  if (ms) *ms = ctx->tm[kind].ms;
+  if (points) *points = ctx->tm[kind].points;
+  return KH_OK;
+}
+
+int kh_kernel_time_reset(kh_ctx *ctx) {
+  if (!ctx) return KH_E_ARG;
+  for (auto &t : ctx->tm) t = timing();
+  return KH_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// parity hooks
+// ---------------------------------------------------------------------------------------------
+int kh_pubkeys(kh_ctx *ctx, const uint8_t *scalars, uint32_t n, uint8_t *xy) {
+  if (!ctx || !scalars || !xy || !n) return KH_E_ARG;
+  (void)hipSetDevice(ctx->device);
+  std::vector<u256> s(n);
+  for (uint32_t i = 0; i < n; i++) {
+    s[i] = sc_reduce(u256_from_be(scalars + 32 * i));
+    if (u256_is_zero(s[i])) return KH_E_ARG;
+  }
+  int r = run_setup(ctx, s, nullptr);
+  if (r) return r;
+  std::vector<uint32_t> cx((size_t)n * 8), cy((size_t)n * 8);
+  for (int w = 0; w < 8; w++) {
+    HIPCHK(ctx, hipMemcpy(&cx[(size_t)w * n], ctx->d_cx + (size_t)w * n, (size_t)n * 4, hipMemcpyDeviceToHost));
+    HIPCHK(ctx, hipMemcpy(&cy[(size_t)w * n], ctx->d_cy + (size_t)w * n, (size_t)n * 4, hipMemcpyDeviceToHost));
+  }
+  for (uint32_t i = 0; i < n; i++) {
+    fe x, y;
+    for (int w = 0; w < 8; w++) {
+      x.d[w] = cx[(size_t)w * n + i];
+      y.d[w] = cy[(size_t)w * n + i];
+    }
+    fe_to_be(xy + 64 * i, x);
+    fe_to_be(xy + 64 * i + 32, y);
+  }
+  return KH_OK;
+}
+
+int kh_walk_points(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride_be[32], uint64_t n_points,
+                   uint8_t *out_x, uint8_t *out_y) {
+  if (!ctx || !start || !out_x || !n_points || n_points % (2 * KH_WALK_H)) return KH_E_ARG;
+  (void)hipSetDevice(ctx->device);
+  const int H = KH_WALK_H;
+  u256 st = sc_reduce(u256_from_be(start));
+  u256 stride = stride_be ? sc_reduce(u256_from_be(stride_be)) : u256_u64(1);
+  const uint32_t *tab = nullptr;
+  int r = get_table(ctx, stride, &tab);
+  if (r) return r;
+  job_geom jg = plan(ctx, n_points / (2 * H), 0);
+  std::vector<u256> s(jg.L);
+  for (uint32_t g = 0; g < jg.L; g++) {
+    u128 off = (u128)g * jg.gpl * 2 * H + H;
+    u256 acc = u256_u64(0), x = stride;
+    for (int b = 0; b < 128; b++) {
+      if ((off >> b) & 1) acc = sc_add(acc, x);
+      x = sc_add(x, x);
+    }
+    s[g] = sc_add(st, acc);
+  }
+  r = run_setup(ctx, s, nullptr);
+  if (r) return r;
+  uint32_t *dx = nullptr, *dy = nullptr;
+  HIPCHK(ctx, hipMalloc(&dx, n_points * 32));
+  if (out_y) HIPCHK(ctx, hipMalloc(&dy, n_points * 32));
+  walk_args A;
+  memset(&A, 0, sizeof A);
+  A.tab = tab;
+  A.cx = ctx->d_cx;
+  A.cy = ctx->d_cy;
+  A.scratch = ctx->d_scratch;
+  A.L = jg.L;
+  A.lane_stride = jg.gpl * 2 * H;
+  A.n_points = n_points;
+  A.dump_x = dx;
+  A.dump_y = dy;
+  r = run_walk(ctx, KM_DUMP, 0, A, jg.gpl, 4);
+  if (r) {
+    (void)hipFree(dx);
+    (void)hipFree(dy);
+    return r;
+  }
+  std::vector<uint32_t> hx(n_points * 8), hy(out_y ? n_points * 8 : 0);
+  HIPCHK(ctx, hipMemcpy(hx.data(), dx, n_points * 32, hipMemcpyDeviceToHost));
+  if (out_y) HIPCHK(ctx, hipMemcpy(hy.data(), dy, n_points * 32, hipMemcpyDeviceToHost));
+  (void)hipFree(dx);
+  (void)hipFree(dy);
+  for (uint64_t i = 0; i < n_points; i++) {
+    fe x;
+    memcpy(x.d, &hx[i * 8], 32);
+    fe_to_be(out_x + 32 * i, x);
+    if (out_y) {
+      fe y;
+      memcpy(y.d, &hy[i * 8], 32);
+      fe_to_be(out_y + 32 * i, y);
+    }
+  }
+  return KH_OK;
+}
+
+int kh_hash160(kh_ctx *ctx, const uint8_t *xy, uint32_t n, uint8_t *out60) {
+  if (!ctx || !xy || !out60 || !n) return KH_E_ARG;
+  (void)hipSetDevice(ctx->device);
+  std::vector<uint32_t> hx((size_t)n * 8), hy((size_t)n * 8), ho((size_t)n * 15);
+  for (uint32_t i = 0; i < n; i++) {
+    fe x, y;
+    fe_from_be(x, xy + 64 * i);
+    fe_from_be(y, xy + 64 * i + 32);
+    memcpy(&hx[(size_t)i * 8], x.d, 32);
+    memcpy(&hy[(size_t)i * 8], y.d, 32);
+  }
+  uint32_t *dx, *dy, *dout;
+  HIPCHK(ctx, hipMalloc(&dx, hx.size() * 4));
+  HIPCHK(ctx, hipMalloc(&dy, hy.size() * 4));
+  HIPCHK(ctx, hipMalloc(&dout, ho.size() * 4));
+  HIPCHK(ctx, hipMemcpy(dx, hx.data(), hx.size() * 4, hipMemcpyHostToDevice));
+  HIPCHK(ctx, hipMemcpy(dy, hy.data(), hy.size() * 4, hipMemcpyHostToDevice));
+  HIPCHK(ctx, launch_test_hash160(dx, dy, n, dout, ctx->stream));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  HIPCHK(ctx, hipMemcpy(ho.data(), dout, ho.size() * 4, hipMemcpyDeviceToHost));
+  (void)hipFree(dx);
+  (void)hipFree(dy);
+  (void)hipFree(dout);
+  memcpy(out60, ho.data(), (size_t)n * 60);
+  return KH_OK;
+}
+
+int kh_field_ops(kh_ctx *ctx, const uint8_t *a, const uint8_t *b, uint32_t n, uint8_t *out160) {
+  if (!ctx || !a || !b || !out160 || !n) return KH_E_ARG;
+  (void)hipSetDevice(ctx->device);
+  std::vector<uint32_t> ha((size_t)n * 8), hb((size_t)n * 8), ho((size_t)n * 40);
+  for (uint32_t i = 0; i < n; i++) {
+    fe x, y;
+    fe_from_be(x, a + 32 * i);
+    fe_from_be(y, b + 32 * i);
+    memcpy(&ha[(size_t)i * 8], x.d, 32);
+    memcpy(&hb[(size_t)i * 8], y.d, 32);
+  }
+  uint32_t *da, *db, *dout;
+  HIPCHK(ctx, hipMalloc(&da, ha.size() * 4));
+  HIPCHK(ctx, hipMalloc(&db, hb.size() * 4));
+  HIPCHK(ctx, hipMalloc(&dout, ho.size() * 4));
+  HIPCHK(ctx, hipMemcpy(da, ha.data(), ha.size() * 4, hipMemcpyHostToDevice));
+  HIPCHK(ctx, hipMemcpy(db, hb.data(), hb.size() * 4, hipMemcpyHostToDevice));
+  HIPCHK(ctx, launch_test_field(da, db, n, dout, ctx->stream));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  HIPCHK(ctx, hipMemcpy(ho.data(), dout, ho.size() * 4, hipMemcpyDeviceToHost));
+  (void)hipFree(da);
+  (void)hipFree(db);
+  (void)hipFree(dout);
+  for (uint32_t i = 0; i < n; i++)
+    for (int k = 0; k < 5; k++) {
+      fe r;
+      memcpy(r.d, &ho[(size_t)i * 40 + 8 * k], 32);
+      fe_to_be(out160 + 160 * i + 32 * k, r);
+    }
+  return KH_OK;
+}
+
+int kh_bloom_check(kh_ctx *ctx, uint32_t layer, const uint8_t *items, uint32_t n, uint32_t len, uint8_t *out) {
+  if (!ctx || !items || !out || !n || (len != 20 && len != 32) || layer > 3) return KH_E_ARG;
+  (void)hipSetDevice(ctx->device);
+  const uint8_t *bl;
+  bloom_desc d;
+  if (layer == 0) {
+    if (!ctx->d_tbloom) return KH_E_STATE;
+    bl = ctx->d_tbloom;
+    d = ctx->tbd;
+  } else {
+    if (!ctx->bsgs_ready) return KH_E_STATE;
+    bl = ctx->d_bl[layer - 1];
+    d = ctx->bd[layer - 1];
+  }
+  uint8_t *ditems;
+  uint32_t *dout;
+  HIPCHK(ctx, hipMalloc(&ditems, (size_t)n * len));
+  HIPCHK(ctx, hipMalloc(&dout, (size_t)n * 4));
+  HIPCHK(ctx, hipMemcpy(ditems, items, (size_t)n * len, hipMemcpyHostToDevice));
+  HIPCHK(ctx, launch_test_bloom(ditems, n, len, bl, d, layer ? 1 : 0, dout, ctx->stream));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  std::vector<uint32_t> ho(n);
+  HIPCHK(ctx, hipMemcpy(ho.data(), dout, (size_t)n * 4, hipMemcpyDeviceToHost));
+  (void)hipFree(ditems);
+  (void)hipFree(dout);
+  for (uint32_t i = 0; i < n; i++) out[i] = (uint8_t)ho[i];
+  return KH_OK;
+}
+
+int kh_get_bloom(kh_ctx *ctx, uint32_t layer, uint8_t *buf, uint64_t cap, uint64_t *bytes) {
+  if (!ctx || layer > 3 || !bytes) return KH_E_ARG;
+  (void)hipSetDevice(ctx->device);
+  if (layer == 0) {
+    if (!ctx->d_tbloom) return KH_E_STATE;
+    *bytes = ctx->tbd.bytes;
+    if (!buf) return KH_OK;
+    if (cap < ctx->tbd.bytes) return KH_E_OVERFLOW;
+    HIPCHK(ctx, hipMemcpy(buf, ctx->d_tbloom, ctx->tbd.bytes, hipMemcpyDeviceToHost));
+    return KH_OK;
+  }
+  if (!ctx->bsgs_ready) return KH_E_STATE;
+  const bloom_desc &d = ctx->bd[layer - 1];
+  *bytes = 256 * d.bytes;
+  if (!buf) return KH_OK;
+  if (cap < 256 * d.bytes) return KH_E_OVERFLOW;
+  HIPCHK(ctx, hipMemcpy2D(buf, d.bytes, ctx->d_bl[layer - 1], d.stride, d.bytes, 256, hipMemcpyDeviceToHost));
+  return KH_OK;
+}
+
+int kh_get_bsgs_table(kh_ctx *ctx, uint8_t *buf, uint64_t cap_rows, uint64_t *rows) {
+  if (!ctx || !rows) return KH_E_ARG;
+  if (!ctx->bsgs_built) return KH_E_STATE;
+  *rows = ctx->info.m3;
+  if (!buf) return KH_OK;
+  if (cap_rows < ctx->info.m3) return KH_E_OVERFLOW;
+  memcpy(buf, ctx->h_rows.data(), ctx->h_rows.size());
+  return KH_OK;
+}
+
+}  // extern "C"

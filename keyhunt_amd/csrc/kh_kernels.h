@@ -1,0 +1,72 @@
+// kh_kernels.h -- kernel argument blocks and launch helpers shared by kh_kernels.hip and the
+// C-ABI implementation (kh_capi.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "kh_math.h"
+
+// Group half-size H: a group is 2H points around one centre (the reference uses 512,
+// keyhunt.cpp:299 CPU_GRP_SIZE/2).  Scratch per lane = H * 32 bytes.
+#ifndef KH_WALK_H
+#define KH_WALK_H 512
+#endif
+
+enum kh_walk_mode {
+  KM_H160C = 0,   // hash160(02||X), hash160(03||X)          -l compress
+  KM_H160U = 1,   // hash160(04||X||Y)                       -l uncompress
+  KM_H160B = 2,   // both                                    -l both (default)
+  KM_XPOINT = 3,  // X[0..20)                                -m xpoint
+  KM_BSGS = 4,    // 32-byte X into the 256-shard layer-1 bloom
+  KM_BUILD = 5,   // BSGS baby-step table build
+  KM_DUMP = 6,    // X/Y dump (parity tests)
+};
+
+struct kh_dev_hit {
+  uint64_t idx;   // point index within the job
+  uint32_t kind;  // 0: 02||X, 1: 03||X, 2: 04||X||Y, 3: xpoint, 4: bsgs candidate
+  uint32_t aux;
+};
+
+struct walk_args {
+  const uint32_t *tab;   // (H+1) entries of {x[8], y[8]} (LE u32 limbs)
+  uint32_t *cx, *cy;     // lane centres, SoA: word w of lane g at [w*L + g]
+  uint4 *scratch;        // H * L * 32 bytes
+  uint32_t L;            // lanes
+  uint32_t groups;       // groups per lane in this launch
+  uint64_t lane_stride;  // points per lane in the job
+  uint64_t group_base;   // groups each lane already walked in this job
+  uint64_t n_points;     // points in the job (indices >= n_points are not probed)
+  // probe target (target bloom, or BSGS layer 1 / build layer 1)
+  const uint8_t *bloom;
+  kh::bloom_desc bd;
+  uint32_t *hit_count;
+  kh_dev_hit *hits;
+  uint32_t hit_cap;
+  uint32_t pad0;
+  // BSGS build
+  uint8_t *bl1, *bl2, *bl3;
+  kh::bloom_desc bd2, bd3;
+  uint64_t m2, m3;
+  uint64_t *rows_key;
+  uint32_t *rows_val;
+  // dump
+  uint32_t *dump_x, *dump_y;
+};
+
+struct setup_args {
+  const uint32_t *scalars;  // L x 8 LE u32 limbs
+  const uint32_t *comb;     // 32 x 256 x 16 words
+  const uint32_t *q;        // optional point added to every lane: {x[8], y[8]}
+  uint32_t has_q;
+  uint32_t L;
+  uint32_t *cx, *cy;
+};
+
+namespace kh {
+hipError_t launch_walk(int mode, const walk_args &A, hipStream_t st);
+hipError_t launch_setup(const setup_args &A, hipStream_t st);
+hipError_t launch_test_hash160(const uint32_t *xs, const uint32_t *ys, uint32_t n, uint32_t *out, hipStream_t st);
+hipError_t launch_test_field(const uint32_t *a, const uint32_t *b, uint32_t n, uint32_t *out, hipStream_t st);
+hipError_t launch_test_bloom(const uint8_t *items, uint32_t n, uint32_t len, const uint8_t *bloom,
+                             const bloom_desc &bd, uint32_t sharded, uint32_t *out, hipStream_t st);
+}  // namespace kh

@@ -1,0 +1,426 @@
+// kh_kernels.hip -- CDNA4 (gfx950) kernels for keyhunt's hot path.
+//
+// One walk kernel serves every mode.  A LANE owns a contiguous run of points on an arithmetic
+// progression P(t) = P0 + t*D (address family: D = stride*G, t = key offset; BSGS giant steps:
+// D = -2M*G, t = giant index; BSGS baby build: D = G, t = baby index).  Per GROUP the lane sits on
+// a centre C and emits the 2H points C + o*D, o in [-H, H-1]: C itself, C +- T[i] (T[i] = (i+1)*D,
+// i < H-1) and C - T[H-1]; then C += T[H] (= 2H*D).  The H+1 differences T[i].x - C.x are inverted
+// together with one Fermat inversion (Montgomery trick, secp256k1/IntGroup.cpp:36-58) whose prefix
+// products live in a per-lane HBM scratch pad ([i][lane][32 B], coalesced 2 KB per wave-access).
+// This is the reference's group geometry (keyhunt.cpp:3349-3461, 4644-4716, 5318-5393) with the
+// group's delta table T read through the scalar cache: i is wave-uniform, so every lane of a wave
+// reads the same T[i] (s_load into SGPRs, no VGPRs and no LDS bank traffic for the table).
+//
+// Why per-lane batching rather than a cross-lane product tree: on a SIMD machine an inversion
+// executed by a wave costs the same whether it serves 1 lane's batch or 64 lanes' batches, so a
+// lane's share of inversion work is I / (elements per lane per inversion) either way; a wave-wide
+// prefix/suffix tree only adds 12+ multiplications per lane.  The lever is elements per lane per
+// inversion (H = 512 here: 0.26 field-mul-equivalents per point), which needs the HBM pad.
+//
+// Probe modes (template MODE):
+//   KM_H160C / KM_H160U / KM_H160B  hash160 of 02/03||X, 04||X||Y or both -> 20-byte target bloom
+//                                    (thread_process, keyhunt.cpp:3475-3830)
+//   KM_XPOINT                        X[0..20) -> target bloom (keyhunt.cpp:3801-3824)
+//   KM_BSGS                          32-byte X -> bloom_bP[X[0]] (keyhunt.cpp:4819-4822)
+//   KM_BUILD                         baby X -> bloom layers 1/2/3 + bP rows (keyhunt.cpp:5394-5443)
+//   KM_DUMP                          write X (and Y) -- parity tests only
+#include <hip/hip_runtime.h>
+#include "kh_math.h"
+#include "kh_kernels.h"
+
+using namespace kh;
+
+namespace {
+
+__device__ __forceinline__ void load_fe(fe &r, const uint32_t *__restrict__ p) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.d[i] = p[i];
+}
+// Read-only tables indexed wave-uniformly (the walk's delta table) are accessed through the
+// constant address space so that uniform reads become s_load_dwordx8 into SGPRs.
+typedef const __attribute__((address_space(4))) uint32_t *kconst_ptr;
+__device__ __forceinline__ void load_fe_k(fe &r, kconst_ptr p) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.d[i] = p[i];
+}
+// SoA centre arrays: word w of lane g at base[w * L + g]
+__device__ __forceinline__ void load_soa(fe &r, const uint32_t *__restrict__ base, uint32_t L, uint32_t g) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.d[i] = base[(size_t)i * L + g];
+}
+__device__ __forceinline__ void store_soa(uint32_t *__restrict__ base, uint32_t L, uint32_t g, const fe &r) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) base[(size_t)i * L + g] = r.d[i];
+}
+__device__ __forceinline__ void scr_store(uint4 *__restrict__ scr, size_t slot, const fe &a) {
+  scr[2 * slot] = make_uint4(a.d[0], a.d[1], a.d[2], a.d[3]);
+  scr[2 * slot + 1] = make_uint4(a.d[4], a.d[5], a.d[6], a.d[7]);
+}
+__device__ __forceinline__ void scr_load(fe &a, const uint4 *__restrict__ scr, size_t slot) {
+  uint4 u = scr[2 * slot], v = scr[2 * slot + 1];
+  a.d[0] = u.x; a.d[1] = u.y; a.d[2] = u.z; a.d[3] = u.w;
+  a.d[4] = v.x; a.d[5] = v.y; a.d[6] = v.z; a.d[7] = v.w;
+}
+
+// bloom_check (bloom/bloom.cpp:189-212) on one filter at `bf`
+__device__ __forceinline__ bool bloom_probe(const uint8_t *__restrict__ bf, const bloom_desc &bd, uint64_t a,
+                                            uint64_t b) {
+  uint64_t h = a;
+  for (uint32_t i = 0; i < bd.hashes; i++) {
+    uint64_t x = mod_bits(h, bd.bits, bd.recip);
+    if (!((bf[x >> 3] >> (x & 7)) & 1)) return false;
+    h += b;
+  }
+  return true;
+}
+// bloom_add (bloom/bloom.cpp:122-146, add=1): set every bit with a 32-bit atomic OR
+__device__ __forceinline__ void bloom_insert(uint8_t *__restrict__ bf_base, uint64_t shard_off,
+                                             const bloom_desc &bd, uint64_t a, uint64_t b) {
+  uint64_t h = a;
+  uint32_t *w = reinterpret_cast<uint32_t *>(bf_base);
+  for (uint32_t i = 0; i < bd.hashes; i++) {
+    uint64_t x = mod_bits(h, bd.bits, bd.recip);
+    uint64_t byte = shard_off + (x >> 3);
+    atomicOr(&w[byte >> 2], 1u << ((uint32_t)((byte & 3) * 8) + (uint32_t)(x & 7)));
+    h += b;
+  }
+}
+
+__device__ __forceinline__ void record_hit(const walk_args &A, uint64_t idx, uint32_t kind) {
+  uint32_t slot = atomicAdd(A.hit_count, 1u);
+  if (slot < A.hit_cap) {
+    A.hits[slot].idx = idx;
+    A.hits[slot].kind = kind;
+    A.hits[slot].aux = 0;
+  }
+}
+
+// X as the 4 little-endian u64 words of its 32 big-endian bytes (Int::Get32Bytes order)
+__device__ __forceinline__ void x_bytes_u64(const fe &x, uint64_t in[4]) {
+#pragma unroll
+  for (int k = 0; k < 4; k++)
+    in[k] = (uint64_t)bswap32(x.d[7 - 2 * k]) | ((uint64_t)bswap32(x.d[6 - 2 * k]) << 32);
+}
+
+template <int MODE>
+__device__ __forceinline__ void probe_point(const walk_args &A, const fe &x, const fe &y, uint64_t idx) {
+  if (idx >= A.n_points) return;
+  if constexpr (MODE == KM_H160C || MODE == KM_H160B) {
+#pragma unroll 1
+    for (uint32_t pfx = 2; pfx <= 3; pfx++) {
+      uint32_t h[5];
+      hash160_comp(x, pfx, h);
+      uint64_t a = xxh64_20(h, KH_BLOOM_SEED);
+      uint64_t b = xxh64_20(h, a);
+      if (bloom_probe(A.bloom, A.bd, a, b)) record_hit(A, idx, pfx - 2);
+    }
+  }
+  if constexpr (MODE == KM_H160U || MODE == KM_H160B) {
+    uint32_t h[5];
+    hash160_uncomp(x, y, h);
+    uint64_t a = xxh64_20(h, KH_BLOOM_SEED);
+    uint64_t b = xxh64_20(h, a);
+    if (bloom_probe(A.bloom, A.bd, a, b)) record_hit(A, idx, 2);
+  }
+  if constexpr (MODE == KM_XPOINT) {
+    uint32_t w[5];
+#pragma unroll
+    for (int j = 0; j < 5; j++) w[j] = bswap32(x.d[7 - j]);
+    uint64_t a = xxh64_20(w, KH_BLOOM_SEED);
+    uint64_t b = xxh64_20(w, a);
+    if (bloom_probe(A.bloom, A.bd, a, b)) record_hit(A, idx, 3);
+  }
+  if constexpr (MODE == KM_BSGS) {
+    uint64_t in[4];
+    x_bytes_u64(x, in);
+    uint64_t a = xxh64_32(in, KH_BLOOM_SEED);
+    uint64_t b = xxh64_32(in, a);
+    const uint8_t *bf = A.bloom + (size_t)(x.d[7] >> 24) * A.bd.stride;
+    if (bloom_probe(bf, A.bd, a, b)) record_hit(A, idx, 4);
+  }
+  if constexpr (MODE == KM_BUILD) {
+    // baby index idx -> point (idx+1)G; layers by index (keyhunt.cpp:5394-5443)
+    uint64_t in[4];
+    x_bytes_u64(x, in);
+    uint64_t a = xxh64_32(in, KH_BLOOM_SEED);
+    uint64_t b = xxh64_32(in, a);
+    uint32_t shard = x.d[7] >> 24;
+    bloom_insert(A.bl1, (uint64_t)shard * A.bd.stride, A.bd, a, b);
+    if (idx < A.m2) bloom_insert(A.bl2, (uint64_t)shard * A.bd2.stride, A.bd2, a, b);
+    if (idx < A.m3) {
+      bloom_insert(A.bl3, (uint64_t)shard * A.bd3.stride, A.bd3, a, b);
+      // bsgs_xvalue {X[16..22), index}: sort key = those 6 bytes big-endian
+      A.rows_key[idx] = ((uint64_t)x.d[3] << 16) | (x.d[2] >> 16);
+      A.rows_val[idx] = idx;
+    }
+  }
+  if constexpr (MODE == KM_DUMP) {
+    uint32_t *o = A.dump_x + (size_t)idx * 8;
+#pragma unroll
+    for (int i = 0; i < 8; i++) o[i] = x.d[i];
+    if (A.dump_y) {
+      uint32_t *q = A.dump_y + (size_t)idx * 8;
+#pragma unroll
+      for (int i = 0; i < 8; i++) q[i] = y.d[i];
+    }
+  }
+}
+
+template <int MODE>
+constexpr bool needs_y() {
+  return MODE == KM_H160U || MODE == KM_H160B || MODE == KM_DUMP;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------
+// The walk.  Every lane runs A.groups groups of 2H points from its saved centre.
+// ------------------------------------------------------------------------------------------
+template <int MODE>
+__global__ void __launch_bounds__(256, 2) k_walk(walk_args A) {
+  constexpr int H = KH_WALK_H;
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= A.L) return;
+  kconst_ptr T = (kconst_ptr)A.tab;  // (H+1) x {x[8], y[8]}, wave-uniform reads
+  uint4 *__restrict__ scr = A.scratch;
+  const size_t L = A.L;
+  fe cx, cy;
+  load_soa(cx, A.cx, A.L, g);
+  load_soa(cy, A.cy, A.L, g);
+
+  for (uint32_t j = 0; j < A.groups; j++) {
+    const uint64_t cidx = (uint64_t)g * A.lane_stride + (uint64_t)(A.group_base + j) * (2 * H) + H;
+    // forward: prefix products of dx_i = T[i].x - C.x
+    fe acc;
+#pragma unroll 1
+    for (int i = 0; i < H; i++) {
+      fe tx, dx;
+      load_fe_k(tx, T + i * 16);
+      fe_sub(dx, tx, cx);
+      if (i == 0)
+        acc = dx;
+      else
+        fe_mul(acc, acc, dx);
+      scr_store(scr, (size_t)i * L + g, acc);
+    }
+    fe t2x, t2y, dxn;
+    load_fe_k(t2x, T + H * 16);
+    load_fe_k(t2y, T + H * 16 + 8);
+    fe_sub(dxn, t2x, cx);
+    fe inv, inv_n;
+    fe_mul(inv, acc, dxn);
+    fe_inv(inv, inv);
+    fe_mul(inv_n, inv, acc);  // 1 / dxn
+    fe_mul(inv, inv, dxn);    // 1 / prefix[H-1]
+
+    // the centre itself (offset 0)
+    probe_point<MODE>(A, cx, cy, cidx);
+
+    // backward: recover 1/dx_i and emit C - T[i] (offset -(i+1)) and C + T[i] (offset i+1).
+    // Both points use the second operand (T.x, +-T.y): x3 = s^2 - C.x - T.x, y3 = s(T.x - x3) -+ T.y.
+#pragma unroll 1
+    for (int i = H - 1; i >= 0; i--) {
+      fe tx, ty, di;
+      load_fe_k(tx, T + i * 16);
+      load_fe_k(ty, T + i * 16 + 8);
+      if (i > 0) {
+        fe pre, dx;
+        scr_load(pre, scr, (size_t)(i - 1) * L + g);
+        fe_mul(di, inv, pre);
+        fe_sub(dx, tx, cx);
+        fe_mul(inv, inv, dx);
+      } else {
+        di = inv;
+      }
+      fe nty;
+      fe_neg(nty, ty);
+#pragma unroll 1
+      for (int side = 0; side < 2; side++) {
+        if (side == 1 && i == H - 1) break;
+        fe tys, dy, s, x, y;
+#pragma unroll
+        for (int w = 0; w < 8; w++) tys.d[w] = side ? ty.d[w] : nty.d[w];
+        fe_sub(dy, tys, cy);
+        fe_mul(s, dy, di);
+        fe_sqr(x, s);
+        fe_sub(x, x, cx);
+        fe_sub(x, x, tx);
+        if constexpr (needs_y<MODE>()) {
+          fe t;
+          fe_sub(t, tx, x);
+          fe_mul(y, s, t);
+          fe_sub(y, y, tys);
+        }
+        const uint64_t off = (uint64_t)(i + 1);
+        probe_point<MODE>(A, x, y, side ? cidx + off : cidx - off);
+      }
+    }
+    // next centre C += T[H]  (keyhunt.cpp:3840-3855)
+    {
+      fe dy, s, s2, nx, ny, t;
+      fe_sub(dy, t2y, cy);
+      fe_mul(s, dy, inv_n);
+      fe_sqr(s2, s);
+      fe_sub(nx, s2, cx);
+      fe_sub(nx, nx, t2x);
+      fe_sub(t, t2x, nx);
+      fe_mul(ny, s, t);
+      fe_sub(ny, ny, t2y);
+      cx = nx;
+      cy = ny;
+    }
+  }
+  store_soa(A.cx, A.L, g, cx);
+  store_soa(A.cy, A.L, g, cy);
+}
+
+// ------------------------------------------------------------------------------------------
+// Lane setup: C_g = [Q +] s_g * G with a fixed-base byte comb, comb[j][v] = v * 2^(8j) * G.
+// Bytes are added from least to most significant, so the accumulator is always (partial
+// scalar)*G with partial < 2^(8j) while comb[j][v] >= 2^(8j): the mixed addition never meets
+// the doubling or inverse case (scalars are < n).  One Fermat inversion per lane to go affine,
+// one more when adding Q (the BSGS target).
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_setup(setup_args A) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= A.L) return;
+  const uint32_t *s = A.scalars + (size_t)g * 8;  // 8 LE u32 limbs
+  gej acc;
+  acc.inf = true;
+  for (int j = 0; j < 32; j++) {
+    uint32_t v = (s[j >> 2] >> ((j & 3) * 8)) & 0xFFu;
+    if (v) {
+      ge q;
+      const uint32_t *c = A.comb + ((size_t)j * 256 + v) * 16;
+      load_fe(q.x, c);
+      load_fe(q.y, c + 8);
+      gej_add_ge(acc, q);
+    }
+  }
+  ge r;
+  gej_to_ge(r, acc);
+  if (A.has_q) {
+    ge q;
+    load_fe(q.x, A.q);
+    load_fe(q.y, A.q + 8);
+    ge_add(r, q, r);
+  }
+  store_soa(A.cx, A.L, g, r.x);
+  store_soa(A.cy, A.L, g, r.y);
+}
+
+// ------------------------------------------------------------------------------------------
+// Parity-test kernels (exercised by tests/ through the C-ABI): hash160 and bloom probes of
+// given inputs, field ops.
+// ------------------------------------------------------------------------------------------
+__global__ void k_test_hash160(const uint32_t *xs, const uint32_t *ys, uint32_t n, uint32_t *out) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  fe x, y;
+  load_fe(x, xs + (size_t)i * 8);
+  load_fe(y, ys + (size_t)i * 8);
+  uint32_t *o = out + (size_t)i * 15;
+  hash160_comp(x, 2, o);
+  hash160_comp(x, 3, o + 5);
+  hash160_uncomp(x, y, o + 10);
+}
+
+__global__ void k_test_field(const uint32_t *a, const uint32_t *b, uint32_t n, uint32_t *out) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  fe x, y, r;
+  load_fe(x, a + (size_t)i * 8);
+  load_fe(y, b + (size_t)i * 8);
+  uint32_t *o = out + (size_t)i * 40;
+  fe_mul(r, x, y);
+#pragma unroll
+  for (int k = 0; k < 8; k++) o[k] = r.d[k];
+  fe_sqr(r, x);
+#pragma unroll
+  for (int k = 0; k < 8; k++) o[8 + k] = r.d[k];
+  fe_inv(r, x);
+#pragma unroll
+  for (int k = 0; k < 8; k++) o[16 + k] = r.d[k];
+  fe_add(r, x, y);
+#pragma unroll
+  for (int k = 0; k < 8; k++) o[24 + k] = r.d[k];
+  fe_sub(r, x, y);
+#pragma unroll
+  for (int k = 0; k < 8; k++) o[32 + k] = r.d[k];
+}
+
+// bloom_check of n items of `len` bytes (20 or 32); shard = first byte when sharded.
+__global__ void k_test_bloom(const uint8_t *items, uint32_t n, uint32_t len, const uint8_t *bloom, bloom_desc bd,
+                             uint32_t sharded, uint32_t *out) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint8_t *p = items + (size_t)i * len;
+  uint64_t a, b;
+  if (len == 32) {
+    uint64_t in[4];
+    for (int k = 0; k < 4; k++) {
+      uint64_t v = 0;
+      for (int q = 7; q >= 0; q--) v = (v << 8) | p[8 * k + q];
+      in[k] = v;
+    }
+    a = xxh64_32(in, KH_BLOOM_SEED);
+    b = xxh64_32(in, a);
+  } else {
+    uint32_t w[5];
+    for (int k = 0; k < 5; k++)
+      w[k] = (uint32_t)p[4 * k] | ((uint32_t)p[4 * k + 1] << 8) | ((uint32_t)p[4 * k + 2] << 16) |
+             ((uint32_t)p[4 * k + 3] << 24);
+    a = xxh64_20(w, KH_BLOOM_SEED);
+    b = xxh64_20(w, a);
+  }
+  const uint8_t *bf = bloom + (sharded ? (size_t)p[0] * bd.stride : 0);
+  out[i] = bloom_probe(bf, bd, a, b) ? 1u : 0u;
+}
+
+// ------------------------------------------------------------------------------------------
+// launch helpers (host side)
+// ------------------------------------------------------------------------------------------
+namespace kh {
+
+hipError_t launch_walk(int mode, const walk_args &A, hipStream_t st) {
+  dim3 block(256), grid((A.L + 255) / 256);
+#ifdef KH_ONLY_MODE
+  if (mode != KH_ONLY_MODE) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_walk<KH_ONLY_MODE>, grid, block, 0, st, A);
+  return hipGetLastError();
+#endif
+  switch (mode) {
+    case KM_H160C: hipLaunchKernelGGL(k_walk<KM_H160C>, grid, block, 0, st, A); break;
+    case KM_H160U: hipLaunchKernelGGL(k_walk<KM_H160U>, grid, block, 0, st, A); break;
+    case KM_H160B: hipLaunchKernelGGL(k_walk<KM_H160B>, grid, block, 0, st, A); break;
+    case KM_XPOINT: hipLaunchKernelGGL(k_walk<KM_XPOINT>, grid, block, 0, st, A); break;
+    case KM_BSGS: hipLaunchKernelGGL(k_walk<KM_BSGS>, grid, block, 0, st, A); break;
+    case KM_BUILD: hipLaunchKernelGGL(k_walk<KM_BUILD>, grid, block, 0, st, A); break;
+    case KM_DUMP: hipLaunchKernelGGL(k_walk<KM_DUMP>, grid, block, 0, st, A); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_setup(const setup_args &A, hipStream_t st) {
+  hipLaunchKernelGGL(k_setup, dim3((A.L + 255) / 256), dim3(256), 0, st, A);
+  return hipGetLastError();
+}
+
+hipError_t launch_test_hash160(const uint32_t *xs, const uint32_t *ys, uint32_t n, uint32_t *out, hipStream_t st) {
+  hipLaunchKernelGGL(k_test_hash160, dim3((n + 127) / 128), dim3(128), 0, st, xs, ys, n, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_test_field(const uint32_t *a, const uint32_t *b, uint32_t n, uint32_t *out, hipStream_t st) {
+  hipLaunchKernelGGL(k_test_field, dim3((n + 127) / 128), dim3(128), 0, st, a, b, n, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_test_bloom(const uint8_t *items, uint32_t n, uint32_t len, const uint8_t *bloom,
+                             const bloom_desc &bd, uint32_t sharded, uint32_t *out, hipStream_t st) {
+  hipLaunchKernelGGL(k_test_bloom, dim3((n + 127) / 128), dim3(128), 0, st, items, n, len, bloom, bd, sharded, out);
+  return hipGetLastError();
+}
+
+}  // namespace kh

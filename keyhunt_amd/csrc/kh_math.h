@@ -1,0 +1,644 @@
+// kh_math.h -- secp256k1 field/group arithmetic, SHA-256, RIPEMD-160, XXH64 and libbloom probes,
+// written once for CDNA4 device code and for the engine's host side (hipcc compiles both).
+//
+// Field elements are 8 x 32-bit little-endian limbs: the 32x32->64 multiply-add that gfx950
+// executes natively (v_mad_u64_u32) is the unit of work, and carry chains use v_add_co/v_addc.
+// In memory (HBM tables, host API) values are the reference's 4 x 64-bit little-endian limbs
+// (secp256k1/Int.h:178-181) -- the same bytes.  All results are canonical (< p); the reference's
+// ModMulK1 omits the final subtraction (secp256k1/IntMod.cpp:912), which can only differ with
+// probability ~2^-224 and never on an emitted X coordinate.
+//
+// Reference behaviour restated here (paths relative to the reference checkout):
+//   fe_mul / fe_sqr ........ secp256k1/IntMod.cpp:855-915, 977-1093 (fold by 0x1000003D1)
+//   fe_add / fe_sub / neg .. secp256k1/IntMod.cpp:41-108
+//   fe_inv ................. secp256k1/IntMod.cpp:382-511 (DRS62 there; Fermat chain here: same value)
+//   sha256 / ripemd160 ..... hash/sha256_sse.cpp:95-554, hash/ripemd160_sse.cpp:323-361
+//   hash160 packing ........ secp256k1/SECP256K1.cpp:974-1024 (04||X||Y), 1187-1250 (02/03||X)
+//   xxh64 .................. xxhash/xxhash.h:2290-2529 (v0.8.0)
+//   bloom probe/add ........ bloom/bloom.cpp:122-146, 189-212
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define KH_HD __host__ __device__ __forceinline__
+#else
+#define KH_HD static inline
+#endif
+
+namespace kh {
+
+struct fe {
+  uint32_t d[8];
+};
+
+// ------------------------------------------------------------------------------------------
+// carry helpers
+// ------------------------------------------------------------------------------------------
+KH_HD uint32_t addc(uint32_t a, uint32_t b, uint32_t cin, uint32_t &cout) {
+  uint64_t s = (uint64_t)a + b + cin;
+  cout = (uint32_t)(s >> 32);
+  return (uint32_t)s;
+}
+KH_HD uint32_t subb(uint32_t a, uint32_t b, uint32_t bin, uint32_t &bout) {
+  uint64_t s = (uint64_t)a - b - bin;
+  bout = (uint32_t)(s >> 63);
+  return (uint32_t)s;
+}
+
+// p = 2^256 - 0x1000003D1
+#define KH_P0 0xFFFFFC2Fu
+#define KH_P1 0xFFFFFFFEu
+
+KH_HD void fe_set_u32(fe &r, uint32_t v) {
+  r.d[0] = v;
+#pragma unroll
+  for (int i = 1; i < 8; i++) r.d[i] = 0;
+}
+KH_HD bool fe_is_zero(const fe &a) {
+  uint32_t o = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) o |= a.d[i];
+  return o == 0;
+}
+KH_HD bool fe_eq(const fe &a, const fe &b) {
+  uint32_t o = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) o |= a.d[i] ^ b.d[i];
+  return o == 0;
+}
+// r >= p ?
+KH_HD bool fe_geq_p(const fe &r) {
+  uint32_t hi = r.d[7] & r.d[6] & r.d[5] & r.d[4] & r.d[3] & r.d[2];
+  if (hi != 0xFFFFFFFFu) return false;
+  if (r.d[1] != KH_P1) return r.d[1] > KH_P1;
+  return r.d[0] >= KH_P0;
+}
+// r -= p  (== r += 0x1000003D1 mod 2^256)
+KH_HD void fe_sub_p(fe &r) {
+  uint32_t c;
+  r.d[0] = addc(r.d[0], 0x3D1u, 0, c);
+  r.d[1] = addc(r.d[1], 1u, c, c);
+#pragma unroll
+  for (int i = 2; i < 8; i++) r.d[i] = addc(r.d[i], 0, c, c);
+}
+KH_HD void fe_canon(fe &r) {
+  if (fe_geq_p(r)) fe_sub_p(r);
+}
+
+KH_HD void fe_add(fe &r, const fe &a, const fe &b) {
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.d[i] = addc(a.d[i], b.d[i], c, c);
+  // if carry or r >= p: r -= p  (t = r + 0x1000003D1 carries out iff r >= p)
+  fe t;
+  uint32_t c2;
+  t.d[0] = addc(r.d[0], 0x3D1u, 0, c2);
+  t.d[1] = addc(r.d[1], 1u, c2, c2);
+#pragma unroll
+  for (int i = 2; i < 8; i++) t.d[i] = addc(r.d[i], 0, c2, c2);
+  bool sel = (c | c2) != 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.d[i] = sel ? t.d[i] : r.d[i];
+}
+KH_HD void fe_sub(fe &r, const fe &a, const fe &b) {
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.d[i] = subb(a.d[i], b.d[i], br, br);
+  // borrow: r += p  == r -= 0x1000003D1 (mod 2^256)
+  uint32_t k0 = br ? 0x3D1u : 0u, k1 = br ? 1u : 0u, b2;
+  r.d[0] = subb(r.d[0], k0, 0, b2);
+  r.d[1] = subb(r.d[1], k1, b2, b2);
+#pragma unroll
+  for (int i = 2; i < 8; i++) r.d[i] = subb(r.d[i], 0, b2, b2);
+}
+KH_HD void fe_neg(fe &r, const fe &a) {
+  fe z;
+  fe_set_u32(z, 0);
+  fe_sub(r, z, a);
+}
+
+// 512-bit t (16 limbs) -> canonical r.  t = lo + hi*2^256 == lo + hi*(2^32 + 977) (mod p).
+KH_HD void fe_reduce512(fe &r, const uint32_t t[16]) {
+  uint32_t u[10];
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint64_t v = (uint64_t)t[8 + i] * 977u + t[i] + c;
+    u[i] = (uint32_t)v;
+    c = v >> 32;
+  }
+  u[8] = (uint32_t)c;
+  uint32_t cy = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) u[i + 1] = addc(u[i + 1], t[8 + i], cy, cy);
+  u[9] = cy;
+  // second fold: h = u[8] + u[9]*2^32 (< 2^34); r = u[0..7] + h*977 + h*2^32
+  uint64_t v = (uint64_t)u[8] * 977u + u[0];
+  r.d[0] = (uint32_t)v;
+  c = v >> 32;
+  v = (uint64_t)u[9] * 977u + u[1] + c + u[8];
+  r.d[1] = (uint32_t)v;
+  c = v >> 32;
+  v = (uint64_t)u[2] + u[9] + c;
+  r.d[2] = (uint32_t)v;
+  uint32_t cc = (uint32_t)(v >> 32);
+#pragma unroll
+  for (int i = 3; i < 8; i++) r.d[i] = addc(u[i], 0, cc, cc);
+  if (cc) fe_sub_p(r);  // wrapped past 2^256: add 0x1000003D1 (cannot wrap again)
+  if (r.d[7] == 0xFFFFFFFFu) fe_canon(r);
+}
+
+KH_HD void fe_mul(fe &r, const fe &a, const fe &b) {
+  uint32_t t[16];
+  {
+    uint64_t c = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      uint64_t v = (uint64_t)a.d[0] * b.d[j] + c;
+      t[j] = (uint32_t)v;
+      c = v >> 32;
+    }
+    t[8] = (uint32_t)c;
+  }
+#pragma unroll
+  for (int i = 1; i < 8; i++) {
+    uint64_t c = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      uint64_t v = (uint64_t)a.d[i] * b.d[j] + t[i + j] + c;
+      t[i + j] = (uint32_t)v;
+      c = v >> 32;
+    }
+    t[i + 8] = (uint32_t)c;
+  }
+  fe_reduce512(r, t);
+}
+
+KH_HD void fe_sqr(fe &r, const fe &a) {
+  uint32_t t[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) t[i] = 0;
+  // cross products a_i*a_j, i<j
+#pragma unroll
+  for (int i = 0; i < 7; i++) {
+    uint64_t c = 0;
+#pragma unroll
+    for (int j = i + 1; j < 8; j++) {
+      uint64_t v = (uint64_t)a.d[i] * a.d[j] + t[i + j] + c;
+      t[i + j] = (uint32_t)v;
+      c = v >> 32;
+    }
+    t[i + 8] = (uint32_t)c;
+  }
+  // double
+  t[15] = (t[15] << 1) | (t[14] >> 31);
+#pragma unroll
+  for (int i = 14; i > 0; i--) t[i] = (t[i] << 1) | (t[i - 1] >> 31);
+  t[0] = t[0] << 1;
+  // add squares
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint64_t v = (uint64_t)a.d[i] * a.d[i] + t[2 * i] + c;
+    t[2 * i] = (uint32_t)v;
+    v = (v >> 32) + t[2 * i + 1];
+    t[2 * i + 1] = (uint32_t)v;
+    c = v >> 32;
+  }
+  fe_reduce512(r, t);
+}
+
+KH_HD void fe_sqr_n(fe &r, const fe &a, int n) {
+  fe_sqr(r, a);
+#pragma unroll 1
+  for (int i = 1; i < n; i++) fe_sqr(r, r);
+}
+
+// a^(p-2): 255 squarings + 15 multiplications (addition chain for p-2 = 2^256 - 2^32 - 979).
+// The squaring runs stay rolled loops: the inversion runs once per 2H points.
+KH_HD void fe_inv(fe &r, const fe &a) {
+  fe x2, x3, x6, x9, x11, x22, x44, x88, x176, x220, x223, t;
+  fe_sqr(x2, a);
+  fe_mul(x2, x2, a);
+  fe_sqr(x3, x2);
+  fe_mul(x3, x3, a);
+  fe_sqr_n(x6, x3, 3);
+  fe_mul(x6, x6, x3);
+  fe_sqr_n(x9, x6, 3);
+  fe_mul(x9, x9, x3);
+  fe_sqr_n(x11, x9, 2);
+  fe_mul(x11, x11, x2);
+  fe_sqr_n(x22, x11, 11);
+  fe_mul(x22, x22, x11);
+  fe_sqr_n(x44, x22, 22);
+  fe_mul(x44, x44, x22);
+  fe_sqr_n(x88, x44, 44);
+  fe_mul(x88, x88, x44);
+  fe_sqr_n(x176, x88, 88);
+  fe_mul(x176, x176, x88);
+  fe_sqr_n(x220, x176, 44);
+  fe_mul(x220, x220, x44);
+  fe_sqr_n(x223, x220, 3);
+  fe_mul(x223, x223, x3);
+  fe_sqr_n(t, x223, 23);
+  fe_mul(t, t, x22);
+  fe_sqr_n(t, t, 5);
+  fe_mul(t, t, a);
+  fe_sqr_n(t, t, 3);
+  fe_mul(t, t, x2);
+  fe_sqr_n(t, t, 2);
+  fe_mul(r, t, a);
+}
+
+// a^((p+1)/4): square root when one exists (p == 3 mod 4).  Returns false if a is a non-residue.
+KH_HD bool fe_sqrt(fe &r, const fe &a) {
+  // (p+1)/4 = 2^254 - 2^30 - 244: chain from libsecp256k1's layout
+  fe x2, x3, x6, x9, x11, x22, x44, x88, x176, x220, x223, t;
+  fe_sqr(x2, a);
+  fe_mul(x2, x2, a);
+  fe_sqr(x3, x2);
+  fe_mul(x3, x3, a);
+  fe_sqr_n(x6, x3, 3);
+  fe_mul(x6, x6, x3);
+  fe_sqr_n(x9, x6, 3);
+  fe_mul(x9, x9, x3);
+  fe_sqr_n(x11, x9, 2);
+  fe_mul(x11, x11, x2);
+  fe_sqr_n(x22, x11, 11);
+  fe_mul(x22, x22, x11);
+  fe_sqr_n(x44, x22, 22);
+  fe_mul(x44, x44, x22);
+  fe_sqr_n(x88, x44, 44);
+  fe_mul(x88, x88, x44);
+  fe_sqr_n(x176, x88, 88);
+  fe_mul(x176, x176, x88);
+  fe_sqr_n(x220, x176, 44);
+  fe_mul(x220, x220, x44);
+  fe_sqr_n(x223, x220, 3);
+  fe_mul(x223, x223, x3);
+  fe_sqr_n(t, x223, 23);
+  fe_mul(t, t, x22);
+  fe_sqr_n(t, t, 6);
+  fe_mul(t, t, x2);
+  fe_sqr(t, t);
+  fe_sqr(r, t);
+  fe chk;
+  fe_sqr(chk, r);
+  return fe_eq(chk, a);
+}
+
+// 4 x u64 little-endian limbs <-> fe
+KH_HD void fe_from_u64(fe &r, const uint64_t v[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    r.d[2 * i] = (uint32_t)v[i];
+    r.d[2 * i + 1] = (uint32_t)(v[i] >> 32);
+  }
+}
+KH_HD void fe_to_u64(uint64_t v[4], const fe &a) {
+#pragma unroll
+  for (int i = 0; i < 4; i++) v[i] = (uint64_t)a.d[2 * i] | ((uint64_t)a.d[2 * i + 1] << 32);
+}
+// 32-byte big-endian (Int::Get32Bytes, secp256k1/Int.cpp:308-316)
+KH_HD void fe_from_be(fe &r, const uint8_t b[32]) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint8_t *p = b + 28 - 4 * i;
+    r.d[i] = ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+  }
+}
+KH_HD void fe_to_be(uint8_t b[32], const fe &a) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint8_t *p = b + 28 - 4 * i;
+    p[0] = (uint8_t)(a.d[i] >> 24);
+    p[1] = (uint8_t)(a.d[i] >> 16);
+    p[2] = (uint8_t)(a.d[i] >> 8);
+    p[3] = (uint8_t)a.d[i];
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Group: affine points; the walk itself lives in the kernels.
+// ------------------------------------------------------------------------------------------
+struct ge {
+  fe x, y;
+};
+struct gej {
+  fe x, y, z;
+  bool inf;
+};
+
+// Jacobian += affine (madd-2007-bl without the doubling/inverse cases: callers never hit them,
+// see kh_kernels.hip scalar-mult comment).
+KH_HD void gej_add_ge(gej &r, const ge &q) {
+  if (r.inf) {
+    r.x = q.x;
+    r.y = q.y;
+    fe_set_u32(r.z, 1);
+    r.inf = false;
+    return;
+  }
+  fe z1z1, u2, s2, h, hh, i, j, rr, v, t;
+  fe_sqr(z1z1, r.z);
+  fe_mul(u2, q.x, z1z1);
+  fe_mul(s2, q.y, r.z);
+  fe_mul(s2, s2, z1z1);
+  fe_sub(h, u2, r.x);
+  fe_sqr(hh, h);
+  fe_add(i, hh, hh);
+  fe_add(i, i, i);
+  fe_mul(j, h, i);
+  fe_sub(rr, s2, r.y);
+  fe_add(rr, rr, rr);
+  fe_mul(v, r.x, i);
+  fe x3, y3, z3;
+  fe_sqr(x3, rr);
+  fe_sub(x3, x3, j);
+  fe_sub(x3, x3, v);
+  fe_sub(x3, x3, v);
+  fe_sub(t, v, x3);
+  fe_mul(y3, rr, t);
+  fe_mul(t, r.y, j);
+  fe_add(t, t, t);
+  fe_sub(y3, y3, t);
+  fe_add(z3, r.z, h);
+  fe_sqr(z3, z3);
+  fe_sub(z3, z3, z1z1);
+  fe_sub(z3, z3, hh);
+  r.x = x3;
+  r.y = y3;
+  r.z = z3;
+}
+KH_HD void gej_to_ge(ge &r, const gej &p) {
+  fe zi, zi2, zi3;
+  fe_inv(zi, p.z);
+  fe_sqr(zi2, zi);
+  fe_mul(zi3, zi2, zi);
+  fe_mul(r.x, p.x, zi2);
+  fe_mul(r.y, p.y, zi3);
+}
+// affine r = p + q with its own inversion (AddDirect, SECP256K1.cpp:455-478); p != +-q.
+KH_HD void ge_add(ge &r, const ge &p, const ge &q) {
+  fe dx, dy, s, s2, t;
+  fe_sub(dx, q.x, p.x);
+  fe_sub(dy, q.y, p.y);
+  fe_inv(dx, dx);
+  fe_mul(s, dy, dx);
+  fe_sqr(s2, s);
+  fe rx, ry;
+  fe_sub(rx, s2, p.x);
+  fe_sub(rx, rx, q.x);
+  fe_sub(t, p.x, rx);
+  fe_mul(ry, s, t);
+  fe_sub(ry, ry, p.y);
+  r.x = rx;
+  r.y = ry;
+}
+// affine doubling (DoubleDirect, SECP256K1.cpp:589-614)
+KH_HD void ge_double(ge &r, const ge &p) {
+  fe x2, n3, d2, s, s2, t, rx, ry;
+  fe_sqr(x2, p.x);
+  fe_add(n3, x2, x2);
+  fe_add(n3, n3, x2);
+  fe_add(d2, p.y, p.y);
+  fe_inv(d2, d2);
+  fe_mul(s, n3, d2);
+  fe_sqr(s2, s);
+  fe_sub(rx, s2, p.x);
+  fe_sub(rx, rx, p.x);
+  fe_sub(t, p.x, rx);
+  fe_mul(ry, s, t);
+  fe_sub(ry, ry, p.y);
+  r.x = rx;
+  r.y = ry;
+}
+
+// ------------------------------------------------------------------------------------------
+// SHA-256 / RIPEMD-160 (single 64-byte blocks, fully unrolled)
+// ------------------------------------------------------------------------------------------
+KH_HD uint32_t rotr32(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+KH_HD uint32_t rotl32(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
+KH_HD uint32_t bswap32(uint32_t x) {
+  return (x >> 24) | ((x >> 8) & 0xFF00u) | ((x << 8) & 0xFF0000u) | (x << 24);
+}
+
+#define KH_SHA_K                                                                                          \
+  {0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u, 0xab1c5ed5u, \
+   0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u, 0x72be5d74u, 0x80deb1feu, 0x9bdc06a7u, 0xc19bf174u, \
+   0xe49b69c1u, 0xefbe4786u, 0x0fc19dc6u, 0x240ca1ccu, 0x2de92c6fu, 0x4a7484aau, 0x5cb0a9dcu, 0x76f988dau, \
+   0x983e5152u, 0xa831c66du, 0xb00327c8u, 0xbf597fc7u, 0xc6e00bf3u, 0xd5a79147u, 0x06ca6351u, 0x14292967u, \
+   0x27b70a85u, 0x2e1b2138u, 0x4d2c6dfcu, 0x53380d13u, 0x650a7354u, 0x766a0abbu, 0x81c2c92eu, 0x92722c85u, \
+   0xa2bfe8a1u, 0xa81a664bu, 0xc24b8b70u, 0xc76c51a3u, 0xd192e819u, 0xd6990624u, 0xf40e3585u, 0x106aa070u, \
+   0x19a4c116u, 0x1e376c08u, 0x2748774cu, 0x34b0bcb5u, 0x391c0cb3u, 0x4ed8aa4au, 0x5b9cca4fu, 0x682e6ff3u, \
+   0x748f82eeu, 0x78a5636fu, 0x84c87814u, 0x8cc70208u, 0x90befffau, 0xa4506cebu, 0xbef9a3f7u, 0xc67178f2u}
+
+KH_HD void sha256_init(uint32_t st[8]) {
+  st[0] = 0x6a09e667u; st[1] = 0xbb67ae85u; st[2] = 0x3c6ef372u; st[3] = 0xa54ff53au;
+  st[4] = 0x510e527fu; st[5] = 0x9b05688cu; st[6] = 0x1f83d9abu; st[7] = 0x5be0cd19u;
+}
+// st = compress(st, w) ; w is consumed (rolling schedule)
+KH_HD void sha256_transform(uint32_t st[8], uint32_t w[16]) {
+  const uint32_t K[64] = KH_SHA_K;
+  uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
+#pragma unroll
+  for (int i = 0; i < 64; i++) {
+    uint32_t wi;
+    if (i < 16) {
+      wi = w[i];
+    } else {
+      uint32_t w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
+      uint32_t s0 = rotr32(w15, 7) ^ rotr32(w15, 18) ^ (w15 >> 3);
+      uint32_t s1 = rotr32(w2, 17) ^ rotr32(w2, 19) ^ (w2 >> 10);
+      wi = w[i & 15] + s0 + w[(i - 7) & 15] + s1;
+      w[i & 15] = wi;
+    }
+    uint32_t t1 = h + (rotr32(e, 6) ^ rotr32(e, 11) ^ rotr32(e, 25)) + ((e & f) ^ (~e & g)) + K[i] + wi;
+    uint32_t t2 = (rotr32(a, 2) ^ rotr32(a, 13) ^ rotr32(a, 22)) + ((a & b) ^ (a & c) ^ (b & c));
+    h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+  }
+  st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+}
+
+// RIPEMD-160 of a 32-byte message given as 8 little-endian words; out: 5 state words (LE bytes)
+KH_HD uint32_t rmd_f(int j, uint32_t x, uint32_t y, uint32_t z) {
+  return j < 16 ? (x ^ y ^ z)
+       : j < 32 ? ((x & y) | (~x & z))
+       : j < 48 ? ((x | ~y) ^ z)
+       : j < 64 ? ((x & z) | (y & ~z))
+                : (x ^ (y | ~z));
+}
+KH_HD void ripemd160_32(const uint32_t m[8], uint32_t out[5]) {
+  const uint8_t RL[80] = {0, 1, 2,  3,  4,  5,  6,  7,  8,  9,  10, 11, 12, 13, 14, 15, 7,  4,  13, 1,
+                          10, 6, 15, 3,  12, 0,  9,  5,  2,  14, 11, 8,  3,  10, 14, 4,  9,  15, 8,  1,
+                          2,  7, 0,  6,  13, 11, 5,  12, 1,  9,  11, 10, 0,  8,  12, 4,  13, 3,  7,  15,
+                          14, 5, 6,  2,  4,  0,  5,  9,  7,  12, 2,  10, 14, 1,  3,  8,  11, 6,  15, 13};
+  const uint8_t RR[80] = {5,  14, 7,  0,  9, 2,  11, 4,  13, 6,  15, 8,  1,  10, 3,  12, 6,  11, 3,  7,
+                          0,  13, 5,  10, 14, 15, 8, 12, 4,  9,  1,  2,  15, 5,  1,  3,  7,  14, 6,  9,
+                          11, 8,  12, 2,  10, 0,  4, 13, 8,  6,  4,  1,  3,  11, 15, 0,  5,  12, 2,  13,
+                          9,  7,  10, 14, 12, 15, 10, 4, 1,  5,  8,  7,  6,  2,  13, 14, 0,  3,  9,  11};
+  const uint8_t SL[80] = {11, 14, 15, 12, 5,  8,  7,  9,  11, 13, 14, 15, 6,  7,  9,  8,  7,  6,  8,  13,
+                          11, 9,  7,  15, 7,  12, 15, 9,  11, 7,  13, 12, 11, 13, 6,  7,  14, 9,  13, 15,
+                          14, 8,  13, 6,  5,  12, 7,  5,  11, 12, 14, 15, 14, 15, 9,  8,  9,  14, 5,  6,
+                          8,  6,  5,  12, 9,  15, 5,  11, 6,  8,  13, 12, 5,  12, 13, 14, 11, 8,  5,  6};
+  const uint8_t SR[80] = {8,  9,  9,  11, 13, 15, 15, 5,  7,  7,  8,  11, 14, 14, 12, 6,  9,  13, 15, 7,
+                          12, 8,  9,  11, 7,  7,  12, 7,  6,  15, 13, 11, 9,  7,  15, 11, 8,  6,  6,  14,
+                          12, 13, 5,  14, 13, 13, 7,  5,  15, 5,  8,  11, 14, 14, 6,  14, 6,  9,  12, 9,
+                          12, 5,  15, 8,  8,  5,  12, 9,  12, 5,  14, 6,  8,  13, 6,  5,  15, 13, 11, 11};
+  const uint32_t KL[5] = {0x00000000u, 0x5A827999u, 0x6ED9EBA1u, 0x8F1BBCDCu, 0xA953FD4Eu};
+  const uint32_t KR[5] = {0x50A28BE6u, 0x5C4DD124u, 0x6D703EF3u, 0x7A6D76E9u, 0x00000000u};
+  uint32_t x[16];
+#pragma unroll
+  for (int i = 0; i < 8; i++) x[i] = m[i];
+  x[8] = 0x80u;
+#pragma unroll
+  for (int i = 9; i < 16; i++) x[i] = 0;
+  x[14] = 256u;
+  const uint32_t h0 = 0x67452301u, h1 = 0xEFCDAB89u, h2 = 0x98BADCFEu, h3 = 0x10325476u, h4 = 0xC3D2E1F0u;
+  uint32_t al = h0, bl = h1, cl = h2, dl = h3, el = h4;
+  uint32_t ar = h0, br = h1, cr = h2, dr = h3, er = h4;
+#pragma unroll
+  for (int j = 0; j < 80; j++) {
+    uint32_t t = rotl32(al + rmd_f(j, bl, cl, dl) + x[RL[j]] + KL[j / 16], SL[j]) + el;
+    al = el; el = dl; dl = rotl32(cl, 10); cl = bl; bl = t;
+    t = rotl32(ar + rmd_f(79 - j, br, cr, dr) + x[RR[j]] + KR[j / 16], SR[j]) + er;
+    ar = er; er = dr; dr = rotl32(cr, 10); cr = br; br = t;
+  }
+  out[0] = h1 + cl + dr;
+  out[1] = h2 + dl + er;
+  out[2] = h3 + el + ar;
+  out[3] = h4 + al + br;
+  out[4] = h0 + bl + cr;
+}
+
+// hash160(prefix || X) for prefix 0x02/0x03, X canonical.  out: 5 LE words = the 20 digest bytes.
+// Message packing as KEYBUFFPREFIX (secp256k1/SECP256K1.cpp:1187-1203).
+KH_HD void hash160_comp(const fe &x, uint32_t prefix, uint32_t out[5]) {
+  uint32_t w[16];
+  w[0] = (prefix << 24) | (x.d[7] >> 8);
+#pragma unroll
+  for (int i = 1; i < 8; i++) w[i] = (x.d[8 - i] << 24) | (x.d[7 - i] >> 8);
+  w[8] = (x.d[0] << 24) | 0x00800000u;
+#pragma unroll
+  for (int i = 9; i < 15; i++) w[i] = 0;
+  w[15] = 0x108u;
+  uint32_t st[8];
+  sha256_init(st);
+  sha256_transform(st, w);
+  uint32_t m[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) m[i] = bswap32(st[i]);
+  ripemd160_32(m, out);
+}
+// hash160(04 || X || Y) (KEYBUFFUNCOMP, secp256k1/SECP256K1.cpp:992-1024): two SHA-256 blocks.
+KH_HD void hash160_uncomp(const fe &x, const fe &y, uint32_t out[5]) {
+  uint32_t w[16];
+  w[0] = 0x04000000u | (x.d[7] >> 8);
+#pragma unroll
+  for (int i = 1; i < 8; i++) w[i] = (x.d[8 - i] << 24) | (x.d[7 - i] >> 8);
+  w[8] = (x.d[0] << 24) | (y.d[7] >> 8);
+#pragma unroll
+  for (int i = 1; i < 8; i++) w[8 + i] = (y.d[8 - i] << 24) | (y.d[7 - i] >> 8);
+  uint32_t st[8];
+  sha256_init(st);
+  sha256_transform(st, w);
+  w[0] = (y.d[0] << 24) | 0x00800000u;
+#pragma unroll
+  for (int i = 1; i < 15; i++) w[i] = 0;
+  w[15] = 0x208u;
+  sha256_transform(st, w);
+  uint32_t m[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) m[i] = bswap32(st[i]);
+  ripemd160_32(m, out);
+}
+
+// ------------------------------------------------------------------------------------------
+// XXH64 for the two input shapes on the hot path (xxhash/xxhash.h:2468-2529).
+// ------------------------------------------------------------------------------------------
+#define KH_XP1 0x9E3779B185EBCA87ULL
+#define KH_XP2 0xC2B2AE3D27D4EB4FULL
+#define KH_XP3 0x165667B19E3779F9ULL
+#define KH_XP4 0x85EBCA77C2B2AE63ULL
+#define KH_XP5 0x27D4EB2F165667C5ULL
+#define KH_BLOOM_SEED 0x59f2815b16f81798ULL
+
+KH_HD uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+KH_HD uint64_t xxh_round(uint64_t acc, uint64_t in) {
+  acc += in * KH_XP2;
+  acc = rotl64(acc, 31);
+  return acc * KH_XP1;
+}
+KH_HD uint64_t xxh_merge(uint64_t acc, uint64_t v) {
+  v = xxh_round(0, v);
+  acc ^= v;
+  return acc * KH_XP1 + KH_XP4;
+}
+KH_HD uint64_t xxh_avalanche(uint64_t h) {
+  h ^= h >> 33;
+  h *= KH_XP2;
+  h ^= h >> 29;
+  h *= KH_XP3;
+  h ^= h >> 32;
+  return h;
+}
+// 32-byte input as 4 little-endian u64 lanes
+KH_HD uint64_t xxh64_32(const uint64_t in[4], uint64_t seed) {
+  uint64_t v1 = seed + KH_XP1 + KH_XP2, v2 = seed + KH_XP2, v3 = seed, v4 = seed - KH_XP1;
+  v1 = xxh_round(v1, in[0]);
+  v2 = xxh_round(v2, in[1]);
+  v3 = xxh_round(v3, in[2]);
+  v4 = xxh_round(v4, in[3]);
+  uint64_t h = rotl64(v1, 1) + rotl64(v2, 7) + rotl64(v3, 12) + rotl64(v4, 18);
+  h = xxh_merge(h, v1);
+  h = xxh_merge(h, v2);
+  h = xxh_merge(h, v3);
+  h = xxh_merge(h, v4);
+  h += 32;
+  return xxh_avalanche(h);
+}
+// 20-byte input as 5 little-endian u32 words
+KH_HD uint64_t xxh64_20(const uint32_t w[5], uint64_t seed) {
+  uint64_t h = seed + KH_XP5 + 20;
+  uint64_t k0 = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+  uint64_t k1 = (uint64_t)w[2] | ((uint64_t)w[3] << 32);
+  h ^= xxh_round(0, k0);
+  h = rotl64(h, 27) * KH_XP1 + KH_XP4;
+  h ^= xxh_round(0, k1);
+  h = rotl64(h, 27) * KH_XP1 + KH_XP4;
+  h ^= (uint64_t)w[4] * KH_XP1;
+  h = rotl64(h, 23) * KH_XP2 + KH_XP3;
+  return xxh_avalanche(h);
+}
+
+// ------------------------------------------------------------------------------------------
+// libbloom2 geometry.  bit index x_i = (a + b*i) mod bits (u64 wrap-around, bloom.cpp:201),
+// computed as h_i = h_{i-1} + b and an exact Barrett reduction by the per-filter reciprocal
+// recip = floor((2^64-1) / bits) (bits < 2^32 on every filter keyhunt builds).
+// ------------------------------------------------------------------------------------------
+struct bloom_desc {
+  uint64_t bits;     // number of bits
+  uint64_t bytes;    // bytes per filter (shard)
+  uint64_t stride;   // bytes between consecutive shards in the device buffer (>= bytes)
+  uint64_t recip;    // floor((2^64-1)/bits)
+  uint32_t hashes;   // number of hash functions
+  uint32_t pad;
+};
+
+KH_HD uint64_t mulhi64(uint64_t a, uint64_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __umul64hi(a, b);
+#else
+  return (uint64_t)(((unsigned __int128)a * b) >> 64);
+#endif
+}
+KH_HD uint64_t mod_bits(uint64_t h, uint64_t bits, uint64_t recip) {
+  uint64_t q = mulhi64(h, recip);
+  uint64_t r = h - q * bits;
+  if (r >= bits) r -= bits;
+  if (r >= bits) r -= bits;
+  return r;
+}
+
+}  // namespace kh

@@ -1,0 +1,261 @@
+"""ctypes binding of include/kh_gpu.h (lib/libkh_gpu.so) -- the MI355X engine.
+
+`Engine` mirrors the reference's worker seams (see include/kh_gpu.h for the keyhunt.cpp lines each
+call replaces).  There is no CPU path here: if the shared library or the GPU is missing, calls
+raise.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+import subprocess
+from dataclasses import dataclass
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(PKG)
+LIB_PATH = os.path.join(PKG, "lib", "libkh_gpu.so")
+HEADER = os.path.join(REPO, "include", "kh_gpu.h")
+
+KH_MODE_ADDRESS, KH_MODE_XPOINT = 0, 1
+KH_SEARCH_COMPRESS, KH_SEARCH_UNCOMPRESS, KH_SEARCH_BOTH = 0, 1, 2
+KH_KIND_02, KH_KIND_03, KH_KIND_04, KH_KIND_XPOINT = 0, 1, 2, 3
+TIME_ADDRESS, TIME_XPOINT, TIME_BSGS, TIME_BUILD, TIME_SETUP = 0, 1, 2, 3, 4
+
+ORDER_N = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141
+
+
+class KhError(RuntimeError):
+    pass
+
+
+class KhHit(ctypes.Structure):
+    _fields_ = [("key", ctypes.c_uint8 * 32), ("offset", ctypes.c_uint64), ("kind", ctypes.c_uint32),
+                ("compressed", ctypes.c_uint32)]
+
+
+class KhBsgsInfo(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_uint64), ("m", ctypes.c_uint64), ("m2", ctypes.c_uint64), ("m3", ctypes.c_uint64),
+                ("aux", ctypes.c_uint64), ("cycles", ctypes.c_uint64), ("bloom_bits", ctypes.c_uint64 * 3),
+                ("bloom_bytes", ctypes.c_uint64 * 3), ("bloom_hashes", ctypes.c_uint32 * 3), ("pad", ctypes.c_uint32)]
+
+
+class KhBsgsFound(ctypes.Structure):
+    _fields_ = [("target", ctypes.c_uint32), ("pad", ctypes.c_uint32), ("key", ctypes.c_uint8 * 32)]
+
+
+_lib = None
+
+
+def build(jobs: int = 8) -> str:
+    subprocess.run(["make", "-s", "-C", PKG, f"-j{jobs}"], check=True)
+    return LIB_PATH
+
+
+def header_symbols() -> list[str]:
+    """Every function the C-ABI header declares."""
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char \*)\s*(kh_\w+)\s*\(", txt, re.M)))
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise KhError(f"{LIB_PATH} is missing: build the HIP engine first (python -c 'import keyhunt_amd; keyhunt_amd.build()')")
+    L = ctypes.CDLL(LIB_PATH)
+    P = ctypes.c_void_p
+    u8p = ctypes.c_char_p
+    L.kh_strerror.restype = ctypes.c_char_p
+    L.kh_last_error.restype = ctypes.c_char_p
+    L.kh_last_error.argtypes = [P]
+    L.kh_open.argtypes = [ctypes.c_int, ctypes.POINTER(P)]
+    L.kh_close.argtypes = [P]
+    L.kh_set_geometry.argtypes = [P, ctypes.c_uint32, ctypes.c_uint32]
+    L.kh_synchronize.argtypes = [P]
+    L.kh_set_targets.argtypes = [P, u8p, ctypes.c_uint64, ctypes.c_uint64]
+    L.kh_scan.argtypes = [P, u8p, u8p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(KhHit),
+                          ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]
+    L.kh_bsgs_setup.argtypes = [P, ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(KhBsgsInfo)]
+    L.kh_bsgs_build.argtypes = [P]
+    L.kh_bsgs_set_targets.argtypes = [P, u8p, ctypes.c_uint32]
+    L.kh_bsgs_scan.argtypes = [P, u8p, ctypes.c_uint64, ctypes.POINTER(KhBsgsFound), ctypes.c_uint32,
+                               ctypes.POINTER(ctypes.c_uint32)]
+    L.kh_bsgs_reset_found.argtypes = [P]
+    L.kh_bsgs_candidates.argtypes = [P, ctypes.POINTER(ctypes.c_uint64)]
+    L.kh_kernel_time.argtypes = [P, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_double),
+                                 ctypes.POINTER(ctypes.c_uint64)]
+    L.kh_kernel_time_reset.argtypes = [P]
+    L.kh_pubkeys.argtypes = [P, u8p, ctypes.c_uint32, u8p]
+    L.kh_walk_points.argtypes = [P, u8p, u8p, ctypes.c_uint64, u8p, u8p]
+    L.kh_hash160.argtypes = [P, u8p, ctypes.c_uint32, u8p]
+    L.kh_field_ops.argtypes = [P, u8p, u8p, ctypes.c_uint32, u8p]
+    L.kh_bloom_check.argtypes = [P, ctypes.c_uint32, u8p, ctypes.c_uint32, ctypes.c_uint32, u8p]
+    L.kh_get_bloom.argtypes = [P, ctypes.c_uint32, u8p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]
+    L.kh_get_bsgs_table.argtypes = [P, u8p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]
+    _lib = L
+    return L
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    lib().kh_device_count(ctypes.byref(n))
+    return n.value
+
+
+def be32(v: int) -> bytes:
+    return (int(v) % (1 << 256)).to_bytes(32, "big")
+
+
+@dataclass
+class ScanHit:
+    key: int
+    offset: int
+    kind: int
+    compressed: bool
+
+
+class Engine:
+    """One device context (kh_open).  Not thread-safe; one Engine per GPU."""
+
+    def __init__(self, device: int = 0, lanes: int = 0, groups_per_launch: int = 0):
+        self._ctx = ctypes.c_void_p()
+        r = lib().kh_open(device, ctypes.byref(self._ctx))
+        if r:
+            raise KhError(f"kh_open({device}) failed: {lib().kh_strerror(r).decode()}")
+        self.device = device
+        if lanes or groups_per_launch:
+            self.set_geometry(lanes, groups_per_launch)
+
+    # -- plumbing ------------------------------------------------------------------------------
+    def _chk(self, r: int, what: str) -> None:
+        if r:
+            raise KhError(f"{what}: {lib().kh_strerror(r).decode()} ({lib().kh_last_error(self._ctx).decode()})")
+
+    def close(self) -> None:
+        if self._ctx:
+            lib().kh_close(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_geometry(self, lanes: int = 0, groups_per_launch: int = 0) -> None:
+        self._chk(lib().kh_set_geometry(self._ctx, lanes, groups_per_launch), "kh_set_geometry")
+
+    def synchronize(self) -> None:
+        self._chk(lib().kh_synchronize(self._ctx), "kh_synchronize")
+
+    # -- address / rmd160 / xpoint -------------------------------------------------------------
+    def set_targets(self, rows: list[bytes], bloom_items: int = 0) -> None:
+        buf = b"".join(rows)
+        assert all(len(r) == 20 for r in rows)
+        self._chk(lib().kh_set_targets(self._ctx, buf, len(rows), bloom_items), "kh_set_targets")
+
+    def scan(self, start: int, n_keys: int, mode: int = KH_MODE_ADDRESS, search: int = KH_SEARCH_BOTH,
+             stride: int = 1, cap: int = 4096) -> list[ScanHit]:
+        hits = (KhHit * cap)()
+        n = ctypes.c_uint32(0)
+        r = lib().kh_scan(self._ctx, be32(start), be32(stride), n_keys, mode, search, hits, cap, ctypes.byref(n))
+        self._chk(r, "kh_scan")
+        return [ScanHit(int.from_bytes(bytes(h.key), "big"), h.offset, h.kind, bool(h.compressed))
+                for h in hits[: n.value]]
+
+    # -- BSGS ----------------------------------------------------------------------------------
+    def bsgs_setup(self, n: int, k: int) -> KhBsgsInfo:
+        info = KhBsgsInfo()
+        self._chk(lib().kh_bsgs_setup(self._ctx, n, k, ctypes.byref(info)), "kh_bsgs_setup")
+        return info
+
+    def bsgs_build(self) -> None:
+        self._chk(lib().kh_bsgs_build(self._ctx), "kh_bsgs_build")
+
+    def bsgs_set_targets(self, points: list[tuple[int, int]]) -> None:
+        buf = b"".join(be32(x) + be32(y) for x, y in points)
+        self._chk(lib().kh_bsgs_set_targets(self._ctx, buf, len(points)), "kh_bsgs_set_targets")
+
+    def bsgs_scan(self, start: int, n_bases: int, cap: int = 1024) -> list[tuple[int, int]]:
+        out = (KhBsgsFound * cap)()
+        n = ctypes.c_uint32(0)
+        self._chk(lib().kh_bsgs_scan(self._ctx, be32(start), n_bases, out, cap, ctypes.byref(n)), "kh_bsgs_scan")
+        return [(f.target, int.from_bytes(bytes(f.key), "big")) for f in out[: n.value]]
+
+    def bsgs_reset_found(self) -> None:
+        self._chk(lib().kh_bsgs_reset_found(self._ctx), "kh_bsgs_reset_found")
+
+    def bsgs_candidates(self) -> int:
+        c = ctypes.c_uint64()
+        self._chk(lib().kh_bsgs_candidates(self._ctx, ctypes.byref(c)), "kh_bsgs_candidates")
+        return c.value
+
+    # -- measurement ---------------------------------------------------------------------------
+    def kernel_time(self, kind: int) -> tuple[int, float, int]:
+        la, ms, pts = ctypes.c_uint64(), ctypes.c_double(), ctypes.c_uint64()
+        self._chk(lib().kh_kernel_time(self._ctx, kind, ctypes.byref(la), ctypes.byref(ms), ctypes.byref(pts)),
+                  "kh_kernel_time")
+        return la.value, ms.value, pts.value
+
+    def kernel_time_reset(self) -> None:
+        self._chk(lib().kh_kernel_time_reset(self._ctx), "kh_kernel_time_reset")
+
+    # -- parity hooks --------------------------------------------------------------------------
+    def pubkeys(self, scalars: list[int]) -> list[tuple[int, int]]:
+        buf = b"".join(be32(s) for s in scalars)
+        out = ctypes.create_string_buffer(64 * len(scalars))
+        self._chk(lib().kh_pubkeys(self._ctx, buf, len(scalars), out), "kh_pubkeys")
+        raw = out.raw
+        return [(int.from_bytes(raw[64 * i:64 * i + 32], "big"), int.from_bytes(raw[64 * i + 32:64 * i + 64], "big"))
+                for i in range(len(scalars))]
+
+    def walk_points(self, start: int, n_points: int, stride: int = 1, need_y: bool = False):
+        xs = ctypes.create_string_buffer(32 * n_points)
+        ys = ctypes.create_string_buffer(32 * n_points) if need_y else None
+        self._chk(lib().kh_walk_points(self._ctx, be32(start), be32(stride), n_points, xs, ys), "kh_walk_points")
+        return xs.raw, (ys.raw if need_y else None)
+
+    def hash160(self, points: list[tuple[int, int]]) -> list[tuple[bytes, bytes, bytes]]:
+        buf = b"".join(be32(x) + be32(y) for x, y in points)
+        out = ctypes.create_string_buffer(60 * len(points))
+        self._chk(lib().kh_hash160(self._ctx, buf, len(points), out), "kh_hash160")
+        raw = out.raw
+        return [(raw[60 * i:60 * i + 20], raw[60 * i + 20:60 * i + 40], raw[60 * i + 40:60 * i + 60])
+                for i in range(len(points))]
+
+    def field_ops(self, a: list[int], b: list[int]) -> list[tuple[int, int, int, int, int]]:
+        ba = b"".join(be32(x) for x in a)
+        bb = b"".join(be32(x) for x in b)
+        out = ctypes.create_string_buffer(160 * len(a))
+        self._chk(lib().kh_field_ops(self._ctx, ba, bb, len(a), out), "kh_field_ops")
+        raw = out.raw
+        return [tuple(int.from_bytes(raw[160 * i + 32 * k:160 * i + 32 * k + 32], "big") for k in range(5))
+                for i in range(len(a))]
+
+    def bloom_check(self, layer: int, items: list[bytes]) -> list[bool]:
+        ln = len(items[0])
+        out = ctypes.create_string_buffer(len(items))
+        self._chk(lib().kh_bloom_check(self._ctx, layer, b"".join(items), len(items), ln, out), "kh_bloom_check")
+        return [b != 0 for b in out.raw]
+
+    def get_bloom(self, layer: int) -> bytes:
+        nb = ctypes.c_uint64()
+        self._chk(lib().kh_get_bloom(self._ctx, layer, None, 0, ctypes.byref(nb)), "kh_get_bloom")
+        buf = ctypes.create_string_buffer(nb.value)
+        self._chk(lib().kh_get_bloom(self._ctx, layer, buf, nb.value, ctypes.byref(nb)), "kh_get_bloom")
+        return buf.raw
+
+    def get_bsgs_table(self) -> bytes:
+        n = ctypes.c_uint64()
+        self._chk(lib().kh_get_bsgs_table(self._ctx, None, 0, ctypes.byref(n)), "kh_get_bsgs_table")
+        buf = ctypes.create_string_buffer(16 * n.value)
+        self._chk(lib().kh_get_bsgs_table(self._ctx, buf, n.value, ctypes.byref(n)), "kh_get_bsgs_table")
+        return buf.raw

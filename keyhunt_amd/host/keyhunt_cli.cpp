@@ -1,0 +1,866 @@
+// keyhunt_cli.cpp -- command-line host of the MI355X engine (bin/keyhunt-amd).
+//
+// Keeps the reference's interface for the hot-path modes: -m address|rmd160|xpoint|bsgs, -f, -r,
+// -b, -k, -n, -l, -q, -s, -I (stride), plus -g (GPUs to use; one host thread + kh_ctx each, like one
+// pthread per -t in the reference, keyhunt.cpp:2717-2839).  Hit text, KEYFOUNDKEYFOUND.txt records
+// and the stats line follow keyhunt.cpp:6891-6923 (writekey), 4825-4858 (BSGS) and 2850-2962.
+// Sequential scans consume the range in whole N_SEQUENTIAL_MAX chunks (keyhunt.cpp:3314-3330) and
+// BSGS in whole 2N bases (keyhunt.cpp:4600-4617), exactly as the reference's cursors do.
+// Random modes (-R, -B random/dance...), endomorphism (-e), vanity, minikeys, ETH and the table
+// persistence flags are outside this engine's scope and are rejected.
+#include <getopt.h>
+#include <pthread.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "kh_gpu.h"
+#include "../csrc/kh_math.h"
+
+using namespace kh;
+
+namespace {
+
+const char *VERSION = "keyhunt-amd 0.1 (MI355X engine for keyhunt 0.2.230519 hot paths)";
+
+// ---------------------------------------------------------------------------------------------
+// big integers (256-bit, plus a little headroom for range arithmetic)
+// ---------------------------------------------------------------------------------------------
+typedef unsigned __int128 u128;
+struct U {
+  uint64_t v[5] = {0, 0, 0, 0, 0};
+};
+U u_from_u64(uint64_t x) {
+  U r;
+  r.v[0] = x;
+  return r;
+}
+int u_cmp(const U &a, const U &b) {
+  for (int i = 4; i >= 0; i--) {
+    if (a.v[i] < b.v[i]) return -1;
+    if (a.v[i] > b.v[i]) return 1;
+  }
+  return 0;
+}
+U u_add(const U &a, const U &b) {
+  U r;
+  u128 c = 0;
+  for (int i = 0; i < 5; i++) {
+    c += (u128)a.v[i] + b.v[i];
+    r.v[i] = (uint64_t)c;
+    c >>= 64;
+  }
+  return r;
+}
+U u_sub(const U &a, const U &b) {
+  U r;
+  uint64_t br = 0;
+  for (int i = 0; i < 5; i++) {
+    u128 t = (u128)a.v[i] - b.v[i] - br;
+    r.v[i] = (uint64_t)t;
+    br = (uint64_t)(t >> 64) & 1;
+  }
+  return r;
+}
+U u_mul_u64(const U &a, uint64_t m) {
+  U r;
+  u128 c = 0;
+  for (int i = 0; i < 5; i++) {
+    c += (u128)a.v[i] * m;
+    r.v[i] = (uint64_t)c;
+    c >>= 64;
+  }
+  return r;
+}
+bool u_is_zero(const U &a) { return !(a.v[0] | a.v[1] | a.v[2] | a.v[3] | a.v[4]); }
+U u_shl1(int bits) {  // 1 << bits
+  U r;
+  r.v[bits / 64] = 1ULL << (bits % 64);
+  return r;
+}
+// a / b for b < 2^64, and remainder
+U u_divmod_u64(const U &a, uint64_t b, uint64_t *rem) {
+  U q;
+  u128 r = 0;
+  for (int i = 4; i >= 0; i--) {
+    r = (r << 64) | a.v[i];
+    q.v[i] = (uint64_t)(r / b);
+    r %= b;
+  }
+  if (rem) *rem = (uint64_t)r;
+  return q;
+}
+bool u_from_hex(const char *s, U &r) {
+  r = U();
+  if (s[0] == '0' && (s[1] == 'x' || s[1] == 'X')) s += 2;
+  size_t n = strlen(s);
+  if (n == 0 || n > 64) return false;
+  for (size_t i = 0; i < n; i++) {
+    char c = s[i];
+    int d = (c >= '0' && c <= '9') ? c - '0' : (c >= 'a' && c <= 'f') ? c - 'a' + 10 : (c >= 'A' && c <= 'F') ? c - 'A' + 10 : -1;
+    if (d < 0) return false;
+    // r = r*16 + d
+    for (int k = 4; k > 0; k--) r.v[k] = (r.v[k] << 4) | (r.v[k - 1] >> 60);
+    r.v[0] = (r.v[0] << 4) | (uint64_t)d;
+  }
+  return true;
+}
+bool u_from_dec(const char *s, U &r) {
+  r = U();
+  if (!*s) return false;
+  for (; *s; s++) {
+    if (*s < '0' || *s > '9') return false;
+    r = u_add(u_mul_u64(r, 10), u_from_u64((uint64_t)(*s - '0')));
+  }
+  return true;
+}
+// lowercase hex without leading zeros (Int::GetBase16, secp256k1/Int.cpp:1019-1055)
+std::string u_hex(const U &a) {
+  static const char *H = "0123456789abcdef";
+  std::string s;
+  bool lead = true;
+  for (int i = 4; i >= 0; i--)
+    for (int j = 60; j >= 0; j -= 4) {
+      int d = (int)((a.v[i] >> j) & 15);
+      if (lead && d == 0) continue;
+      lead = false;
+      s += H[d];
+    }
+  return s.empty() ? "0" : s;
+}
+std::string u_dec(const U &a) {
+  if (u_is_zero(a)) return "0";
+  std::string s;
+  U x = a;
+  while (!u_is_zero(x)) {
+    uint64_t r;
+    x = u_divmod_u64(x, 10, &r);
+    s += (char)('0' + r);
+  }
+  std::reverse(s.begin(), s.end());
+  return s;
+}
+void u_to_be32(const U &a, uint8_t b[32]) {
+  for (int i = 0; i < 4; i++)
+    for (int j = 0; j < 8; j++) b[(3 - i) * 8 + j] = (uint8_t)(a.v[i] >> (56 - 8 * j));
+}
+U u_from_be32(const uint8_t b[32]) {
+  U r;
+  for (int i = 0; i < 4; i++) {
+    uint64_t w = 0;
+    for (int j = 0; j < 8; j++) w = (w << 8) | b[(3 - i) * 8 + j];
+    r.v[i] = w;
+  }
+  return r;
+}
+const char *ORDER_HEX = "FFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141";
+
+// ---------------------------------------------------------------------------------------------
+// hashing / encoding for hit output
+// ---------------------------------------------------------------------------------------------
+void sha256(const uint8_t *msg, size_t len, uint8_t out[32]) {
+  uint32_t st[8];
+  sha256_init(st);
+  size_t off = 0;
+  uint32_t w[16];
+  auto load = [&](const uint8_t *b) {
+    for (int i = 0; i < 16; i++)
+      w[i] = ((uint32_t)b[4 * i] << 24) | ((uint32_t)b[4 * i + 1] << 16) | ((uint32_t)b[4 * i + 2] << 8) | b[4 * i + 3];
+  };
+  while (len - off >= 64) {
+    load(msg + off);
+    sha256_transform(st, w);
+    off += 64;
+  }
+  uint8_t blk[128] = {0};
+  size_t rem = len - off;
+  memcpy(blk, msg + off, rem);
+  blk[rem] = 0x80;
+  size_t nb = rem >= 56 ? 2 : 1;
+  uint64_t bits = (uint64_t)len * 8;
+  for (int i = 0; i < 8; i++) blk[nb * 64 - 1 - i] = (uint8_t)(bits >> (8 * i));
+  for (size_t b = 0; b < nb; b++) {
+    load(blk + 64 * b);
+    sha256_transform(st, w);
+  }
+  for (int i = 0; i < 8; i++) {
+    out[4 * i] = st[i] >> 24;
+    out[4 * i + 1] = st[i] >> 16;
+    out[4 * i + 2] = st[i] >> 8;
+    out[4 * i + 3] = st[i];
+  }
+}
+const char *B58 = "123456789ABCDEFGHJKLMNPQRSTUVWXYZabcdefghijkmnopqrstuvwxyz";
+std::string b58enc(const uint8_t *d, int n) {
+  std::vector<uint8_t> buf;
+  int zeros = 0;
+  while (zeros < n && d[zeros] == 0) zeros++;
+  for (int i = zeros; i < n; i++) {
+    int carry = d[i];
+    for (auto &b : buf) {
+      carry += b * 256;
+      b = carry % 58;
+      carry /= 58;
+    }
+    while (carry) {
+      buf.push_back(carry % 58);
+      carry /= 58;
+    }
+  }
+  std::string s(zeros, '1');
+  for (auto it = buf.rbegin(); it != buf.rend(); ++it) s += B58[*it];
+  return s;
+}
+// b58tobin into exactly 25 bytes (forceReadFileAddress, keyhunt.cpp:7283-7292)
+bool b58dec25(const char *s, uint8_t out[25]) {
+  std::vector<uint8_t> buf;
+  int zeros = 0;
+  while (s[zeros] == '1') zeros++;
+  for (const char *q = s + zeros; *q; q++) {
+    const char *pos = strchr(B58, *q);
+    if (!pos) return false;
+    int carry = (int)(pos - B58);
+    for (auto &b : buf) {
+      carry += b * 58;
+      b = carry & 0xff;
+      carry >>= 8;
+    }
+    while (carry) {
+      buf.push_back(carry & 0xff);
+      carry >>= 8;
+    }
+  }
+  if (zeros + (int)buf.size() != 25) return false;
+  memset(out, 0, zeros);
+  for (size_t i = 0; i < buf.size(); i++) out[zeros + i] = buf[buf.size() - 1 - i];
+  return true;
+}
+std::string hex(const uint8_t *b, int n) {
+  static const char *H = "0123456789abcdef";
+  std::string s;
+  for (int i = 0; i < n; i++) {
+    s += H[b[i] >> 4];
+    s += H[b[i] & 15];
+  }
+  return s;
+}
+bool is_hex(const char *s) {
+  for (; *s; s++)
+    if (!strchr("0123456789abcdefABCDEF", *s)) return false;
+  return true;
+}
+bool hex2bin(const char *s, uint8_t *out, size_t n) {
+  if (strlen(s) < 2 * n) return false;
+  for (size_t i = 0; i < n; i++) {
+    unsigned v;
+    if (sscanf(s + 2 * i, "%2x", &v) != 1) return false;
+    out[i] = (uint8_t)v;
+  }
+  return true;
+}
+std::string rmd_to_address(const uint8_t h[20]) {
+  uint8_t d[25], c1[32], c2[32];
+  d[0] = 0;
+  memcpy(d + 1, h, 20);
+  sha256(d, 21, c1);
+  sha256(c1, 32, c2);
+  memcpy(d + 21, c2, 4);
+  return b58enc(d, 25);
+}
+void trim(char *s) {
+  size_t n = strlen(s);
+  while (n && strchr(" \t\r\n", s[n - 1])) s[--n] = 0;
+  size_t i = 0;
+  while (s[i] && strchr(" \t\r\n", s[i])) i++;
+  if (i) memmove(s, s + i, n - i + 1);
+}
+
+// ---------------------------------------------------------------------------------------------
+// options and shared state
+// ---------------------------------------------------------------------------------------------
+enum { MODE_ADDRESS, MODE_RMD160, MODE_XPOINT, MODE_BSGS };
+struct options {
+  int mode = MODE_ADDRESS;
+  const char *file = nullptr;
+  int search = KH_SEARCH_BOTH;
+  bool have_range = false, have_bits = false;
+  U start, end;
+  int bits = 0;
+  uint64_t kfactor = 1;
+  bool flag_n = false;
+  const char *str_n = nullptr;
+  int gpus = 0;
+  bool quiet = false;
+  int seconds = 30;
+  U stride = u_from_u64(1);
+  bool matrix = false;
+} opt;
+
+std::mutex g_keys_mtx, g_cursor_mtx;
+std::atomic<uint64_t> g_groups_done{0};  // 1024-key groups (address family)
+std::atomic<uint64_t> g_bases_done{0};   // BSGS bases
+std::atomic<int> g_running{0};
+U g_cursor;
+U g_end;
+
+// ---------------------------------------------------------------------------------------------
+// hit output
+// ---------------------------------------------------------------------------------------------
+void writekey(kh_ctx *ctx, bool compressed, const uint8_t key[32]) {
+  // keyhunt.cpp:6891-6923
+  uint8_t xy[64];
+  kh_pubkeys(ctx, key, 1, xy);
+  fe x, y;
+  fe_from_be(x, xy);
+  fe_from_be(y, xy + 32);
+  uint32_t hw[5];
+  std::string pub;
+  if (compressed) {
+    uint8_t pfx = (y.d[0] & 1) ? 3 : 2;
+    hash160_comp(x, pfx, hw);
+    pub = hex(&pfx, 1) + hex(xy, 32);
+  } else {
+    uint8_t pfx = 4;
+    hash160_uncomp(x, y, hw);
+    pub = hex(&pfx, 1) + hex(xy, 64);
+  }
+  uint8_t rmd[20];
+  memcpy(rmd, hw, 20);
+  std::string addr = rmd_to_address(rmd);
+  std::string k = u_hex(u_from_be32(key));
+  std::lock_guard<std::mutex> lk(g_keys_mtx);
+  FILE *f = fopen("KEYFOUNDKEYFOUND.txt", "a+");
+  if (f) {
+    fprintf(f, "Private Key: %s\npubkey: %s\nAddress %s\nrmd160 %s\n", k.c_str(), pub.c_str(), addr.c_str(),
+            hex(rmd, 20).c_str());
+    fclose(f);
+  }
+  printf("\nHit! Private Key: %s\npubkey: %s\nAddress %s\nrmd160 %s\n", k.c_str(), pub.c_str(), addr.c_str(),
+         hex(rmd, 20).c_str());
+  fflush(stdout);
+}
+
+// ---------------------------------------------------------------------------------------------
+// target files
+// ---------------------------------------------------------------------------------------------
+// forceReadFileAddress (keyhunt.cpp:7239-7310) / forceReadFileXPoint (7392-7490)
+bool read_targets(const char *fn, int mode, std::vector<uint8_t> &rows, uint64_t &bloom_items) {
+  FILE *f = fopen(fn, "r");
+  if (!f) {
+    fprintf(stderr, "[E] Error opening the file %s\n", fn);
+    return false;
+  }
+  char line[1024];
+  uint64_t counted = 0;
+  std::vector<std::string> lines;
+  while (fgets(line, sizeof line, f)) {
+    trim(line);
+    size_t r = strlen(line);
+    if ((mode == MODE_XPOINT && r >= 40) || (mode != MODE_XPOINT && r > 20)) counted++;
+    lines.push_back(line);
+  }
+  fclose(f);
+  bloom_items = counted;
+  printf("[+] Allocating memory for %llu elements: %.2f MB\n", (unsigned long long)counted,
+         (double)(counted * 20) / 1048576.0);
+  for (auto &ln : lines) {
+    size_t r = ln.size();
+    uint8_t raw[100];
+    if (mode == MODE_XPOINT) {
+      if (r < 40) continue;
+      std::string tok = ln.substr(0, ln.find_first_of(" \t"));
+      if (!is_hex(tok.c_str())) {
+        fprintf(stderr, "[E] Ignoring invalid hexvalue %s\n", ln.c_str());
+        rows.insert(rows.end(), 20, 0);  // the reference leaves a zero row (keyhunt.cpp:7419-7486)
+        continue;
+      }
+      if (tok.size() == 64 && hex2bin(tok.c_str(), raw, 32)) rows.insert(rows.end(), raw, raw + 20);
+      else if (tok.size() == 66 && hex2bin(tok.c_str() + 2, raw, 32)) rows.insert(rows.end(), raw, raw + 20);
+      else if (tok.size() == 130 && hex2bin(tok.c_str(), raw, 65)) rows.insert(rows.end(), raw + 2, raw + 22);
+      else {
+        fprintf(stderr, "[E] Omiting line unknow length size %zu: %s\n", tok.size(), ln.c_str());
+        rows.insert(rows.end(), 20, 0);
+      }
+      continue;
+    }
+    if (r <= 20) continue;
+    bool ok = false;
+    if (r > 0 && r <= 40) {
+      if (r < 40) {
+        uint8_t a[25];
+        if (b58dec25(ln.c_str(), a)) {
+          rows.insert(rows.end(), a + 1, a + 21);
+          ok = true;
+        }
+      }
+      if (r == 40 && is_hex(ln.c_str()) && hex2bin(ln.c_str(), raw, 20)) {
+        rows.insert(rows.end(), raw, raw + 20);
+        ok = true;
+      }
+    }
+    if (!ok) fprintf(stderr, "[I] Ommiting invalid line %s\n", ln.c_str());
+  }
+  return true;
+}
+
+bool parse_pubkey(const char *s, fe &x, fe &y, bool &compressed) {
+  size_t n = strlen(s);
+  uint8_t raw[65];
+  if (n == 66 && (s[0] == '0' && (s[1] == '2' || s[1] == '3'))) {
+    if (!hex2bin(s + 2, raw, 32)) return false;
+    fe_from_be(x, raw);
+    fe t, s3, seven;
+    fe_sqr(t, x);
+    fe_mul(t, t, x);
+    fe_set_u32(seven, 7);
+    fe_add(s3, t, seven);
+    if (!fe_sqrt(y, s3)) return false;
+    uint32_t odd = s[1] == '3';
+    if ((y.d[0] & 1) != odd) fe_neg(y, y);
+    compressed = true;
+    return true;
+  }
+  if (n == 130 && s[0] == '0' && s[1] == '4') {
+    if (!hex2bin(s + 2, raw, 64)) return false;
+    fe_from_be(x, raw);
+    fe_from_be(y, raw + 32);
+    compressed = false;
+    return true;
+  }
+  return false;
+}
+
+// validate_nk (util.c:358-389)
+bool validate_nk(uint64_t n, uint64_t k) {
+  if (n < (1ULL << 20)) {
+    fprintf(stderr, "[E] n must be at least 2^20 (0x100000)\n");
+    return false;
+  }
+  if (n & (n - 1)) {
+    fprintf(stderr, "[E] n must be a power of two\n");
+    return false;
+  }
+  int bits = 0;
+  for (uint64_t t = n; t > 1; t >>= 1) bits++;
+  if (bits % 2 || bits < 20 || bits > 64) {
+    fprintf(stderr, "[E] invalid n 0x%llx\n", (unsigned long long)n);
+    return false;
+  }
+  uint64_t kmax = 1ULL << ((bits - 20) / 2 * 1);
+  // table: {20,1},{22,2},{24,4},... k_max doubles every 2 bits
+  kmax = 1ULL << ((bits - 20) / 2);
+  if (k > kmax) {
+    fprintf(stderr, "[E] k value %llu is too large for n 0x%llx (max %llu)\n", (unsigned long long)k,
+            (unsigned long long)n, (unsigned long long)kmax);
+    return false;
+  }
+  return true;
+}
+
+// ---------------------------------------------------------------------------------------------
+// stats (keyhunt.cpp:2850-2962)
+// ---------------------------------------------------------------------------------------------
+void print_stats(uint64_t secs, const U &total) {
+  static const char *pfx[7] = {"Mkeys/s", "Gkeys/s", "Tkeys/s", "Pkeys/s", "Ekeys/s", "Zkeys/s", "Ykeys/s"};
+  uint64_t rem;
+  U per = u_divmod_u64(total, secs ? secs : 1, &rem);
+  U lim[7];
+  U l = u_from_u64(1000000);
+  for (int i = 0; i < 7; i++) {
+    lim[i] = l;
+    l = u_mul_u64(l, 1000);
+  }
+  if (u_cmp(per, lim[0]) < 0) {
+    printf("\r[+] Total %s keys in %llu seconds: %s keys/s\r", u_dec(total).c_str(), (unsigned long long)secs,
+           u_dec(per).c_str());
+  } else {
+    int i = 0;
+    while (i < 6 && u_cmp(per, lim[i + 1]) >= 0) i++;
+    uint64_t div = 1;
+    for (int k = 0; k < 6 + 3 * i && k < 18; k++) div *= 10;
+    U d = per;
+    for (int k = 0; k < i; k++) d = u_divmod_u64(d, 1000, nullptr);
+    d = u_divmod_u64(d, 1000000, nullptr);
+    printf("\r[+] Total %s keys in %llu seconds: ~%s %s (%s keys/s)\r", u_dec(total).c_str(),
+           (unsigned long long)secs, u_dec(d).c_str(), pfx[i], u_dec(per).c_str());
+  }
+  fflush(stdout);
+}
+
+U keys_done(const U &twoN) {
+  if (opt.mode == MODE_BSGS) {
+    U t = u_mul_u64(twoN, g_bases_done.load());
+    return t;
+  }
+  U t = u_mul_u64(u_from_u64(1024), g_groups_done.load());
+  if (opt.search == KH_SEARCH_COMPRESS) t = u_mul_u64(t, 2);
+  return t;
+}
+
+// ---------------------------------------------------------------------------------------------
+// workers
+// ---------------------------------------------------------------------------------------------
+struct addr_job {
+  int device;
+  const std::vector<uint8_t> *rows;
+  uint64_t bloom_items;
+  uint64_t nseq;
+  int rc = 0;
+};
+
+void addr_worker(addr_job *j) {
+  kh_ctx *ctx = nullptr;
+  int r = kh_open(j->device, &ctx);
+  if (r) {
+    fprintf(stderr, "[E] GPU %d: %s\n", j->device, kh_strerror(r));
+    j->rc = r;
+    g_running--;
+    return;
+  }
+  r = kh_set_targets(ctx, j->rows->data(), j->rows->size() / 20, j->bloom_items);
+  std::vector<kh_hit> hits(1 << 12);
+  uint8_t st_be[32], stride_be[32];
+  u_to_be32(opt.stride, stride_be);
+  const U span = u_mul_u64(opt.stride, j->nseq);
+  while (!r) {
+    U base;
+    {
+      std::lock_guard<std::mutex> lk(g_cursor_mtx);
+      if (u_cmp(g_cursor, g_end) >= 0) break;
+      base = g_cursor;
+      g_cursor = u_add(g_cursor, span);
+    }
+    if (opt.matrix) printf("Base key: %s gpu %d\n", u_hex(base).c_str(), j->device);
+    u_to_be32(base, st_be);
+    uint32_t nh = 0;
+    r = kh_scan(ctx, st_be, stride_be, j->nseq, opt.mode == MODE_XPOINT ? KH_MODE_XPOINT : KH_MODE_ADDRESS,
+                (uint32_t)opt.search, hits.data(), (uint32_t)hits.size(), &nh);
+    if (r) {
+      fprintf(stderr, "[E] kh_scan: %s (%s)\n", kh_strerror(r), kh_last_error(ctx));
+      break;
+    }
+    for (uint32_t i = 0; i < nh; i++) writekey(ctx, hits[i].compressed != 0, hits[i].key);
+    g_groups_done += j->nseq / 1024;
+  }
+  j->rc = r;
+  kh_close(ctx);
+  g_running--;
+}
+
+struct bsgs_job {
+  int device;
+  const std::vector<fe> *tx, *ty;
+  const std::vector<bool> *comp;
+  uint64_t n, k;
+  uint64_t bases_per_call;
+  int rc = 0;
+};
+std::vector<uint8_t> g_found;  // bsgs_found[]
+std::mutex g_found_mtx;
+
+void bsgs_worker(bsgs_job *j) {
+  kh_ctx *ctx = nullptr;
+  int r = kh_open(j->device, &ctx);
+  if (r) {
+    j->rc = r;
+    g_running--;
+    return;
+  }
+  kh_bsgs_info info;
+  r = kh_bsgs_setup(ctx, j->n, j->k, &info);
+  if (!r) r = kh_bsgs_build(ctx);
+  size_t nt = j->tx->size();
+  std::vector<uint8_t> xy(64 * nt);
+  for (size_t i = 0; i < nt; i++) {
+    fe_to_be(&xy[64 * i], (*j->tx)[i]);
+    fe_to_be(&xy[64 * i + 32], (*j->ty)[i]);
+  }
+  if (!r) r = kh_bsgs_set_targets(ctx, xy.data(), (uint32_t)nt);
+  const U twoN = u_mul_u64(u_from_u64(info.n), 2);
+  std::vector<kh_bsgs_found> found(nt + 1);
+  while (!r) {
+    U base;
+    uint64_t nb;
+    {
+      std::lock_guard<std::mutex> lk(g_cursor_mtx);
+      if (u_cmp(g_cursor, g_end) >= 0) break;
+      base = g_cursor;
+      // whole bases while base < end (keyhunt.cpp:4600-4617)
+      U left = u_sub(g_end, g_cursor);
+      uint64_t rem;
+      U q = u_divmod_u64(left, 1, &rem);
+      (void)q;
+      nb = 0;
+      U c = g_cursor;
+      while (nb < j->bases_per_call && u_cmp(c, g_end) < 0) {
+        c = u_add(c, twoN);
+        nb++;
+      }
+      g_cursor = c;
+    }
+    uint8_t st_be[32];
+    u_to_be32(base, st_be);
+    uint32_t nf = 0;
+    r = kh_bsgs_scan(ctx, st_be, nb, found.data(), (uint32_t)found.size(), &nf);
+    if (r) {
+      fprintf(stderr, "[E] kh_bsgs_scan: %s (%s)\n", kh_strerror(r), kh_last_error(ctx));
+      break;
+    }
+    g_bases_done += nb;
+    for (uint32_t i = 0; i < nf; i++) {
+      uint32_t t = found[i].target;
+      std::lock_guard<std::mutex> lk(g_found_mtx);
+      if (g_found[t]) continue;
+      g_found[t] = 1;
+      std::string k = u_hex(u_from_be32(found[i].key));
+      uint8_t pxy[64];
+      kh_pubkeys(ctx, found[i].key, 1, pxy);
+      std::string pub;
+      if ((*j->comp)[t]) {
+        uint8_t p = (pxy[63] & 1) ? 3 : 2;
+        pub = hex(&p, 1) + hex(pxy, 32);
+      } else {
+        uint8_t p = 4;
+        pub = hex(&p, 1) + hex(pxy, 64);
+      }
+      {
+        std::lock_guard<std::mutex> lk2(g_keys_mtx);
+        printf("[+] Thread Key found privkey %s   \n", k.c_str());
+        printf("[+] Publickey %s\n", pub.c_str());
+        FILE *f = fopen("KEYFOUNDKEYFOUND.txt", "a");
+        if (f) {
+          fprintf(f, "Key found privkey %s\nPublickey %s\n", k.c_str(), pub.c_str());
+          fclose(f);
+        }
+        fflush(stdout);
+      }
+      bool all = std::all_of(g_found.begin(), g_found.end(), [](uint8_t v) { return v != 0; });
+      if (all) {
+        printf("All points were found\n");
+        fflush(stdout);
+        _exit(EXIT_FAILURE);  // keyhunt.cpp:4811-4814
+      }
+    }
+  }
+  j->rc = r;
+  kh_close(ctx);
+  g_running--;
+}
+
+void usage(const char *p) {
+  printf("Usage: %s -m address|rmd160|xpoint|bsgs -f FILE [-b BITS | -r START:END] [-l compress|uncompress|both]\n"
+         "       [-n N] [-k K] [-I STRIDE] [-g GPUS] [-q] [-s SECONDS] [-M]\n", p);
+}
+
+}  // namespace
+
+int main(int argc, char **argv) {
+  printf("[+] Version %s\n", VERSION);
+  const char *mode_names[] = {"address", "rmd160", "xpoint", "bsgs"};
+  int c;
+  U order;
+  u_from_hex(ORDER_HEX, order);
+  while ((c = getopt(argc, argv, "m:f:l:r:b:k:n:t:g:qs:I:MRec:B:S")) != -1) {
+    switch (c) {
+      case 'm': {
+        int m = -1;
+        for (int i = 0; i < 4; i++)
+          if (!strcmp(optarg, mode_names[i])) m = i;
+        if (m < 0) {
+          fprintf(stderr, "[E] Unsupported mode %s (engine covers address, rmd160, xpoint, bsgs)\n", optarg);
+          return EXIT_FAILURE;
+        }
+        opt.mode = m;
+        printf("[+] Mode %s\n", optarg);
+        break;
+      }
+      case 'f': opt.file = optarg; break;
+      case 'l':
+        if (!strcmp(optarg, "compress")) opt.search = KH_SEARCH_COMPRESS;
+        else if (!strcmp(optarg, "uncompress")) opt.search = KH_SEARCH_UNCOMPRESS;
+        else if (!strcmp(optarg, "both")) opt.search = KH_SEARCH_BOTH;
+        else { fprintf(stderr, "[E] Unknow search type %s\n", optarg); return EXIT_FAILURE; }
+        break;
+      case 'r': {
+        std::string s(optarg);
+        size_t p = s.find(':');
+        if (p == std::string::npos || !u_from_hex(s.substr(0, p).c_str(), opt.start) ||
+            !u_from_hex(s.substr(p + 1).c_str(), opt.end)) {
+          fprintf(stderr, "[E] Invalid range %s\n", optarg);
+          return EXIT_FAILURE;
+        }
+        opt.have_range = true;
+        break;
+      }
+      case 'b':
+        opt.bits = atoi(optarg);
+        if (opt.bits > 0 && opt.bits <= 256) {
+          opt.have_bits = true;
+        } else {
+          fprintf(stderr, "[E] invalid bits param: %s.\n", optarg);
+        }
+        break;
+      case 'k': opt.kfactor = strtoull(optarg, nullptr, 10); if (!opt.kfactor) opt.kfactor = 1; printf("[+] K factor %llu\n", (unsigned long long)opt.kfactor); break;
+      case 'n': opt.flag_n = true; opt.str_n = optarg; break;
+      case 't': break;  // host threads: one per GPU here (see -g)
+      case 'g': opt.gpus = atoi(optarg); break;
+      case 'q': opt.quiet = true; printf("[+] Quiet thread output\n"); break;
+      case 's': opt.seconds = atoi(optarg); break;
+      case 'I': {
+        U s;
+        bool ok = (optarg[0] == '0' && optarg[1] == 'x') ? u_from_hex(optarg, s) : u_from_dec(optarg, s);
+        if (!ok || u_is_zero(s)) { fprintf(stderr, "[E] invalid stride %s\n", optarg); return EXIT_FAILURE; }
+        opt.stride = s;
+        break;
+      }
+      case 'M': opt.matrix = true; break;
+      case 'R': case 'e': case 'c': case 'B': case 'S':
+        fprintf(stderr, "[E] -%c is outside the scope of this engine (sequential hot path only)\n", c);
+        return EXIT_FAILURE;
+      default: usage(argv[0]); return EXIT_FAILURE;
+    }
+  }
+  if (!opt.file) {
+    fprintf(stderr, "[E] -f FILE is required\n");
+    return EXIT_FAILURE;
+  }
+  // validate_nk (keyhunt.cpp:1173-1183): applied to every mode
+  uint64_t nk_n = 0x100000000000ULL;
+  if (opt.flag_n) nk_n = (opt.str_n[0] == '0' && (opt.str_n[1] == 'x' || opt.str_n[1] == 'X')) ? strtoull(opt.str_n + 2, nullptr, 16) : strtoull(opt.str_n, nullptr, 10);
+  if (!validate_nk(nk_n, opt.kfactor)) return EXIT_FAILURE;
+  if (opt.mode == MODE_BSGS && u_cmp(opt.stride, u_from_u64(1)) != 0) {
+    fprintf(stderr, "[E] Stride doesn't work with BSGS\n");
+    return EXIT_FAILURE;
+  }
+  // ranges (keyhunt.cpp:854-873, 1221-1269)
+  if (opt.have_bits) {
+    opt.start = u_shl1(opt.bits - 1);
+    opt.end = u_shl1(opt.bits);
+    if (u_cmp(opt.end, order) > 0) opt.end = order;
+    printf("[+] Bit Range %d\n", opt.bits);
+  } else if (opt.have_range) {
+    if (u_is_zero(opt.start)) opt.start = u_from_u64(1);
+    if (u_cmp(opt.start, opt.end) == 0 || u_cmp(opt.start, order) >= 0 || u_cmp(opt.end, order) > 0) {
+      fprintf(stderr, "[E] invalid range (random mode is outside this engine's scope)\n");
+      return EXIT_FAILURE;
+    }
+    if (u_cmp(opt.start, opt.end) > 0) std::swap(opt.start, opt.end);
+    printf("[+] Range \n");
+  } else {
+    fprintf(stderr, "[E] a range (-r or -b) is required: random mode is outside this engine's scope\n");
+    return EXIT_FAILURE;
+  }
+  printf("[+] -- from : 0x%s\n[+] -- to   : 0x%s\n", u_hex(opt.start).c_str(), u_hex(opt.end).c_str());
+  int ndev = 0;
+  kh_device_count(&ndev);
+  if (ndev < 1) {
+    fprintf(stderr, "[E] no GPU found\n");
+    return EXIT_FAILURE;
+  }
+  int gpus = opt.gpus > 0 ? std::min(opt.gpus, ndev) : ndev;
+  printf("[+] GPUs : %d\n", gpus);
+  g_cursor = opt.start;
+  g_end = opt.end;
+  U twoN;
+  std::vector<std::thread> th;
+  std::vector<addr_job> aj(gpus);
+  std::vector<bsgs_job> bj(gpus);
+  std::vector<uint8_t> rows;
+  std::vector<fe> tx, ty;
+  std::vector<bool> comp;
+
+  if (opt.mode != MODE_BSGS) {
+    uint64_t nseq = 0x100000000ULL;  // N_SEQUENTIAL_MAX (keyhunt.cpp:464, 1272-1292)
+    if (opt.flag_n) {
+      nseq = nk_n;
+      if (nseq < 1024 || nseq % 1024) nseq = 0x100000000ULL;
+    }
+    printf("[+] N = %p\n", (void *)nseq);
+    uint64_t items = 0;
+    if (!read_targets(opt.file, opt.mode, rows, items)) return EXIT_FAILURE;
+    printf("[+] Sorting data ... done! %llu values were loaded and sorted\n", (unsigned long long)(rows.size() / 20));
+    g_running = gpus;
+    for (int d = 0; d < gpus; d++) {
+      aj[d].device = d;
+      aj[d].rows = &rows;
+      aj[d].bloom_items = items;
+      aj[d].nseq = nseq;
+      th.emplace_back(addr_worker, &aj[d]);
+    }
+  } else {
+    FILE *f = fopen(opt.file, "r");
+    if (!f) {
+      fprintf(stderr, "[E] Can't open file %s\n", opt.file);
+      return EXIT_FAILURE;
+    }
+    printf("[+] Opening file %s\n", opt.file);
+    char line[1024];
+    while (fgets(line, sizeof line, f)) {
+      trim(line);
+      if (strlen(line) < 66) continue;
+      char *tok = strtok(line, " \t");
+      fe x, y;
+      bool cp;
+      if (tok && parse_pubkey(tok, x, y, cp)) {
+        tx.push_back(x);
+        ty.push_back(y);
+        comp.push_back(cp);
+      } else {
+        printf("Invalid length: %s\n", tok ? tok : "");
+      }
+    }
+    fclose(f);
+    if (tx.empty()) {
+      fprintf(stderr, "[E] The file don't have any valid publickeys\n");
+      return EXIT_FAILURE;
+    }
+    printf("[+] Added %zu points from file\n", tx.size());
+    g_found.assign(tx.size(), 0);
+    // BSGS N: -n or 2^44 (keyhunt.cpp:1454-1471); the library validates sqrt / 1024 and derives M
+    uint64_t n = nk_n;
+    U diff = u_sub(opt.end, opt.start);
+    if (u_cmp(diff, u_from_u64(n)) < 0) {
+      fprintf(stderr, "[E] the given range is small\n");
+      return EXIT_FAILURE;
+    }
+    uint64_t m = 1;
+    while ((m + 1) * (m + 1) <= n) m++;
+    uint64_t M = m * opt.kfactor;
+    uint64_t Nr = (n / M) * M;
+    twoN = u_mul_u64(u_from_u64(Nr), 2);
+    printf("[+] N = 0x%llx\n", (unsigned long long)Nr);
+    g_running = gpus;
+    for (int d = 0; d < gpus; d++) {
+      bj[d].device = d;
+      bj[d].tx = &tx;
+      bj[d].ty = &ty;
+      bj[d].comp = &comp;
+      bj[d].n = n;
+      bj[d].k = opt.kfactor;
+      bj[d].bases_per_call = 64;
+      th.emplace_back(bsgs_worker, &bj[d]);
+    }
+  }
+  // stats loop (keyhunt.cpp:2850-2962)
+  uint64_t secs = 0;
+  while (g_running > 0) {
+    sleep(1);
+    secs++;
+    if (opt.seconds > 0 && secs % opt.seconds == 0) print_stats(secs, keys_done(twoN));
+  }
+  for (auto &t : th) t.join();
+  int rc = 0;
+  for (int d = 0; d < gpus; d++) rc |= (opt.mode == MODE_BSGS ? bj[d].rc : aj[d].rc);
+  printf("\nEnd\n");
+  return rc ? EXIT_FAILURE : EXIT_SUCCESS;
+}
