@@ -1,0 +1,52 @@
+"""The C ABI library loads on a CPU-only host and exports exactly what include/kh_gpu.h declares;
+host-side argument checking works without touching a GPU."""
+import ctypes
+import os
+import subprocess
+
+import pytest
+
+import keyhunt_amd
+from keyhunt_amd import engine as E
+
+
+def test_library_exports_every_header_symbol():
+    L = keyhunt_amd.lib()
+    syms = keyhunt_amd.header_symbols()
+    assert len(syms) >= 25
+    for s in syms:
+        assert hasattr(L, s), s
+
+
+def test_abi_version_and_errors():
+    L = keyhunt_amd.lib()
+    assert L.kh_abi_version() == 1
+    assert L.kh_strerror(0) == b"ok"
+    assert L.kh_strerror(-6).startswith(b"BSGS n")
+
+
+def test_null_context_is_rejected():
+    L = keyhunt_amd.lib()
+    n = ctypes.c_uint32()
+    assert L.kh_scan(None, b"\0" * 32, None, 1024, 0, 0, None, 0, ctypes.byref(n)) == -1
+    assert L.kh_bsgs_setup(None, 1 << 20, 1, None) == -1
+    assert L.kh_open(0, None) == -1
+
+
+def test_device_count_without_gpu_is_zero_or_more():
+    assert keyhunt_amd.device_count() >= 0
+
+
+def test_cli_rejects_out_of_scope_and_bad_nk(tmp_path):
+    cli = os.path.join(E.PKG, "bin", "keyhunt-amd")
+    if not os.path.exists(cli):
+        pytest.skip("CLI not built")
+    r = subprocess.run([cli, "-m", "vanity", "-f", "x"], capture_output=True, text=True)
+    assert r.returncode == 1 and "Unsupported mode" in r.stderr
+    r = subprocess.run([cli, "-m", "address", "-f", "x", "-r", "1:100000", "-n", "0x10000"], capture_output=True,
+                       text=True)
+    assert r.returncode == 1 and "n must be at least 2^20" in r.stderr
+    r = subprocess.run([cli, "-m", "bsgs", "-f", "x", "-k", "5000", "-b", "66"], capture_output=True, text=True)
+    assert r.returncode == 1 and "too large" in r.stderr
+    r = subprocess.run([cli, "-m", "address", "-f", "x", "-R"], capture_output=True, text=True)
+    assert r.returncode == 1

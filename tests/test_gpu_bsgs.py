@@ -1,0 +1,74 @@
+"""BSGS parity on the GPU: baby-step tables (three bloom layers + sorted bP table) bit-identical to
+the reference's at small M (tests/golden/ref_vectors.json), first-level candidate sets identical to
+the CPU oracle, and found keys identical to the reference CLI on known-answer windows
+(tests/golden/ref_e2e.json), including the benchmark configuration (k = 128)."""
+import hashlib
+import json
+import os
+
+import pytest
+
+from conftest import GOLDEN
+from _cli import run_cli
+
+pytestmark = pytest.mark.gpu
+VEC = json.load(open(os.path.join(GOLDEN, "ref_vectors.json")))
+E2E = json.load(open(os.path.join(GOLDEN, "ref_e2e.json")))
+
+
+@pytest.mark.parametrize("cfg", VEC["bsgs_build"], ids=lambda c: f"n{c['n']:x}_k{c['k']}")
+def test_baby_tables_match_reference(engine, cfg):
+    info = engine.bsgs_setup(cfg["n"], cfg["k"])
+    assert (info.m, info.m2, info.m3) == (cfg["m"], cfg["m2"], cfg["m3"])
+    assert list(info.bloom_bytes) == cfg["bytes"]
+    engine.bsgs_build()
+    for layer, key in ((1, "sha256_l1"), (2, "sha256_l2"), (3, "sha256_l3")):
+        assert hashlib.sha256(engine.get_bloom(layer)).hexdigest() == cfg[key], layer
+    assert hashlib.sha256(engine.get_bsgs_table()).hexdigest() == cfg["sha256_table"]
+
+
+def test_candidates_and_key_vs_oracle(engine, oracle):
+    n, k = 1 << 22, 2
+    p = oracle.bsgs_params(n, k)
+    tabs = oracle.BsgsTables(p)
+    engine.bsgs_setup(n, k)
+    engine.bsgs_build()
+    assert engine.get_bloom(1) == tabs.bf1.raw
+    assert engine.get_bloom(2) == tabs.bf2.raw
+    assert engine.get_bloom(3) == tabs.bf3.raw
+    assert engine.get_bsgs_table() == tabs.table_bytes()
+    key = 0x5A5A5A5A123456
+    q = oracle.pubkey(key)
+    start = key - 3 * 2 * p.n - 12345
+    # no hit in the first 3 bases: identical candidate counts; found in the 4th
+    engine.bsgs_set_targets([q])
+    c0 = engine.bsgs_candidates()
+    assert engine.bsgs_scan(start, 3) == []
+    got_c = engine.bsgs_candidates() - c0
+    okey, ocands = tabs.scan(start, 3, q)
+    assert okey is None and got_c == len(ocands)
+    found = engine.bsgs_scan(start + 3 * 2 * p.n, 1)
+    assert found == [(0, key)]
+    okey, _ = tabs.scan(start, 4, q)
+    assert okey == key
+
+
+BSGS_CASES = [k for k in E2E if k.startswith("bsgs")]
+
+
+@pytest.mark.parametrize("name", BSGS_CASES)
+def test_cli_bsgs_matches_reference(name):
+    ref = E2E[name]
+    argv = [a for a in ref["argv"] if a not in ("-t", "8")]
+    p, hits = run_cli(argv)
+    assert p.returncode == ref["exit"], p.stdout[-2000:] + p.stderr[-2000:]
+    assert hits == ref["hits"]
+
+
+def test_bench_config_k128_known_answer():
+    """configs[3] geometry (-k 128, N = 2^44, M = 2^29: 1.84 GB layer-1 bloom) on a window that holds
+    puzzle 125's key (verified by the reference)."""
+    p, hits = run_cli(["-m", "bsgs", "-f", "125.txt", "-k", "128", "-r",
+                       "1c533b6bb7f0804e0995fe0000000000:1c533b6bb7f0804e09963e0000000000"], timeout=900)
+    assert p.returncode == 1, p.stdout[-2000:] + p.stderr[-2000:]
+    assert [h["key"] for h in hits] == ["1c533b6bb7f0804e09960225e44877ac"]

@@ -1,0 +1,148 @@
+"""The CPU oracle (oracle/kh_oracle.c) pinned against the reference: primitive vectors printed by the
+reference's own code (tests/golden/ref_vectors.json) and the reference CLI's hit sets on
+known-answer windows (tests/golden/ref_e2e.json)."""
+import hashlib
+import json
+import os
+import random
+
+import pytest
+
+from conftest import GOLDEN
+
+VEC = json.load(open(os.path.join(GOLDEN, "ref_vectors.json")))
+E2E = json.load(open(os.path.join(GOLDEN, "ref_e2e.json")))
+P = 2**256 - 2**32 - 977
+
+
+def h(x):
+    return int(x, 16)
+
+
+def test_field_vs_reference(oracle):
+    for v in VEC["field"]:
+        a, b = h(v["a"]), h(v["b"])
+        assert oracle.fe_mul(a, b) == h(v["mul"]) % P
+        assert oracle.fe_mul(a, a) == h(v["sqr"]) % P
+        assert oracle.fe_inv(a) == h(v["inv"])
+
+
+def test_pubkeys_and_hash160_vs_reference(oracle):
+    for v in VEC["pubkeys"]:
+        x, y = oracle.pubkey(h(v["k"]))
+        assert (x, y) == (h(v["x"]), h(v["y"]))
+        assert oracle.hash160_comp(x, 2).hex() == v["h02"]
+        assert oracle.hash160_comp(x, 3).hex() == v["h03"]
+        assert oracle.hash160_uncomp(x, y).hex() == v["h04"]
+        assert oracle.decompress(x, y & 1) == y
+
+
+def test_xxh64_vs_reference(oracle):
+    for v in VEC["xxh64"]:
+        buf = bytes.fromhex(v["buf"])
+        a = oracle.xxh64(buf, 0x59F2815B16F81798)
+        assert a == h(v["a"])
+        assert oracle.xxh64(buf, a) == h(v["b"])
+
+
+def test_bloom_sizing_vs_reference(oracle):
+    for v in VEC["bloom_params"]:
+        assert oracle.bloom_params(v["entries"]) == (v["bits"], v["bytes"], v["hashes"])
+
+
+def test_bloom_fill_vs_reference(oracle):
+    fill = VEC["bloom_fill"]
+    b = oracle.Bloom(fill["entries"])
+    items = [bytes.fromhex(x) for x in fill["items"]]
+    for it in items:
+        b.add(it)
+    assert hashlib.sha256(b.raw()).hexdigest() == fill["sha256"]
+    assert all(b.check(it) for it in items)
+
+
+def test_group_walk_vs_reference(oracle):
+    for gw in VEC["group_walk"]:
+        xs, _ = oracle.walk_points(h(gw["start"]), gw["n"] // 1024)
+        assert hashlib.sha256(xs).hexdigest() == gw["sha256_walk"] == gw["sha256_direct"]
+
+
+@pytest.mark.parametrize("cfg", VEC["bsgs_build"][:2], ids=lambda c: f"n{c['n']:x}_k{c['k']}")
+def test_bsgs_build_vs_reference(oracle, cfg):
+    p = oracle.bsgs_params(cfg["n"], cfg["k"])
+    assert (p.m, p.m2, p.m3) == (cfg["m"], cfg["m2"], cfg["m3"])
+    t = oracle.BsgsTables(p)
+    assert hashlib.sha256(t.bf1.raw).hexdigest() == cfg["sha256_l1"]
+    assert hashlib.sha256(t.bf2.raw).hexdigest() == cfg["sha256_l2"]
+    assert hashlib.sha256(t.bf3.raw).hexdigest() == cfg["sha256_l3"]
+    assert hashlib.sha256(t.table_bytes()).hexdigest() == cfg["sha256_table"]
+
+
+def test_bsgs_params_configs(oracle):
+    """BASELINE configs 4/5 geometry."""
+    p = oracle.bsgs_params(2**44, 128)
+    assert (p.m, p.m2, p.m3, p.cycles) == (2**29, 2**24, 2**19, 32)
+    assert (p.bits[0], p.bytes[0], p.hashes[0]) == (60303973, 7537997, 20)
+    assert (p.bytes[1], p.bytes[2]) == (235563, 35944)
+    p = oracle.bsgs_params(2**44, 512)
+    assert (p.m, p.m2, p.m3, p.cycles) == (2**31, 2**26, 2**21, 8)
+    assert (p.bytes[0], p.bytes[1]) == (30151987, 942250)
+
+
+def _read_rows(oracle, fn, mode):
+    from conftest import DATA
+    rows = []
+    for line in open(os.path.join(DATA, fn)):
+        s = line.strip()
+        if mode == "xpoint":
+            if len(s) == 66:
+                rows.append(bytes.fromhex(s[2:])[:20])
+            continue
+        if len(s) == 40:
+            rows.append(bytes.fromhex(s))
+        elif 20 < len(s) < 40:
+            raw = oracle.address_decode(s)
+            if raw:
+                rows.append(raw[1:21])
+    return rows
+
+
+@pytest.mark.parametrize("name,fn,mode,search", [
+    ("rmd160_1to32_compress_2p20", "1to32.rmd", 0, 0),
+    ("xpoint_1to63_65_2p20", "1to63_65.txt", 1, 2),
+])
+def test_oracle_scan_vs_reference_cli(oracle, name, fn, mode, search):
+    """Keys 1..2^20 (one 2^20 chunk): the oracle's hit list equals the reference CLI's."""
+    rows = _read_rows(oracle, fn, "xpoint" if mode == 1 else "addr")
+    hits = oracle.scan_chunk(mode, search, 1, 1 << 20, rows)
+    assert [f"{k:x}" for k in sorted(k for k, _, _ in hits)] == [x["key"] for x in E2E[name]["hits"]]
+
+
+def test_oracle_scan_window_66(oracle):
+    rows = _read_rows(oracle, "66.rmd", "addr")
+    start = 0x2832ED74F2B5E0000
+    hits = oracle.scan_chunk(0, 0, start, 1 << 16, rows)
+    assert [(f"{k:x}", c) for k, c, _ in hits] == [("2832ed74f2b5e35ee", True)]
+    assert [x["key"] for x in E2E["rmd160_66_window"]["hits"]] == ["2832ed74f2b5e35ee"]
+
+
+def test_oracle_bsgs_known_answer_small_n(oracle):
+    """-m bsgs -f 63.pub -n 0x1000000 -k 4 -r 7cce5efdac000000:7cce5efdad000000 (reference: found)."""
+    p = oracle.bsgs_params(1 << 24, 4)
+    t = oracle.BsgsTables(p)
+    q = oracle.parse_pubkey_hex(open(os.path.join(GOLDEN, "data", "63.pub")).read().split()[0])
+    key, cands = t.scan(0x7CCE5EFDAC000000, 1, q)
+    assert f"{key:x}" == E2E["bsgs_63_small_n_k4"]["hits"][0]["key"]
+    assert len(cands) >= 1
+
+
+def test_searchbinary_is_membership(oracle):
+    """keyhunt's midpoint loop (keyhunt.cpp:3065-3089) answers exact membership on sorted tables."""
+    rng = random.Random(3)
+    for n in list(range(1, 40)) + [100, 1000, 4097]:
+        rows = sorted({rng.getrandbits(160).to_bytes(20, "big") for _ in range(n)})
+        table = b"".join(rows)
+        for r in rows:
+            assert oracle.searchbinary(table, len(rows), r)
+        for _ in range(50):
+            q = rng.getrandbits(160).to_bytes(20, "big")
+            assert oracle.searchbinary(table, len(rows), q) == (q in set(rows))
