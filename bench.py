@@ -1,0 +1,264 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X keyhunt engine -- one JSON line on rank 0.
+
+Metric (BASELINE.json): "Mkeys/s at 1/2/4/8 GPU (BSGS b125; addr b66); HBM GB/s fraction".
+  primary   : -m bsgs -f tests/125.txt -b 125 -k 128  (configs[3]).  A step = one kh_bsgs_scan over
+              BASES consecutive bases of 2N keys (N = 2^44) for the puzzle-125 public key, i.e.
+              BASES x 32768 giant-step points probed against the 1.84 GB layer-1 bloom, plus the
+              host refinement of every first-level candidate.  Keys counted as the reference does
+              (2N per base, keyhunt.cpp:4883-4884 / 2871-2874).
+  secondary : -m rmd160 -f tests/66.rmd -b 66 -l compress (configs[1]).  A step = one 2^32-key
+              N_SEQUENTIAL_MAX chunk; keys counted x2 for -l compress (keyhunt.cpp:2889-2891).
+Ranks split the keyspace (weak scaling, no collective on the data path): rank r of N walks chunk /
+base-batch s*N + r.  The table build (baby steps) is replicated per GPU and not timed; its time is
+reported.  torch.distributed (gloo, CPU tensors) provides the barrier and the max over ranks; the
+engine owns the GPU through its own HIP stream, synchronised on both sides of the timed region.
+
+roofline: dominant kernel = the BSGS giant-step walk.  achieved = algorithmic bytes per launch
+(128 B per giant point: ~2 random 64-B bloom lines per reference-layout probe) / mean
+launch time from HIP events recorded by the engine on its own stream.  traffic: HBM bytes per launch
+from rocprofv3 PMC (profiles/), or null.
+cpu_baseline: rank 0 at N=1 only.  BSGS: the oracle's restatement of the giant-step loop
+(oracle/kh_oracle.c, keyhunt.cpp:4644-4880) on all host threads against the same GPU-built bloom
+(kind "port").  rmd160: the reference binary built from its own sources (oracle/_ref/keyhunt, kind
+"reference") on all host threads for ~20 s.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import re
+import shutil
+import subprocess
+import sys
+import tempfile
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "Mkeys/s at 1/2/4/8 GPU (BSGS b125; addr b66); HBM GB/s fraction"
+HBM_PEAK_GBS = 8000.0
+ALGO_BYTES_PER_GIANT_POINT = 128
+PUZZLE125 = "0233709eb11e0d4439a729f21c2c443dedb727528229713f0065721ba8fa46f00e"
+PUZZLE66_RMD = "20d45a6a762535700ce9e0b216e31994335db8a5"
+P = 2**256 - 2**32 - 977
+
+
+def decompress(s: str) -> tuple[int, int]:
+    x = int(s[2:], 16)
+    y = pow((x * x * x + 7) % P, (P + 1) // 4, P)
+    if (y & 1) != (int(s[:2], 16) & 1):
+        y = P - y
+    return x, y
+
+
+class Dist:
+    def __init__(self):
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.local = int(os.environ.get("LOCAL_RANK", str(self.rank)))
+        self.pg = None
+        if self.world > 1:
+            import torch
+            import torch.distributed as dist
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
+            self.torch, self.dist = torch, dist
+
+    def barrier(self):
+        if self.world > 1:
+            self.dist.barrier()
+
+    def max(self, v: float) -> float:
+        if self.world == 1:
+            return v
+        t = self.torch.tensor([v], dtype=self.torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum(self, v: float) -> float:
+        if self.world == 1:
+            return v
+        t = self.torch.tensor([v], dtype=self.torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        return float(t.item())
+
+    def close(self):
+        if self.world > 1:
+            self.dist.destroy_process_group()
+
+
+def timed(D: Dist, eng, warmup: int, steps: int, step_fn):
+    for s in range(warmup):
+        step_fn(s)
+    eng.synchronize()
+    D.barrier()
+    eng.kernel_time_reset()
+    t0 = time.perf_counter()
+    for s in range(steps):
+        step_fn(warmup + s)
+    eng.synchronize()
+    t1 = time.perf_counter()
+    D.barrier()
+    return D.max(t1 - t0)
+
+
+def bsgs_leg(D: Dist, eng, args):
+    import keyhunt_amd as K
+    info = eng.bsgs_setup(1 << 44, 128)
+    t = time.perf_counter()
+    eng.bsgs_build()
+    eng.synchronize()
+    build_s = time.perf_counter() - t
+    q = decompress(PUZZLE125)
+    eng.bsgs_set_targets([q])
+    two_n = 2 * info.n
+    base0 = 1 << 124
+    B = args.bases
+
+    def step(s):
+        batch = s * D.world + D.rank
+        found = eng.bsgs_scan(base0 + batch * B * two_n, B)
+        assert not found  # puzzle 125's key lies far from the start of the range
+
+    T = timed(D, eng, args.warmup, args.steps, step)
+    la, ms, pts = eng.kernel_time(K.engine.TIME_BSGS)
+    keys = D.world * args.steps * B * two_n
+    pts_launch = pts / la
+    ms_launch = ms / la
+    achieved = pts_launch * ALGO_BYTES_PER_GIANT_POINT / (ms_launch / 1e3) / 1e9
+    res = {
+        "value": keys / T / 1e6,
+        "ms_per_step": T / args.steps * 1e3,
+        "giant_points_per_s": D.world * args.steps * B * info.cycles * 1024 / T,
+        "build_seconds": build_s,
+        "candidates": eng.bsgs_candidates(),
+        "info": info,
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": "k_walk<KM_BSGS>", "launches": la, "mean_launch_ms": ms_launch,
+                     "giant_points_per_launch": pts_launch,
+                     "algorithmic_bytes_per_giant_point": ALGO_BYTES_PER_GIANT_POINT},
+        "q": q,
+    }
+    return res
+
+
+def rmd160_leg(D: Dist, eng, args):
+    import keyhunt_amd as K
+    eng.set_targets([bytes.fromhex(PUZZLE66_RMD)], bloom_items=1)
+    chunk = 1 << 32
+    base0 = 1 << 65
+
+    def step(s):
+        c = s * D.world + D.rank
+        hits = eng.scan(base0 + c * chunk, chunk, K.KH_MODE_ADDRESS, K.KH_SEARCH_COMPRESS)
+        assert not hits
+
+    T = timed(D, eng, args.warmup_rmd, args.steps_rmd, step)
+    la, ms, pts = eng.kernel_time(K.engine.TIME_ADDRESS)
+    keys = D.world * args.steps_rmd * chunk * 2
+    return {"value": keys / T / 1e6, "ms_per_step": T / args.steps_rmd * 1e3,
+            "kernel": {"name": "k_walk<KM_H160C>", "launches": la, "mean_launch_ms": ms / la,
+                       "points_per_launch": pts / la, "points_per_s_in_kernel": pts / (ms / 1e3)}}
+
+
+def cpu_threads() -> int:
+    try:
+        return max(1, min(16, len(os.sched_getaffinity(0))))
+    except Exception:
+        return max(1, min(16, os.cpu_count() or 1))
+
+
+def cpu_baseline_bsgs(eng, info, q, seconds: float):
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle
+    bf1 = eng.get_bloom(1)
+    p = oracle.bsgs_params(1 << 44, 128)
+    thr = cpu_threads()
+    t = time.perf_counter()
+    oracle.bsgs_giant_probe(p, bf1, q, 4, thr)
+    cal = time.perf_counter() - t
+    groups = max(4, int(4 * seconds / max(cal, 1e-3)))
+    t = time.perf_counter()
+    oracle.bsgs_giant_probe(p, bf1, q, groups, thr)
+    dt = time.perf_counter() - t
+    pts = thr * groups * 1024
+    return {"value": pts * 2 * info.m / dt / 1e6, "unit": "Mkeys/s", "cores": thr, "kind": "port",
+            "sample": f"{pts} giant-step points ({groups} 1024-point groups x {thr} threads) probed against the "
+                      f"GPU-built k=128 layer-1 bloom, {dt:.1f} s; keys = points x 2M",
+            "giant_points_per_s": pts / dt}
+
+
+def cpu_baseline_rmd160(seconds: int):
+    ref = os.path.join(REPO, "oracle", "_ref", "keyhunt")
+    if not os.path.exists(ref):
+        return None
+    thr = cpu_threads()
+    with tempfile.TemporaryDirectory() as td:
+        shutil.copy(os.path.join(REPO, "tests", "golden", "data", "66.rmd"), td)
+        p = subprocess.run(["timeout", str(seconds), ref, "-m", "rmd160", "-f", "66.rmd", "-b", "66", "-l", "compress",
+                            "-t", str(thr), "-s", "5", "-q"], cwd=td, capture_output=True, text=True)
+    rates = re.findall(r"Total (\d+) keys in (\d+) seconds", p.stdout)
+    if not rates:
+        return None
+    keys, secs = map(int, rates[-1])
+    return {"value": keys / secs / 1e6, "unit": "Mkeys/s", "cores": thr, "kind": "reference",
+            "sample": f"oracle/_ref/keyhunt -m rmd160 -f 66.rmd -b 66 -l compress -t {thr}: {keys} keys in {secs} s "
+                      f"(reference's own stats line)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--bases", type=int, default=16384, help="BSGS bases (of 2N keys) per step per GPU")
+    ap.add_argument("--steps-rmd", type=int, default=None)
+    ap.add_argument("--warmup-rmd", type=int, default=None)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true")
+    args = ap.parse_args()
+    args.steps_rmd = args.steps if args.steps_rmd is None else args.steps_rmd
+    args.warmup_rmd = args.warmup if args.warmup_rmd is None else args.warmup_rmd
+
+    import keyhunt_amd as K
+    D = Dist()
+    eng = K.Engine(D.local)
+    prim = bsgs_leg(D, eng, args)
+    sec = None if args.no_secondary else rmd160_leg(D, eng, args)
+    cpu_b = cpu_r = None
+    if D.rank == 0 and D.world == 1 and not args.no_cpu_baseline:
+        cpu_b = cpu_baseline_bsgs(eng, prim["info"], prim["q"], args.cpu_seconds)
+        cpu_r = cpu_baseline_rmd160(int(args.cpu_seconds + 5))
+    eng.close()
+    D.barrier()
+    if D.rank == 0:
+        info = prim["info"]
+        line = {
+            "metric": METRIC, "value": prim["value"], "unit": "Mkeys/s", "n_gpus": D.world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": prim["ms_per_step"], "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic: puzzle-125 public key (tests/125.txt), sequential bases from 2^124",
+            "config": {"workload": "-m bsgs -f tests/125.txt -b 125 -k 128", "n": info.n, "k": 128, "m": info.m,
+                       "bases_per_step": args.bases, "giant_points_per_step": args.bases * info.cycles * 1024,
+                       "parallelism": f"keyspace split x{D.world} (no collective)"},
+            "giant_points_per_s": prim["giant_points_per_s"],
+            "build_seconds": prim["build_seconds"],
+            "first_level_candidates": prim["candidates"],
+            "roofline": prim["roofline"],
+            "cpu_baseline": cpu_b,
+        }
+        if sec:
+            line["secondary"] = {"workload": "-m rmd160 -f tests/66.rmd -b 66 -l compress", "value": sec["value"],
+                                 "unit": "Mkeys/s", "ms_per_step": sec["ms_per_step"], "steps": args.steps_rmd,
+                                 "kernel": sec["kernel"], "cpu_baseline": cpu_r}
+        print(json.dumps(line), flush=True)
+    D.close()
+
+
+if __name__ == "__main__":
+    main()
