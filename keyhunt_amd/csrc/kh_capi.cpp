@@ -10,7 +10,9 @@
 #include <string.h>
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <mutex>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -319,6 +321,16 @@ struct kh_ctx {
   hipEvent_t ev_a = nullptr, ev_b = nullptr;
   timing tm[5];
 
+  // pipelined BSGS rounds: double-buffered hit buffers, pinned host mirrors, host scalar arrays
+  uint32_t *d_cnt2[2] = {nullptr, nullptr};
+  kh_dev_hit *d_hits2[2] = {nullptr, nullptr};
+  uint32_t *h_cnt2[2] = {nullptr, nullptr};
+  kh_dev_hit *h_hits2[2] = {nullptr, nullptr};
+  uint32_t *h_scal2[2] = {nullptr, nullptr};
+  uint32_t h_scal_cap = 0;
+  hipEvent_t ev_round[2][4] = {{nullptr, nullptr, nullptr, nullptr}, {nullptr, nullptr, nullptr, nullptr}};
+  unsigned refine_threads = 0;
+
   ~kh_ctx();
 };
 
@@ -344,6 +356,15 @@ kh_ctx::~kh_ctx() {
   (void)hipFree(d_hits);
   (void)hipFree(d_tbloom);
   for (int i = 0; i < 3; i++) (void)hipFree(d_bl[i]);
+  for (int i = 0; i < 2; i++) {
+    (void)hipFree(d_cnt2[i]);
+    (void)hipFree(d_hits2[i]);
+    if (h_cnt2[i]) (void)hipHostFree(h_cnt2[i]);
+    if (h_hits2[i]) (void)hipHostFree(h_hits2[i]);
+    if (h_scal2[i]) (void)hipHostFree(h_scal2[i]);
+    for (int j = 0; j < 4; j++)
+      if (ev_round[i][j]) (void)hipEventDestroy(ev_round[i][j]);
+  }
   if (ev_a) (void)hipEventDestroy(ev_a);
   if (ev_b) (void)hipEventDestroy(ev_b);
   if (stream) (void)hipStreamDestroy(stream);
@@ -969,6 +990,39 @@ bool second_check(const kh_ctx *c, const u256 &base, uint64_t a, const ge &Q, u2
 
 }  // namespace
 
+namespace {
+
+int ensure_pipeline(kh_ctx *c, uint32_t L) {
+  for (int i = 0; i < 2; i++) {
+    if (!c->d_cnt2[i]) {
+      HIPCHK(c, hipMalloc(&c->d_cnt2[i], 4));
+      HIPCHK(c, hipMalloc(&c->d_hits2[i], (size_t)c->hit_cap * sizeof(kh_dev_hit)));
+      HIPCHK(c, hipHostMalloc(&c->h_cnt2[i], 4, hipHostMallocDefault));
+      HIPCHK(c, hipHostMalloc(&c->h_hits2[i], (size_t)c->hit_cap * sizeof(kh_dev_hit), hipHostMallocDefault));
+      for (int j = 0; j < 4; j++) HIPCHK(c, hipEventCreate(&c->ev_round[i][j]));
+    }
+  }
+  if (L > c->h_scal_cap) {
+    for (int i = 0; i < 2; i++) {
+      if (c->h_scal2[i]) (void)hipHostFree(c->h_scal2[i]);
+      c->h_scal2[i] = nullptr;
+      HIPCHK(c, hipHostMalloc(&c->h_scal2[i], (size_t)L * 32, hipHostMallocDefault));
+    }
+    c->h_scal_cap = L;
+  }
+  return ensure_lanes(c, L);
+}
+
+struct bsgs_round {
+  uint64_t t_round;  // first giant index of the round
+  uint32_t L;
+  uint64_t gpl;
+  uint32_t launches;
+  uint64_t points;
+};
+
+}  // namespace
+
 int kh_bsgs_scan(kh_ctx *ctx, const uint8_t start[32], uint64_t n_bases, kh_bsgs_found *found, uint32_t cap,
                  uint32_t *n_found) {
   if (!ctx || !start || !n_found) return KH_E_ARG;
@@ -983,31 +1037,62 @@ int kh_bsgs_scan(kh_ctx *ctx, const uint8_t start[32], uint64_t n_bases, kh_bsgs
   const uint32_t *tab = nullptr;
   int r = get_table(ctx, sc_neg(u256_u64(2 * I.m)), &tab);
   if (r) return r;
+  if (!ctx->refine_threads) {
+    unsigned hw = std::thread::hardware_concurrency();
+    ctx->refine_threads = std::max(1u, std::min(16u, hw ? hw : 4u));
+  }
   uint32_t nf = 0;
-  int rc = KH_OK;
+  const uint32_t per_launch = ctx->groups_per_launch ? ctx->groups_per_launch : 8;
   for (uint32_t tgt = 0; tgt < ctx->targets.size(); tgt++) {
     if (ctx->found[tgt]) continue;
-    const ge &Q = ctx->targets[tgt];
-    // giant points of this call: t in [0, n_bases*A); t -> base b = t / A, a = t % A.
-    // A lane's run of gpl groups never crosses a base: gpl divides `cycles`.
-    uint64_t total_groups = n_bases * I.cycles;
+    const ge Q = ctx->targets[tgt];
+    // giant points of this call: t in [0, n_bases*A); t -> base b = t / A, a = t % A.  A lane's
+    // run of gpl groups never crosses a base (gpl divides `cycles`).  Rounds are pipelined: the
+    // GPU walks round r+1 while the host refines round r's first-level candidates.
+    const uint64_t total_groups = n_bases * I.cycles;
+    const uint64_t round_max = (uint64_t)ctx->lanes_max * I.cycles;
+    uint64_t g0 = 0;
+    int cur = 0, pending = -1;
+    bsgs_round rounds[2];
     bool done = false;
-    uint64_t g0 = 0;  // first group of this round
-    while (g0 < total_groups && !done) {
-      uint64_t round_groups = std::min<uint64_t>(total_groups - g0, (uint64_t)ctx->lanes_max * I.cycles);
-      job_geom jg = plan(ctx, round_groups, I.cycles);
-      uint64_t t_round = g0 * 2 * H;
-      std::vector<u256> s(jg.L);
+    uint32_t Qw[16];
+    memcpy(Qw, Q.x.d, 32);
+    memcpy(Qw + 8, Q.y.d, 32);
+    uint32_t *dq = nullptr;
+    HIPCHK(ctx, hipMalloc(&dq, 64));
+    HIPCHK(ctx, hipMemcpy(dq, Qw, 64, hipMemcpyHostToDevice));
+    auto enqueue = [&](int slot) -> int {
+      uint64_t rg = std::min<uint64_t>(total_groups - g0, round_max);
+      job_geom jg = plan(ctx, rg, I.cycles);
+      bsgs_round &R = rounds[slot];
+      R.t_round = g0 * 2 * H;
+      R.L = jg.L;
+      R.gpl = jg.gpl;
+      int rr = ensure_pipeline(ctx, jg.L);
+      if (rr) return rr;
+      uint32_t *hs = ctx->h_scal2[slot];
       for (uint32_t g = 0; g < jg.L; g++) {
-        uint64_t t0 = t_round + (uint64_t)g * jg.gpl * 2 * H;
+        uint64_t t0 = R.t_round + (uint64_t)g * jg.gpl * 2 * H;
         uint64_t b = t0 / A_pts, a0 = t0 % A_pts;
         // centre key: base_b + M + 2M*(a0 + H); lane centre = Q - key*G
         u256 kb = sc_add(st, sc_reduce(u256_from_u128((u128)b * 2 * I.n)));
         kb = sc_add(kb, sc_reduce(u256_from_u128((u128)I.m + (u128)2 * I.m * (a0 + H))));
-        s[g] = sc_neg(kb);
+        u256_to_limbs(hs + (size_t)g * 8, sc_neg(kb));
       }
-      r = run_setup(ctx, s, &Q);
-      if (r) return r;
+      HIPCHK(ctx, hipMemcpyAsync(ctx->d_scalars, hs, (size_t)jg.L * 32, hipMemcpyHostToDevice, ctx->stream));
+      setup_args S;
+      memset(&S, 0, sizeof S);
+      S.scalars = ctx->d_scalars;
+      S.comb = ctx->d_comb;
+      S.q = dq;
+      S.has_q = 1;
+      S.L = jg.L;
+      S.cx = ctx->d_cx;
+      S.cy = ctx->d_cy;
+      HIPCHK(ctx, hipEventRecord(ctx->ev_round[slot][0], ctx->stream));
+      HIPCHK(ctx, launch_setup(S, ctx->stream));
+      HIPCHK(ctx, hipEventRecord(ctx->ev_round[slot][1], ctx->stream));
+      HIPCHK(ctx, hipMemsetAsync(ctx->d_cnt2[slot], 0, 4, ctx->stream));
       walk_args Aw;
       memset(&Aw, 0, sizeof Aw);
       Aw.tab = tab;
@@ -1016,43 +1101,111 @@ int kh_bsgs_scan(kh_ctx *ctx, const uint8_t start[32], uint64_t n_bases, kh_bsgs
       Aw.scratch = ctx->d_scratch;
       Aw.L = jg.L;
       Aw.lane_stride = jg.gpl * 2 * H;
-      Aw.n_points = round_groups * 2 * H;
+      Aw.n_points = rg * 2 * H;
       Aw.bloom = ctx->d_bl[0];
       Aw.bd = ctx->bd[0];
-      Aw.hit_count = ctx->d_hit_count;
-      Aw.hits = ctx->d_hits;
+      Aw.hit_count = ctx->d_cnt2[slot];
+      Aw.hits = ctx->d_hits2[slot];
       Aw.hit_cap = ctx->hit_cap;
-      HIPCHK(ctx, hipMemsetAsync(ctx->d_hit_count, 0, 4, ctx->stream));
-      r = run_walk(ctx, KM_BSGS, 2, Aw, jg.gpl, 8);
-      if (r) return r;
-      uint32_t nd = 0;
-      r = fetch_hits(ctx, nd);
-      if (r) return r;
-      std::vector<kh_dev_hit> dh(ctx->h_hits.begin(), ctx->h_hits.begin() + nd);
+      R.launches = 0;
+      R.points = 0;
+      for (uint64_t gb = 0; gb < jg.gpl; gb += per_launch) {
+        Aw.group_base = gb;
+        Aw.groups = (uint32_t)std::min<uint64_t>(per_launch, jg.gpl - gb);
+        HIPCHK(ctx, launch_walk(KM_BSGS, Aw, ctx->stream));
+        R.launches++;
+        R.points += (uint64_t)jg.L * Aw.groups * 2 * H;
+      }
+      HIPCHK(ctx, hipEventRecord(ctx->ev_round[slot][2], ctx->stream));
+      HIPCHK(ctx, hipMemcpyAsync(ctx->h_cnt2[slot], ctx->d_cnt2[slot], 4, hipMemcpyDeviceToHost, ctx->stream));
+      HIPCHK(ctx, hipMemcpyAsync(ctx->h_hits2[slot], ctx->d_hits2[slot], (size_t)ctx->hit_cap * sizeof(kh_dev_hit),
+                                 hipMemcpyDeviceToHost, ctx->stream));
+      HIPCHK(ctx, hipEventRecord(ctx->ev_round[slot][3], ctx->stream));
+      g0 += rg;
+      return KH_OK;
+    };
+    // wait for round `slot`, account its time, refine its candidates in parallel
+    auto finish = [&](int slot) -> int {
+      bsgs_round &R = rounds[slot];
+      // ev[3] follows the walk and the candidate copies of this round only
+      HIPCHK(ctx, hipEventSynchronize(ctx->ev_round[slot][3]));
+      float ms_setup = 0, ms_walk = 0;
+      (void)hipEventElapsedTime(&ms_setup, ctx->ev_round[slot][0], ctx->ev_round[slot][1]);
+      (void)hipEventElapsedTime(&ms_walk, ctx->ev_round[slot][1], ctx->ev_round[slot][2]);
+      ctx->tm[4].launches++;
+      ctx->tm[4].ms += ms_setup;
+      ctx->tm[4].points += R.L;
+      ctx->tm[2].launches += R.launches;
+      ctx->tm[2].ms += ms_walk;
+      ctx->tm[2].points += R.points;
+      uint32_t cnt = *ctx->h_cnt2[slot];
+      if (cnt > ctx->hit_cap) {
+        ctx->err = "device candidate buffer overflow";
+        return KH_E_OVERFLOW;
+      }
+      std::vector<kh_dev_hit> dh(ctx->h_hits2[slot], ctx->h_hits2[slot] + cnt);
       std::sort(dh.begin(), dh.end(), [](const kh_dev_hit &x, const kh_dev_hit &y) { return x.idx < y.idx; });
-      ctx->candidates += nd;
-      for (auto &h : dh) {
-        uint64_t t = t_round + h.idx;
-        uint64_t b = t / A_pts, a = t % A_pts;
-        u256 base = sc_add(st, sc_reduce(u256_from_u128((u128)b * 2 * I.n)));
-        u256 key;
-        if (second_check(ctx, base, a, Q, key)) {
+      ctx->candidates += cnt;
+      std::vector<uint8_t> ok(dh.size(), 0);
+      std::vector<u256> keys(dh.size());
+      std::atomic<size_t> next{0};
+      auto work = [&]() {
+        for (;;) {
+          size_t i = next++;
+          if (i >= dh.size()) break;
+          uint64_t t = R.t_round + dh[i].idx;
+          uint64_t b = t / A_pts, a = t % A_pts;
+          u256 base = sc_add(st, sc_reduce(u256_from_u128((u128)b * 2 * I.n)));
+          ok[i] = second_check(ctx, base, a, Q, keys[i]) ? 1 : 0;
+        }
+      };
+      unsigned nt = std::min<unsigned>(ctx->refine_threads, (unsigned)dh.size());
+      if (nt <= 1) {
+        work();
+      } else {
+        std::vector<std::thread> th;
+        for (unsigned k = 0; k < nt; k++) th.emplace_back(work);
+        for (auto &x : th) x.join();
+      }
+      for (size_t i = 0; i < dh.size(); i++)
+        if (ok[i]) {  // the first candidate (in giant-step order) that refines to a key
           ctx->found[tgt] = 1;
           if (found && nf < cap) {
             found[nf].target = tgt;
             found[nf].pad = 0;
-            u256_to_be(found[nf].key, key);
+            u256_to_be(found[nf].key, keys[i]);
           }
           nf++;
           done = true;
           break;
         }
+      return KH_OK;
+    };
+    while ((g0 < total_groups || pending >= 0) && !done) {
+      int nxt = -1;
+      if (g0 < total_groups) {
+        r = enqueue(cur);
+        if (r) {
+          (void)hipFree(dq);
+          return r;
+        }
+        nxt = cur;
+        cur ^= 1;
       }
-      g0 += round_groups;
+      if (pending >= 0) {
+        r = finish(pending);
+        if (r) {
+          (void)hipFree(dq);
+          return r;
+        }
+      }
+      pending = nxt;
     }
+    if (pending >= 0 && done) (void)hipStreamSynchronize(ctx->stream);  // drain the speculative round
+    (void)hipFree(dq);
   }
   *n_found = nf;
-  return nf > cap ? KH_E_OVERFLOW : rc;
+  return nf > cap ? KH_E_OVERFLOW : KH_OK;
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -11,6 +11,15 @@
 #define KH_WALK_H 512
 #endif
 
+// minimum waves per SIMD requested for the walk kernel: XPOINT/BSGS/BUILD modes (KH_WALK_LB) and
+// the hash160 modes (KH_WALK_LB_HASH).  256 / LB VGPRs per lane at most; see DESIGN.md.
+#ifndef KH_WALK_LB
+#define KH_WALK_LB 4
+#endif
+#ifndef KH_WALK_LB_HASH
+#define KH_WALK_LB_HASH 3
+#endif
+
 enum kh_walk_mode {
   KM_H160C = 0,   // hash160(02||X), hash160(03||X)          -l compress
   KM_H160U = 1,   // hash160(04||X||Y)                       -l uncompress

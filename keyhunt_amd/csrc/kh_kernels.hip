@@ -73,6 +73,22 @@ __device__ __forceinline__ bool bloom_probe(const uint8_t *__restrict__ bf, cons
   }
   return true;
 }
+// Same result, but the second hash b = XXH64(buf, a) is only computed once bit 0 (which depends on
+// a alone) is set: a negative probe usually stops there.
+template <typename HashB>
+__device__ __forceinline__ bool bloom_probe_lazy(const uint8_t *__restrict__ bf, const bloom_desc &bd, uint64_t a,
+                                                 HashB hash_b) {
+  uint64_t x = mod_bits(a, bd.bits, bd.recip);
+  if (!((bf[x >> 3] >> (x & 7)) & 1)) return false;
+  uint64_t b = hash_b(a);
+  uint64_t h = a + b;
+  for (uint32_t i = 1; i < bd.hashes; i++) {
+    x = mod_bits(h, bd.bits, bd.recip);
+    if (!((bf[x >> 3] >> (x & 7)) & 1)) return false;
+    h += b;
+  }
+  return true;
+}
 // bloom_add (bloom/bloom.cpp:122-146, add=1): set every bit with a 32-bit atomic OR
 __device__ __forceinline__ void bloom_insert(uint8_t *__restrict__ bf_base, uint64_t shard_off,
                                              const bloom_desc &bd, uint64_t a, uint64_t b) {
@@ -111,32 +127,28 @@ __device__ __forceinline__ void probe_point(const walk_args &A, const fe &x, con
       uint32_t h[5];
       hash160_comp(x, pfx, h);
       uint64_t a = xxh64_20(h, KH_BLOOM_SEED);
-      uint64_t b = xxh64_20(h, a);
-      if (bloom_probe(A.bloom, A.bd, a, b)) record_hit(A, idx, pfx - 2);
+      if (bloom_probe_lazy(A.bloom, A.bd, a, [&](uint64_t s) { return xxh64_20(h, s); })) record_hit(A, idx, pfx - 2);
     }
   }
   if constexpr (MODE == KM_H160U || MODE == KM_H160B) {
     uint32_t h[5];
     hash160_uncomp(x, y, h);
     uint64_t a = xxh64_20(h, KH_BLOOM_SEED);
-    uint64_t b = xxh64_20(h, a);
-    if (bloom_probe(A.bloom, A.bd, a, b)) record_hit(A, idx, 2);
+    if (bloom_probe_lazy(A.bloom, A.bd, a, [&](uint64_t s) { return xxh64_20(h, s); })) record_hit(A, idx, 2);
   }
   if constexpr (MODE == KM_XPOINT) {
     uint32_t w[5];
 #pragma unroll
     for (int j = 0; j < 5; j++) w[j] = bswap32(x.d[7 - j]);
     uint64_t a = xxh64_20(w, KH_BLOOM_SEED);
-    uint64_t b = xxh64_20(w, a);
-    if (bloom_probe(A.bloom, A.bd, a, b)) record_hit(A, idx, 3);
+    if (bloom_probe_lazy(A.bloom, A.bd, a, [&](uint64_t s) { return xxh64_20(w, s); })) record_hit(A, idx, 3);
   }
   if constexpr (MODE == KM_BSGS) {
     uint64_t in[4];
     x_bytes_u64(x, in);
     uint64_t a = xxh64_32(in, KH_BLOOM_SEED);
-    uint64_t b = xxh64_32(in, a);
     const uint8_t *bf = A.bloom + (size_t)(x.d[7] >> 24) * A.bd.stride;
-    if (bloom_probe(bf, A.bd, a, b)) record_hit(A, idx, 4);
+    if (bloom_probe_lazy(bf, A.bd, a, [&](uint64_t s) { return xxh64_32(in, s); })) record_hit(A, idx, 4);
   }
   if constexpr (MODE == KM_BUILD) {
     // baby index idx -> point (idx+1)G; layers by index (keyhunt.cpp:5394-5443)
@@ -176,8 +188,17 @@ constexpr bool needs_y() {
 // ------------------------------------------------------------------------------------------
 // The walk.  Every lane runs A.groups groups of 2H points from its saved centre.
 // ------------------------------------------------------------------------------------------
+// Minimum waves per SIMD per mode (VGPR cap 512/(2*LB)... measured: the probe-light modes gain from
+// 4 waves/SIMD even with a few spills; the hash160 modes prefer 3).
 template <int MODE>
-__global__ void __launch_bounds__(256, 2) k_walk(walk_args A) {
+constexpr int walk_lb() {
+  return (MODE == KM_H160C || MODE == KM_H160U || MODE == KM_H160B) ? KH_WALK_LB_HASH
+         : MODE == KM_DUMP                                          ? 2
+                                                                    : KH_WALK_LB;
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(256, walk_lb<MODE>()) k_walk(walk_args A) {
   constexpr int H = KH_WALK_H;
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= A.L) return;

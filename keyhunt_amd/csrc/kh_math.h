@@ -35,15 +35,31 @@ struct fe {
 // ------------------------------------------------------------------------------------------
 // carry helpers
 // ------------------------------------------------------------------------------------------
+// add/sub with carry: clang's __builtin_addc/__builtin_subc select v_add_co_u32/v_addc_co_u32
+// (v_sub_co/v_subb_co) carry chains on gfx950; the portable form is for g++ host builds.
 KH_HD uint32_t addc(uint32_t a, uint32_t b, uint32_t cin, uint32_t &cout) {
+#if defined(__clang__)
+  unsigned int co;
+  uint32_t r = __builtin_addc(a, b, cin, &co);
+  cout = co;
+  return r;
+#else
   uint64_t s = (uint64_t)a + b + cin;
   cout = (uint32_t)(s >> 32);
   return (uint32_t)s;
+#endif
 }
 KH_HD uint32_t subb(uint32_t a, uint32_t b, uint32_t bin, uint32_t &bout) {
+#if defined(__clang__)
+  unsigned int bo;
+  uint32_t r = __builtin_subc(a, b, bin, &bo);
+  bout = bo;
+  return r;
+#else
   uint64_t s = (uint64_t)a - b - bin;
   bout = (uint32_t)(s >> 63);
   return (uint32_t)s;
+#endif
 }
 
 // p = 2^256 - 0x1000003D1
@@ -149,11 +165,41 @@ KH_HD void fe_reduce512(fe &r, const uint32_t t[16]) {
   if (r.d[7] == 0xFFFFFFFFu) fe_canon(r);
 }
 
+#if defined(__HIP_DEVICE_COMPILE__)
+// acc += a*b with the 64-bit carry-out of v_mad_u64_u32 counted into cnt (product scanning).
+// The carry lands in an SGPR lane mask and is folded by v_addc_co_u32.
+__device__ __forceinline__ uint64_t mad_acc(uint32_t a, uint32_t b, uint64_t acc, uint32_t &cnt) {
+  uint64_t d, m, junk;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(d), "=s"(m) : "v"(a), "v"(b), "v"(acc));
+  uint32_t o;
+  asm("v_addc_co_u32 %0, %1, 0, %2, %3" : "=v"(o), "=s"(junk) : "v"(cnt), "s"(m));
+  cnt = o;
+  return d;
+}
+#endif
+
 KH_HD void fe_mul(fe &r, const fe &a, const fe &b) {
   uint32_t t[16];
+#if defined(__HIP_DEVICE_COMPILE__)
+  // product scanning: column k = sum_{i+j=k} a_i*b_j in a 64-bit accumulator + carry count
+  uint64_t acc = 0;
+  uint32_t cnt = 0;
+#pragma unroll
+  for (int k = 0; k < 15; k++) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const int j = k - i;
+      if (j < 0 || j > 7) continue;
+      acc = mad_acc(a.d[i], b.d[j], acc, cnt);
+    }
+    t[k] = (uint32_t)acc;
+    acc = (acc >> 32) | ((uint64_t)cnt << 32);
+    cnt = 0;
+  }
+  t[15] = (uint32_t)acc;
+#else
   {
     uint64_t c = 0;
-#pragma unroll
     for (int j = 0; j < 8; j++) {
       uint64_t v = (uint64_t)a.d[0] * b.d[j] + c;
       t[j] = (uint32_t)v;
@@ -161,10 +207,8 @@ KH_HD void fe_mul(fe &r, const fe &a, const fe &b) {
     }
     t[8] = (uint32_t)c;
   }
-#pragma unroll
   for (int i = 1; i < 8; i++) {
     uint64_t c = 0;
-#pragma unroll
     for (int j = 0; j < 8; j++) {
       uint64_t v = (uint64_t)a.d[i] * b.d[j] + t[i + j] + c;
       t[i + j] = (uint32_t)v;
@@ -172,18 +216,48 @@ KH_HD void fe_mul(fe &r, const fe &a, const fe &b) {
     }
     t[i + 8] = (uint32_t)c;
   }
+#endif
   fe_reduce512(r, t);
 }
 
 KH_HD void fe_sqr(fe &r, const fe &a) {
   uint32_t t[16];
+#if defined(__HIP_DEVICE_COMPILE__)
+  // cross products a_i*a_j (i<j) by product scanning, doubled, plus the squares a_i^2
+  uint64_t acc = 0;
+  uint32_t cnt = 0;
+  t[0] = 0;
 #pragma unroll
+  for (int k = 1; k < 14; k++) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const int j = k - i;
+      if (j <= i || j > 7) continue;
+      acc = mad_acc(a.d[i], a.d[j], acc, cnt);
+    }
+    t[k] = (uint32_t)acc;
+    acc = (acc >> 32) | ((uint64_t)cnt << 32);
+    cnt = 0;
+  }
+  t[14] = (uint32_t)acc;
+  t[15] = (uint32_t)(acc >> 32);
+  // double
+#pragma unroll
+  for (int i = 15; i > 0; i--) t[i] = __builtin_amdgcn_alignbit(t[i], t[i - 1], 31);
+  t[0] = 0;
+  // add squares: pair (t[2i], t[2i+1]) += a_i^2, carries rippled into the next pair
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint64_t sq = (uint64_t)a.d[i] * a.d[i];
+    uint32_t c1;
+    t[2 * i] = addc(t[2 * i], (uint32_t)sq, c, c1);
+    t[2 * i + 1] = addc(t[2 * i + 1], (uint32_t)(sq >> 32), c1, c);
+  }
+#else
   for (int i = 0; i < 16; i++) t[i] = 0;
-  // cross products a_i*a_j, i<j
-#pragma unroll
   for (int i = 0; i < 7; i++) {
     uint64_t c = 0;
-#pragma unroll
     for (int j = i + 1; j < 8; j++) {
       uint64_t v = (uint64_t)a.d[i] * a.d[j] + t[i + j] + c;
       t[i + j] = (uint32_t)v;
@@ -191,14 +265,10 @@ KH_HD void fe_sqr(fe &r, const fe &a) {
     }
     t[i + 8] = (uint32_t)c;
   }
-  // double
   t[15] = (t[15] << 1) | (t[14] >> 31);
-#pragma unroll
   for (int i = 14; i > 0; i--) t[i] = (t[i] << 1) | (t[i - 1] >> 31);
   t[0] = t[0] << 1;
-  // add squares
   uint64_t c = 0;
-#pragma unroll
   for (int i = 0; i < 8; i++) {
     uint64_t v = (uint64_t)a.d[i] * a.d[i] + t[2 * i] + c;
     t[2 * i] = (uint32_t)v;
@@ -206,6 +276,7 @@ KH_HD void fe_sqr(fe &r, const fe &a) {
     t[2 * i + 1] = (uint32_t)v;
     c = v >> 32;
   }
+#endif
   fe_reduce512(r, t);
 }
 

@@ -14,7 +14,7 @@ from dataclasses import dataclass
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(PKG)
-LIB_PATH = os.path.join(PKG, "lib", "libkh_gpu.so")
+LIB_PATH = os.environ.get("KH_LIB") or os.path.join(PKG, "lib", "libkh_gpu.so")
 HEADER = os.path.join(REPO, "include", "kh_gpu.h")
 
 KH_MODE_ADDRESS, KH_MODE_XPOINT = 0, 1
