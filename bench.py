@@ -215,7 +215,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--bases", type=int, default=16384, help="BSGS bases (of 2N keys) per step per GPU")
+    ap.add_argument("--bases", type=int, default=65536, help="BSGS bases (of 2N keys) per step per GPU")
     ap.add_argument("--steps-rmd", type=int, default=None)
     ap.add_argument("--warmup-rmd", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)

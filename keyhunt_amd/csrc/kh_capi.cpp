@@ -1050,7 +1050,8 @@ int kh_bsgs_scan(kh_ctx *ctx, const uint8_t start[32], uint64_t n_bases, kh_bsgs
     // run of gpl groups never crosses a base (gpl divides `cycles`).  Rounds are pipelined: the
     // GPU walks round r+1 while the host refines round r's first-level candidates.
     const uint64_t total_groups = n_bases * I.cycles;
-    const uint64_t round_max = (uint64_t)ctx->lanes_max * I.cycles;
+    // rounds of at most lanes_max lanes x 2 groups, so several rounds pipeline within one call
+    const uint64_t round_max = (uint64_t)ctx->lanes_max * std::min<uint64_t>(I.cycles, 2);
     uint64_t g0 = 0;
     int cur = 0, pending = -1;
     bsgs_round rounds[2];

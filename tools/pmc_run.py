@@ -1,0 +1,17 @@
+"""Small fixed workload for rocprofv3 counter passes (one BSGS round, one rmd160 chunk)."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+import keyhunt_amd as K  # noqa: E402
+
+e = K.Engine(0)
+info = e.bsgs_setup(1 << 44, 128)
+e.bsgs_build()
+e.bsgs_set_targets([bench.decompress(bench.PUZZLE125)])
+e.bsgs_scan(1 << 124, 16384)          # one round: 2^18 lanes x 2 groups = 2^29 giant points
+e.set_targets([bytes.fromhex(bench.PUZZLE66_RMD)], bloom_items=1)
+e.scan(1 << 65, 1 << 30, K.KH_MODE_ADDRESS, K.KH_SEARCH_COMPRESS)
+e.synchronize()
+print("done", e.kernel_time(2), e.kernel_time(0))

@@ -32,10 +32,10 @@ y = pow((x * x * x + 7) % P, (P + 1) // 4, P)
 if y & 1:
     y = P - y
 e.bsgs_set_targets([(x, y)])
-e.bsgs_scan(1 << 124, 16384)
+e.bsgs_scan(1 << 124, 65536)
 e.kernel_time_reset()
 t = time.time()
-e.bsgs_scan((1 << 124) + 16384 * 2 * info.n, 16384)
+e.bsgs_scan((1 << 124) + 65536 * 2 * info.n, 65536)
 dt = time.time() - t
 la, ms, pts = e.kernel_time(2)
-print(f"[{tag}] bsgs k=128 16384 bases: wall {16384 * 32768 / dt / 1e9:.2f} G giant pts/s, kernel {pts / ms / 1e6:.2f} Gpts/s", flush=True)
+print(f"[{tag}] bsgs k=128 65536 bases: wall {65536 * 32768 / dt / 1e9:.2f} G giant pts/s, kernel {pts / ms / 1e6:.2f} Gpts/s", flush=True)
