@@ -129,6 +129,7 @@ def bsgs_leg(D: Dist, eng, args):
     pts_launch = pts / la
     ms_launch = ms / la
     achieved = pts_launch * ALGO_BYTES_PER_GIANT_POINT / (ms_launch / 1e3) / 1e9
+    traffic, tsrc = pmc_traffic("k_walk<4>", pts_launch)
     res = {
         "value": keys / T / 1e6,
         "ms_per_step": T / args.steps * 1e3,
@@ -137,13 +138,28 @@ def bsgs_leg(D: Dist, eng, args):
         "candidates": eng.bsgs_candidates(),
         "info": info,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tsrc,
+                     "algorithmic_bytes_per_launch": pts_launch * ALGO_BYTES_PER_GIANT_POINT,
                      "kernel": "k_walk<KM_BSGS>", "launches": la, "mean_launch_ms": ms_launch,
                      "giant_points_per_launch": pts_launch,
                      "algorithmic_bytes_per_giant_point": ALGO_BYTES_PER_GIANT_POINT},
         "q": q,
     }
     return res
+
+
+def pmc_traffic(kernel: str, points_per_launch: float):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary of this kernel (bytes per point
+    measured as TCC_EA0_RDREQ x 64 B + WRITE_SIZE x 1 KiB, MI355X_MICROARCH.md HBM section), scaled
+    to this run's points per launch; None when no summary is present."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_summary.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1])).get(kernel)
+    if not d or "hbm_bytes_per_point" not in d:
+        return None, None
+    return d["hbm_bytes_per_point"] * points_per_launch, os.path.relpath(files[-1], REPO)
 
 
 def rmd160_leg(D: Dist, eng, args):
