@@ -227,6 +227,11 @@ def cpu_baseline_rmd160(seconds: int):
 
 
 def main():
+    # stdout carries exactly one JSON line (rank 0); native libraries (gloo, HIP) may print on fd 1,
+    # so fd 1 is pointed at stderr for the run and the JSON goes to the saved descriptor.
+    json_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -243,7 +248,9 @@ def main():
 
     import keyhunt_amd as K
     D = Dist()
-    eng = K.Engine(D.local)
+    ndev = K.device_count()
+    # one process per GPU; on a box with fewer GPUs than ranks (rehearsal) ranks share devices
+    eng = K.Engine(D.local % max(1, ndev))
     prim = bsgs_leg(D, eng, args)
     sec = None if args.no_secondary else rmd160_leg(D, eng, args)
     cpu_b = cpu_r = None
@@ -272,7 +279,8 @@ def main():
             line["secondary"] = {"workload": "-m rmd160 -f tests/66.rmd -b 66 -l compress", "value": sec["value"],
                                  "unit": "Mkeys/s", "ms_per_step": sec["ms_per_step"], "steps": args.steps_rmd,
                                  "kernel": sec["kernel"], "cpu_baseline": cpu_r}
-        print(json.dumps(line), flush=True)
+        json_out.write(json.dumps(line) + "\n")
+        json_out.flush()
     D.close()
 
 

@@ -178,6 +178,47 @@ __device__ __forceinline__ void probe_point(const walk_args &A, const fe &x, con
   }
 }
 
+// Layer-1 probes of two giant-step points in lockstep (keyhunt.cpp:4819-4822 for each): both
+// chains issue their byte loads before either result is consumed, so every lane keeps two
+// independent HBM reads in flight.  Same result as two bloom_probe_lazy calls.
+__device__ __forceinline__ void probe_pair_bsgs(const walk_args &A, const fe &x1, uint64_t idx1, const fe &x2,
+                                                uint64_t idx2, bool valid2) {
+  uint64_t in1[4], in2[4];
+  x_bytes_u64(x1, in1);
+  x_bytes_u64(x2, in2);
+  bool alive1 = idx1 < A.n_points;
+  bool alive2 = valid2 && idx2 < A.n_points;
+  uint64_t h1 = xxh64_32(in1, KH_BLOOM_SEED), h2 = xxh64_32(in2, KH_BLOOM_SEED);
+  const uint64_t a1 = h1, a2 = h2;
+  uint64_t b1 = 0, b2 = 0;
+  const uint8_t *bf1 = A.bloom + (size_t)(x1.d[7] >> 24) * A.bd.stride;
+  const uint8_t *bf2 = A.bloom + (size_t)(x2.d[7] >> 24) * A.bd.stride;
+  for (uint32_t i = 0; i < A.bd.hashes && (alive1 || alive2); i++) {
+    uint64_t p1 = mod_bits(h1, A.bd.bits, A.bd.recip);
+    uint64_t p2 = mod_bits(h2, A.bd.bits, A.bd.recip);
+    uint32_t v1 = alive1 ? bf1[p1 >> 3] : 0u;
+    uint32_t v2 = alive2 ? bf2[p2 >> 3] : 0u;
+    if (alive1) {
+      if (!((v1 >> (p1 & 7)) & 1)) {
+        alive1 = false;
+      } else {
+        if (i == 0) b1 = xxh64_32(in1, a1);
+        h1 += b1;
+      }
+    }
+    if (alive2) {
+      if (!((v2 >> (p2 & 7)) & 1)) {
+        alive2 = false;
+      } else {
+        if (i == 0) b2 = xxh64_32(in2, a2);
+        h2 += b2;
+      }
+    }
+  }
+  if (alive1) record_hit(A, idx1, 4);
+  if (alive2) record_hit(A, idx2, 4);
+}
+
 template <int MODE>
 constexpr bool needs_y() {
   return MODE == KM_H160U || MODE == KM_H160B || MODE == KM_DUMP;
@@ -239,14 +280,18 @@ __global__ void __launch_bounds__(256, walk_lb<MODE>()) k_walk(walk_args A) {
 
     // backward: recover 1/dx_i and emit C - T[i] (offset -(i+1)) and C + T[i] (offset i+1).
     // Both points use the second operand (T.x, +-T.y): x3 = s^2 - C.x - T.x, y3 = s(T.x - x3) -+ T.y.
+    // prefix[i-1] is fetched one iteration ahead so its HBM latency overlaps the previous pair
+    fe pre_next;
+    scr_load(pre_next, scr, (size_t)(H - 2) * L + g);
 #pragma unroll 1
     for (int i = H - 1; i >= 0; i--) {
       fe tx, ty, di;
       load_fe_k(tx, T + i * 16);
       load_fe_k(ty, T + i * 16 + 8);
       if (i > 0) {
-        fe pre, dx;
-        scr_load(pre, scr, (size_t)(i - 1) * L + g);
+        fe pre = pre_next;
+        if (i > 1) scr_load(pre_next, scr, (size_t)(i - 2) * L + g);
+        fe dx;
         fe_mul(di, inv, pre);
         fe_sub(dx, tx, cx);
         fe_mul(inv, inv, dx);
@@ -255,6 +300,23 @@ __global__ void __launch_bounds__(256, walk_lb<MODE>()) k_walk(walk_args A) {
       }
       fe nty;
       fe_neg(nty, ty);
+      if constexpr (MODE == KM_BSGS) {
+        // both points first, then one lockstep probe of the pair (two loads in flight per lane)
+        fe xm, xp, s, dy;
+        fe_sub(dy, nty, cy);
+        fe_mul(s, dy, di);
+        fe_sqr(xm, s);
+        fe_sub(xm, xm, cx);
+        fe_sub(xm, xm, tx);
+        fe_sub(dy, ty, cy);
+        fe_mul(s, dy, di);
+        fe_sqr(xp, s);
+        fe_sub(xp, xp, cx);
+        fe_sub(xp, xp, tx);
+        const uint64_t off = (uint64_t)(i + 1);
+        probe_pair_bsgs(A, xm, cidx - off, xp, cidx + off, i < H - 1);
+        continue;
+      }
 #pragma unroll 1
       for (int side = 0; side < 2; side++) {
         if (side == 1 && i == H - 1) break;
