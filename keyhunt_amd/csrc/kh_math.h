@@ -489,11 +489,36 @@ KH_HD void ge_double(ge &r, const ge &p) {
 // ------------------------------------------------------------------------------------------
 // SHA-256 / RIPEMD-160 (single 64-byte blocks, fully unrolled)
 // ------------------------------------------------------------------------------------------
-KH_HD uint32_t rotr32(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
-KH_HD uint32_t rotl32(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
+KH_HD uint32_t rotr32(uint32_t x, int n) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_alignbit(x, x, n);
+#else
+  return (x >> n) | (x << (32 - n));
+#endif
+}
+KH_HD uint32_t rotl32(uint32_t x, int n) { return rotr32(x, (32 - n) & 31); }
 KH_HD uint32_t bswap32(uint32_t x) {
   return (x >> 24) | ((x >> 8) & 0xFF00u) | ((x << 8) & 0xFF0000u) | (x << 24);
 }
+// Any 3-input boolean function in one gfx950 v_bitop3_b32: IMM is the truth table evaluated on
+// a = 0xF0, b = 0xCC, c = 0xAA (so xor3 = 0x96, ch = 0xCA, maj = 0xE8).
+template <uint32_t IMM>
+KH_HD uint32_t bitop3(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:%4" : "=v"(r) : "v"(a), "v"(b), "v"(c), "i"(IMM));
+  return r;
+#else
+  uint32_t r = 0;
+  for (int i = 0; i < 8; i++)
+    if ((IMM >> i) & 1) {
+      uint32_t m = ((i & 4) ? a : ~a) & ((i & 2) ? b : ~b) & ((i & 1) ? c : ~c);
+      r |= m;
+    }
+  return r;
+#endif
+}
+KH_HD uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) { return bitop3<0x96>(a, b, c); }
 
 #define KH_SHA_K                                                                                          \
   {0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u, 0xab1c5ed5u, \
@@ -520,13 +545,13 @@ KH_HD void sha256_transform(uint32_t st[8], uint32_t w[16]) {
       wi = w[i];
     } else {
       uint32_t w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
-      uint32_t s0 = rotr32(w15, 7) ^ rotr32(w15, 18) ^ (w15 >> 3);
-      uint32_t s1 = rotr32(w2, 17) ^ rotr32(w2, 19) ^ (w2 >> 10);
+      uint32_t s0 = xor3(rotr32(w15, 7), rotr32(w15, 18), w15 >> 3);
+      uint32_t s1 = xor3(rotr32(w2, 17), rotr32(w2, 19), w2 >> 10);
       wi = w[i & 15] + s0 + w[(i - 7) & 15] + s1;
       w[i & 15] = wi;
     }
-    uint32_t t1 = h + (rotr32(e, 6) ^ rotr32(e, 11) ^ rotr32(e, 25)) + ((e & f) ^ (~e & g)) + K[i] + wi;
-    uint32_t t2 = (rotr32(a, 2) ^ rotr32(a, 13) ^ rotr32(a, 22)) + ((a & b) ^ (a & c) ^ (b & c));
+    uint32_t t1 = h + xor3(rotr32(e, 6), rotr32(e, 11), rotr32(e, 25)) + bitop3<0xCA>(e, f, g) + K[i] + wi;
+    uint32_t t2 = xor3(rotr32(a, 2), rotr32(a, 13), rotr32(a, 22)) + bitop3<0xE8>(a, b, c);
     h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
   }
   st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
@@ -534,11 +559,12 @@ KH_HD void sha256_transform(uint32_t st[8], uint32_t w[16]) {
 
 // RIPEMD-160 of a 32-byte message given as 8 little-endian words; out: 5 state words (LE bytes)
 KH_HD uint32_t rmd_f(int j, uint32_t x, uint32_t y, uint32_t z) {
-  return j < 16 ? (x ^ y ^ z)
-       : j < 32 ? ((x & y) | (~x & z))
-       : j < 48 ? ((x | ~y) ^ z)
-       : j < 64 ? ((x & z) | (y & ~z))
-                : (x ^ (y | ~z));
+  // x^y^z, (x&y)|(~x&z), (x|~y)^z, (x&z)|(y&~z), x^(y|~z) as single v_bitop3_b32 truth tables
+  return j < 16 ? bitop3<0x96>(x, y, z)
+       : j < 32 ? bitop3<0xCA>(x, y, z)
+       : j < 48 ? bitop3<0x59>(x, y, z)
+       : j < 64 ? bitop3<0xE4>(x, y, z)
+                : bitop3<0x2D>(x, y, z);
 }
 KH_HD void ripemd160_32(const uint32_t m[8], uint32_t out[5]) {
   const uint8_t RL[80] = {0, 1, 2,  3,  4,  5,  6,  7,  8,  9,  10, 11, 12, 13, 14, 15, 7,  4,  13, 1,
