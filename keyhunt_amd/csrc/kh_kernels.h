@@ -16,6 +16,10 @@
 #ifndef KH_WALK_LB
 #define KH_WALK_LB 4
 #endif
+// compute hash160(02||X) and hash160(03||X) with interleaved SHA-256 chains
+#ifndef KH_HASH_PAIR
+#define KH_HASH_PAIR 1
+#endif
 #ifndef KH_WALK_LB_HASH
 #define KH_WALK_LB_HASH 3
 #endif

@@ -122,6 +122,18 @@ template <int MODE>
 __device__ __forceinline__ void probe_point(const walk_args &A, const fe &x, const fe &y, uint64_t idx) {
   if (idx >= A.n_points) return;
   if constexpr (MODE == KM_H160C || MODE == KM_H160B) {
+#if KH_HASH_PAIR
+    uint32_t hh[2][5];
+    hash160_comp2(x, hh[0], hh[1]);
+#pragma unroll 1
+    for (uint32_t k = 0; k < 2; k++) {
+      uint32_t h[5];
+#pragma unroll
+      for (int q = 0; q < 5; q++) h[q] = k ? hh[1][q] : hh[0][q];
+      uint64_t a = xxh64_20(h, KH_BLOOM_SEED);
+      if (bloom_probe_lazy(A.bloom, A.bd, a, [&](uint64_t s) { return xxh64_20(h, s); })) record_hit(A, idx, k);
+    }
+#else
 #pragma unroll 1
     for (uint32_t pfx = 2; pfx <= 3; pfx++) {
       uint32_t h[5];
@@ -129,6 +141,7 @@ __device__ __forceinline__ void probe_point(const walk_args &A, const fe &x, con
       uint64_t a = xxh64_20(h, KH_BLOOM_SEED);
       if (bloom_probe_lazy(A.bloom, A.bd, a, [&](uint64_t s) { return xxh64_20(h, s); })) record_hit(A, idx, pfx - 2);
     }
+#endif
   }
   if constexpr (MODE == KM_H160U || MODE == KM_H160B) {
     uint32_t h[5];

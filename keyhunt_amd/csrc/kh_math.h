@@ -557,6 +557,40 @@ KH_HD void sha256_transform(uint32_t st[8], uint32_t w[16]) {
   st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
 }
 
+
+// Two independent SHA-256 compressions advanced round by round together (two dependency chains in
+// flight per lane: hash160(02||X) and hash160(03||X) differ only in the first message byte).
+KH_HD void sha256_transform2(uint32_t sa[8], uint32_t wa[16], uint32_t sb[8], uint32_t wb[16]) {
+  const uint32_t K[64] = KH_SHA_K;
+  uint32_t a = sa[0], b = sa[1], c = sa[2], d = sa[3], e = sa[4], f = sa[5], g = sa[6], h = sa[7];
+  uint32_t a2 = sb[0], b2 = sb[1], c2 = sb[2], d2 = sb[3], e2 = sb[4], f2 = sb[5], g2 = sb[6], h2 = sb[7];
+#pragma unroll
+  for (int i = 0; i < 64; i++) {
+    uint32_t wi, wj;
+    if (i < 16) {
+      wi = wa[i];
+      wj = wb[i];
+    } else {
+      uint32_t w15 = wa[(i - 15) & 15], w2v = wa[(i - 2) & 15];
+      wi = wa[i & 15] + xor3(rotr32(w15, 7), rotr32(w15, 18), w15 >> 3) + wa[(i - 7) & 15] +
+           xor3(rotr32(w2v, 17), rotr32(w2v, 19), w2v >> 10);
+      wa[i & 15] = wi;
+      uint32_t v15 = wb[(i - 15) & 15], v2 = wb[(i - 2) & 15];
+      wj = wb[i & 15] + xor3(rotr32(v15, 7), rotr32(v15, 18), v15 >> 3) + wb[(i - 7) & 15] +
+           xor3(rotr32(v2, 17), rotr32(v2, 19), v2 >> 10);
+      wb[i & 15] = wj;
+    }
+    uint32_t t1 = h + xor3(rotr32(e, 6), rotr32(e, 11), rotr32(e, 25)) + bitop3<0xCA>(e, f, g) + K[i] + wi;
+    uint32_t t2 = xor3(rotr32(a, 2), rotr32(a, 13), rotr32(a, 22)) + bitop3<0xE8>(a, b, c);
+    uint32_t u1 = h2 + xor3(rotr32(e2, 6), rotr32(e2, 11), rotr32(e2, 25)) + bitop3<0xCA>(e2, f2, g2) + K[i] + wj;
+    uint32_t u2 = xor3(rotr32(a2, 2), rotr32(a2, 13), rotr32(a2, 22)) + bitop3<0xE8>(a2, b2, c2);
+    h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+    h2 = g2; g2 = f2; f2 = e2; e2 = d2 + u1; d2 = c2; c2 = b2; b2 = a2; a2 = u1 + u2;
+  }
+  sa[0] += a; sa[1] += b; sa[2] += c; sa[3] += d; sa[4] += e; sa[5] += f; sa[6] += g; sa[7] += h;
+  sb[0] += a2; sb[1] += b2; sb[2] += c2; sb[3] += d2; sb[4] += e2; sb[5] += f2; sb[6] += g2; sb[7] += h2;
+}
+
 // RIPEMD-160 of a 32-byte message given as 8 little-endian words; out: 5 state words (LE bytes)
 KH_HD uint32_t rmd_f(int j, uint32_t x, uint32_t y, uint32_t z) {
   // x^y^z, (x&y)|(~x&z), (x|~y)^z, (x&z)|(y&~z), x^(y|~z) as single v_bitop3_b32 truth tables
@@ -628,6 +662,33 @@ KH_HD void hash160_comp(const fe &x, uint32_t prefix, uint32_t out[5]) {
   for (int i = 0; i < 8; i++) m[i] = bswap32(st[i]);
   ripemd160_32(m, out);
 }
+
+// hash160(02||X) and hash160(03||X) with the two SHA-256 compressions interleaved.
+KH_HD void hash160_comp2(const fe &x, uint32_t out02[5], uint32_t out03[5]) {
+  uint32_t wa[16], wb[16];
+  wa[0] = (2u << 24) | (x.d[7] >> 8);
+#pragma unroll
+  for (int i = 1; i < 8; i++) wa[i] = (x.d[8 - i] << 24) | (x.d[7 - i] >> 8);
+  wa[8] = (x.d[0] << 24) | 0x00800000u;
+#pragma unroll
+  for (int i = 9; i < 15; i++) wa[i] = 0;
+  wa[15] = 0x108u;
+#pragma unroll
+  for (int i = 0; i < 16; i++) wb[i] = wa[i];
+  wb[0] = (3u << 24) | (x.d[7] >> 8);
+  uint32_t sa[8], sb[8];
+  sha256_init(sa);
+  sha256_init(sb);
+  sha256_transform2(sa, wa, sb, wb);
+  uint32_t m[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) m[i] = bswap32(sa[i]);
+  ripemd160_32(m, out02);
+#pragma unroll
+  for (int i = 0; i < 8; i++) m[i] = bswap32(sb[i]);
+  ripemd160_32(m, out03);
+}
+
 // hash160(04 || X || Y) (KEYBUFFUNCOMP, secp256k1/SECP256K1.cpp:992-1024): two SHA-256 blocks.
 KH_HD void hash160_uncomp(const fe &x, const fe &y, uint32_t out[5]) {
   uint32_t w[16];

@@ -72,3 +72,29 @@ def test_bench_config_k128_known_answer():
                        "1c533b6bb7f0804e0995fe0000000000:1c533b6bb7f0804e09963e0000000000"], timeout=900)
     assert p.returncode == 1, p.stdout[-2000:] + p.stderr[-2000:]
     assert [h["key"] for h in hits] == ["1c533b6bb7f0804e09960225e44877ac"]
+
+
+def test_config5_geometry_k512_known_answer():
+    """configs[4] geometry (-k 512: M = 2^31, 7.36 GB layer-1 bloom per GPU) on the window that holds
+    puzzle 130's key (verified by the reference)."""
+    p, hits = run_cli(["-m", "bsgs", "-f", "130.txt", "-k", "512", "-r",
+                       "33e7665705359f04f28b8880000000000:33e7665705359f04f28b8c80000000000"], timeout=900)
+    assert p.returncode == 1, p.stdout[-2000:] + p.stderr[-2000:]
+    assert [h["key"] for h in hits] == ["33e7665705359f04f28b88cf897c603c9"]
+
+
+def test_bsgs_multi_target_and_not_found(engine, oracle):
+    """Several targets in one scan (the reference loops all targets per base); keys outside the
+    scanned bases are not reported; kh_bsgs_reset_found re-arms targets."""
+    n, k = 1 << 24, 4
+    engine.bsgs_setup(n, k)
+    engine.bsgs_build()
+    p = oracle.bsgs_params(n, k)
+    start = 0x10000000000
+    keys = [start + 5, start + 3 * 2 * p.n + 1000, start + 40 * 2 * p.n]  # bases 0, 3 and (outside) 40
+    engine.bsgs_set_targets([oracle.pubkey(x) for x in keys])
+    found = sorted(engine.bsgs_scan(start, 8))
+    assert found == [(0, keys[0]), (1, keys[1])]
+    assert engine.bsgs_scan(start, 8) == []          # already found: skipped like bsgs_found[]
+    engine.bsgs_reset_found()
+    assert sorted(engine.bsgs_scan(start, 8)) == found

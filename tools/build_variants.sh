@@ -8,7 +8,7 @@ for v in "${VARS[@]}"; do
   read -r lb lbh h <<< "$v"
   d=../variants/lb${lb}_h${lbh}_w${h}
   mkdir -p $d
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I../include -Icsrc -DKH_WALK_LB=$lb -DKH_WALK_LB_HASH=$lbh -DKH_WALK_H=$h -c csrc/kh_kernels.hip -o $d/k.o &
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I../include -Icsrc -DKH_WALK_LB=$lb -DKH_WALK_LB_HASH=$lbh -DKH_WALK_H=$h $EXTRA -c csrc/kh_kernels.hip -o $d/k.o &
 done
 wait
 for v in "${VARS[@]}"; do
