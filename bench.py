@@ -14,10 +14,12 @@ base-batch s*N + r.  The table build (baby steps) is replicated per GPU and not 
 reported.  torch.distributed (gloo, CPU tensors) provides the barrier and the max over ranks; the
 engine owns the GPU through its own HIP stream, synchronised on both sides of the timed region.
 
-roofline: dominant kernel = the BSGS giant-step walk.  achieved = algorithmic bytes per launch
-(128 B per giant point: ~2 random 64-B bloom lines per reference-layout probe) / mean
-launch time from HIP events recorded by the engine on its own stream.  traffic: HBM bytes per launch
-from rocprofv3 PMC (profiles/), or null.
+roofline: dominant kernel = the BSGS giant-step walk.  achieved = algorithmic bytes per launch / mean
+launch time from HIP events recorded by the engine on its own stream.  Algorithmic bytes per giant
+point: 64 B with the default blocked layer 1 (one random 64-B line per probe), 128 B with the
+reference layout (~2 random lines per probe).  traffic: HBM bytes per launch from the
+committed rocprofv3 PMC summary (profiles/), or null.  The walk is VALU-bound, so a "valu" object
+reports VALU lane-instructions/s (PMC instructions per point x points/s) against the gfx950 peak.
 cpu_baseline: rank 0 at N=1 only.  BSGS: the oracle's restatement of the giant-step loop
 (oracle/kh_oracle.c, keyhunt.cpp:4644-4880) on all host threads against the same GPU-built bloom
 (kind "port").  rmd160: the reference binary built from its own sources (oracle/_ref/keyhunt, kind
@@ -40,7 +42,10 @@ sys.path.insert(0, REPO)
 
 METRIC = "Mkeys/s at 1/2/4/8 GPU (BSGS b125; addr b66); HBM GB/s fraction"
 HBM_PEAK_GBS = 8000.0
-ALGO_BYTES_PER_GIANT_POINT = 128
+ALGO_BYTES_PER_GIANT_POINT = {0: 128, 1: 64}      # by layer-1 layout (reference, blocked)
+WALK_KERNEL = {0: "k_walk<4>", 1: "k_walk<7>"}    # KM_BSGS, KM_BSGSB
+# 256 CU x 4 SIMD x 32 lanes/clk (a wave64 VALU op issues over 2 clk) x 2.4 GHz, MI355X_MICROARCH.md
+VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
 PUZZLE125 = "0233709eb11e0d4439a729f21c2c443dedb727528229713f0065721ba8fa46f00e"
 PUZZLE66_RMD = "20d45a6a762535700ce9e0b216e31994335db8a5"
 P = 2**256 - 2**32 - 977
@@ -107,7 +112,7 @@ def timed(D: Dist, eng, warmup: int, steps: int, step_fn):
 
 def bsgs_leg(D: Dist, eng, args):
     import keyhunt_amd as K
-    info = eng.bsgs_setup(1 << 44, 128)
+    info = eng.bsgs_setup(1 << 44, 128, layer1=args.layer1)
     t = time.perf_counter()
     eng.bsgs_build()
     eng.synchronize()
@@ -128,8 +133,16 @@ def bsgs_leg(D: Dist, eng, args):
     keys = D.world * args.steps * B * two_n
     pts_launch = pts / la
     ms_launch = ms / la
-    achieved = pts_launch * ALGO_BYTES_PER_GIANT_POINT / (ms_launch / 1e3) / 1e9
-    traffic, tsrc = pmc_traffic("k_walk<4>", pts_launch)
+    bpp = ALGO_BYTES_PER_GIANT_POINT[info.layer1_layout]
+    kname = WALK_KERNEL[info.layer1_layout]
+    achieved = pts_launch * bpp / (ms_launch / 1e3) / 1e9
+    traffic, tsrc = pmc_traffic(kname, pts_launch)
+    ipp = pmc_entry(kname).get("valu_lane_instructions_per_point")
+    valu = None
+    if ipp:
+        a = ipp * pts_launch / (ms_launch / 1e3) / 1e12
+        valu = {"achieved": a, "peak": VALU_PEAK_TOPS, "unit": "T lane-instr/s", "frac": a / VALU_PEAK_TOPS,
+                "lane_instructions_per_giant_point": ipp, "source": tsrc}
     res = {
         "value": keys / T / 1e6,
         "ms_per_step": T / args.steps * 1e3,
@@ -139,10 +152,11 @@ def bsgs_leg(D: Dist, eng, args):
         "info": info,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tsrc,
-                     "algorithmic_bytes_per_launch": pts_launch * ALGO_BYTES_PER_GIANT_POINT,
-                     "kernel": "k_walk<KM_BSGS>", "launches": la, "mean_launch_ms": ms_launch,
+                     "algorithmic_bytes_per_launch": pts_launch * bpp,
+                     "kernel": kname, "launches": la, "mean_launch_ms": ms_launch,
                      "giant_points_per_launch": pts_launch,
-                     "algorithmic_bytes_per_giant_point": ALGO_BYTES_PER_GIANT_POINT},
+                     "algorithmic_bytes_per_giant_point": bpp},
+        "valu": valu,
         "q": q,
     }
     return res
@@ -152,14 +166,20 @@ def pmc_traffic(kernel: str, points_per_launch: float):
     """HBM bytes per launch from the committed rocprofv3 PMC summary of this kernel (bytes per point
     measured as TCC_EA0_RDREQ x 64 B + WRITE_SIZE x 1 KiB, MI355X_MICROARCH.md HBM section), scaled
     to this run's points per launch; None when no summary is present."""
+    d = pmc_entry(kernel)
+    if "hbm_bytes_per_point" not in d:
+        return None, None
+    return d["hbm_bytes_per_point"] * points_per_launch, d["source"]
+
+
+def pmc_entry(kernel: str) -> dict:
+    """This kernel's entry in the newest profiles/r*_pmc_summary.json that has it ({} if none)."""
     import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_summary.json")))
-    if not files:
-        return None, None
-    d = json.load(open(files[-1])).get(kernel)
-    if not d or "hbm_bytes_per_point" not in d:
-        return None, None
-    return d["hbm_bytes_per_point"] * points_per_launch, os.path.relpath(files[-1], REPO)
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_summary.json")), reverse=True):
+        d = json.load(open(f)).get(kernel)
+        if d:
+            return dict(d, source=os.path.relpath(f, REPO))
+    return {}
 
 
 def rmd160_leg(D: Dist, eng, args):
@@ -191,6 +211,9 @@ def cpu_threads() -> int:
 def cpu_baseline_bsgs(eng, info, q, seconds: float):
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle
+    # the CPU restatement probes the reference-layout layer 1: rebuild it in that layout
+    eng.bsgs_setup(1 << 44, 128, layer1=0)
+    eng.bsgs_build()
     bf1 = eng.get_bloom(1)
     p = oracle.bsgs_params(1 << 44, 128)
     thr = cpu_threads()
@@ -242,6 +265,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
+    ap.add_argument("--layer1", type=int, default=1, help="BSGS layer-1 layout: 1 blocked (default), 0 reference")
     args = ap.parse_args()
     args.steps_rmd = args.steps if args.steps_rmd is None else args.steps_rmd
     args.warmup_rmd = args.warmup if args.warmup_rmd is None else args.warmup_rmd
@@ -267,12 +291,14 @@ def main():
             "vs_baseline": None, "dtype": "u32",
             "data": "synthetic: puzzle-125 public key (tests/125.txt), sequential bases from 2^124",
             "config": {"workload": "-m bsgs -f tests/125.txt -b 125 -k 128", "n": info.n, "k": 128, "m": info.m,
+                       "layer1_layout": "blocked" if info.layer1_layout == 1 else "reference",
                        "bases_per_step": args.bases, "giant_points_per_step": args.bases * info.cycles * 1024,
                        "parallelism": f"keyspace split x{D.world} (no collective)"},
             "giant_points_per_s": prim["giant_points_per_s"],
             "build_seconds": prim["build_seconds"],
             "first_level_candidates": prim["candidates"],
             "roofline": prim["roofline"],
+            "valu": prim["valu"],
             "cpu_baseline": cpu_b,
         }
         if sec:

@@ -48,6 +48,12 @@ extern "C" {
 #define KH_SEARCH_UNCOMPRESS 1
 #define KH_SEARCH_BOTH 2   /* reference default (FLAGSEARCH = 2) */
 
+/* layer-1 (bloom_bP) layouts for kh_bsgs_set_layer1 */
+#define KH_LAYER1_REFERENCE 0  /* the reference's bit layout (bloom/bloom.cpp): bit-identical tables */
+#define KH_LAYER1_BLOCKED 1    /* default: all of an item's bits in one 64-B line (same XXH64 and k, 1.5x the
+                                  bits per shard, FP 3.9e-7 vs 1e-6); one HBM line per probe.  Layers 2/3
+                                  stay in the reference layout, so refinement and found keys are unchanged */
+
 /* hit kinds */
 #define KH_KIND_02 0       /* hash160(02||X) matched */
 #define KH_KIND_03 1       /* hash160(03||X) matched */
@@ -72,7 +78,7 @@ typedef struct {
   uint64_t cycles;      /* ceil(aux / 1024) 1024-point groups per base */
   uint64_t bloom_bits[3], bloom_bytes[3];  /* per shard, layers 1..3 */
   uint32_t bloom_hashes[3];
-  uint32_t pad;
+  uint32_t layer1_layout; /* KH_LAYER1_*; for BLOCKED, bloom_bits[0] is the bit count rounded to whole blocks */
 } kh_bsgs_info;
 
 /* one key found by kh_bsgs_scan */
@@ -104,6 +110,8 @@ int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride[32], uint
             uint32_t search, kh_hit *hits, uint32_t cap, uint32_t *n_hits);
 
 /* ---- BSGS --------------------------------------------------------------------------------- */
+/* layer-1 layout for the next kh_bsgs_setup (KH_LAYER1_BLOCKED unless changed) */
+int kh_bsgs_set_layer1(kh_ctx *ctx, uint32_t layout);
 int kh_bsgs_setup(kh_ctx *ctx, uint64_t n, uint64_t k, kh_bsgs_info *info);
 int kh_bsgs_build(kh_ctx *ctx);                  /* baby-step blooms + sorted bP table on the GPU */
 /* targets: n x {x[32], y[32]} affine points (big-endian) */

@@ -6,6 +6,7 @@
 // build runs on the GPU kernels in kh_kernels.hip; there is no CPU fallback.
 #include <hip/hip_runtime.h>
 #include <math.h>
+#include <stdlib.h>
 #include <stdio.h>
 #include <string.h>
 #include <algorithm>
@@ -306,6 +307,7 @@ struct kh_ctx {
   uint8_t *d_tbloom = nullptr;
 
   // bsgs
+  uint32_t l1_layout = KH_LAYER1_BLOCKED;
   bool bsgs_ready = false, bsgs_built = false;
   kh_bsgs_info info{};
   bloom_desc bd[3]{};
@@ -326,6 +328,7 @@ struct kh_ctx {
   kh_dev_hit *d_hits2[2] = {nullptr, nullptr};
   uint32_t *h_cnt2[2] = {nullptr, nullptr};
   kh_dev_hit *h_hits2[2] = {nullptr, nullptr};
+  uint32_t cand_cap = 1u << 16;  // candidates per round; grown (and the round redone) on overflow
   uint32_t *h_scal2[2] = {nullptr, nullptr};
   uint32_t h_scal_cap = 0;
   hipEvent_t ev_round[2][4] = {{nullptr, nullptr, nullptr, nullptr}, {nullptr, nullptr, nullptr, nullptr}};
@@ -572,6 +575,8 @@ int kh_open(int device, kh_ctx **out) {
   }
   if (hipMalloc(&c->d_comb, h.size() * 4) != hipSuccess) return fail(KH_E_NOMEM);
   if (hipMemcpy(c->d_comb, h.data(), h.size() * 4, hipMemcpyHostToDevice) != hipSuccess) return fail(KH_E_HIP);
+  // test hook: a small initial BSGS candidate buffer exercises the grow-and-redo path
+  if (const char *e = getenv("KH_CAND_CAP")) c->cand_cap = std::max<uint32_t>(1, (uint32_t)strtoul(e, nullptr, 0));
   if (hipMalloc(&c->d_hit_count, 4) != hipSuccess) return fail(KH_E_NOMEM);
   if (hipMalloc(&c->d_hits, (size_t)c->hit_cap * sizeof(kh_dev_hit)) != hipSuccess) return fail(KH_E_NOMEM);
   *out = c;
@@ -764,11 +769,19 @@ int kh_bsgs_setup(kh_ctx *ctx, uint64_t n, uint64_t k, kh_bsgs_info *info) {
   it[2] = (m3 / 256 > 1000) ? (m3 / 256 + (m3 % 256 ? 1 : 0)) : 1000;
   for (int l = 0; l < 3; l++) {
     ctx->bd[l] = bloom_size(bloom_entries(it[l]));
+    if (l == 0 && ctx->l1_layout == KH_LAYER1_BLOCKED) {
+      // 1.5x the reference's bits per shard in whole 512-bit blocks (kh_kernels.h); desc.bits = blocks
+      uint64_t blocks = (ctx->bd[0].bits * KH_BLK_BITS_NUM / KH_BLK_BITS_DEN + 511) / 512;
+      ctx->bd[0].bits = blocks;
+      ctx->bd[0].recip = ~0ULL / blocks;
+      ctx->bd[0].bytes = blocks * 64;
+    }
     ctx->bd[l].stride = (ctx->bd[l].bytes + 255) & ~255ULL;
-    I.bloom_bits[l] = ctx->bd[l].bits;
+    I.bloom_bits[l] = (l == 0 && ctx->l1_layout == KH_LAYER1_BLOCKED) ? ctx->bd[0].bits * 512 : ctx->bd[l].bits;
     I.bloom_bytes[l] = ctx->bd[l].bytes;
     I.bloom_hashes[l] = ctx->bd[l].hashes;
   }
+  I.layer1_layout = ctx->l1_layout;
   for (int l = 0; l < 3; l++) {
     (void)hipFree(ctx->d_bl[l]);
     ctx->d_bl[l] = nullptr;
@@ -792,6 +805,12 @@ int kh_bsgs_setup(kh_ctx *ctx, uint64_t n, uint64_t k, kh_bsgs_info *info) {
   ctx->bsgs_built = false;
   ctx->candidates = 0;
   if (info) *info = I;
+  return KH_OK;
+}
+
+int kh_bsgs_set_layer1(kh_ctx *ctx, uint32_t layout) {
+  if (!ctx || layout > KH_LAYER1_BLOCKED) return KH_E_ARG;
+  ctx->l1_layout = layout;
   return KH_OK;
 }
 
@@ -833,7 +852,7 @@ int kh_bsgs_build(kh_ctx *ctx) {
   A.m3 = I.m3;
   A.rows_key = d_key;
   A.rows_val = d_val;
-  r = run_walk(ctx, KM_BUILD, 3, A, jg.gpl, 4);
+  r = run_walk(ctx, ctx->l1_layout == KH_LAYER1_BLOCKED ? KM_BUILDB : KM_BUILD, 3, A, jg.gpl, 4);
   if (r) {
     (void)hipFree(d_key);
     (void)hipFree(d_val);
@@ -996,9 +1015,9 @@ int ensure_pipeline(kh_ctx *c, uint32_t L) {
   for (int i = 0; i < 2; i++) {
     if (!c->d_cnt2[i]) {
       HIPCHK(c, hipMalloc(&c->d_cnt2[i], 4));
-      HIPCHK(c, hipMalloc(&c->d_hits2[i], (size_t)c->hit_cap * sizeof(kh_dev_hit)));
+      HIPCHK(c, hipMalloc(&c->d_hits2[i], (size_t)c->cand_cap * sizeof(kh_dev_hit)));
       HIPCHK(c, hipHostMalloc(&c->h_cnt2[i], 4, hipHostMallocDefault));
-      HIPCHK(c, hipHostMalloc(&c->h_hits2[i], (size_t)c->hit_cap * sizeof(kh_dev_hit), hipHostMallocDefault));
+      HIPCHK(c, hipHostMalloc(&c->h_hits2[i], (size_t)c->cand_cap * sizeof(kh_dev_hit), hipHostMallocDefault));
       for (int j = 0; j < 4; j++) HIPCHK(c, hipEventCreate(&c->ev_round[i][j]));
     }
   }
@@ -1013,7 +1032,33 @@ int ensure_pipeline(kh_ctx *c, uint32_t L) {
   return ensure_lanes(c, L);
 }
 
+// grow the per-round candidate buffers to hold `need` entries (stream must be idle)
+int grow_candidates(kh_ctx *c, uint64_t need) {
+  uint64_t cap = c->cand_cap;
+  while (cap < need) cap *= 2;
+  if (cap > (1u << 28)) {
+    c->err = "first-level candidates per round exceed 2^28";
+    return KH_E_OVERFLOW;
+  }
+  for (int i = 0; i < 2; i++) {
+    (void)hipFree(c->d_hits2[i]);
+    if (c->h_hits2[i]) (void)hipHostFree(c->h_hits2[i]);
+    c->d_hits2[i] = nullptr;
+    c->h_hits2[i] = nullptr;
+  }
+  c->cand_cap = (uint32_t)cap;
+  for (int i = 0; i < 2; i++) {
+    HIPCHK(c, hipMalloc(&c->d_hits2[i], (size_t)cap * sizeof(kh_dev_hit)));
+    HIPCHK(c, hipHostMalloc(&c->h_hits2[i], (size_t)cap * sizeof(kh_dev_hit), hipHostMallocDefault));
+  }
+  return KH_OK;
+}
+
+// candidates copied back with each round's count; more are fetched on demand
+constexpr uint32_t KH_CAND_EAGER = 4096;
+
 struct bsgs_round {
+  uint64_t g0, rg;   // walk groups [g0, g0 + rg) of this call
   uint64_t t_round;  // first giant index of the round
   uint32_t L;
   uint64_t gpl;
@@ -1049,9 +1094,11 @@ int kh_bsgs_scan(kh_ctx *ctx, const uint8_t start[32], uint64_t n_bases, kh_bsgs
     // giant points of this call: t in [0, n_bases*A); t -> base b = t / A, a = t % A.  A lane's
     // run of gpl groups never crosses a base (gpl divides `cycles`).  Rounds are pipelined: the
     // GPU walks round r+1 while the host refines round r's first-level candidates.
-    const uint64_t total_groups = n_bases * I.cycles;
+    // walk groups of 2H points; a base holds A = cycles*1024 giant points = gpb groups
+    const uint64_t gpb = A_pts / (2 * H);
+    const uint64_t total_groups = n_bases * gpb;
     // rounds of at most lanes_max lanes x 2 groups, so several rounds pipeline within one call
-    const uint64_t round_max = (uint64_t)ctx->lanes_max * std::min<uint64_t>(I.cycles, 2);
+    const uint64_t round_max = (uint64_t)ctx->lanes_max * std::min<uint64_t>(gpb, 2);
     uint64_t g0 = 0;
     int cur = 0, pending = -1;
     bsgs_round rounds[2];
@@ -1064,8 +1111,10 @@ int kh_bsgs_scan(kh_ctx *ctx, const uint8_t start[32], uint64_t n_bases, kh_bsgs
     HIPCHK(ctx, hipMemcpy(dq, Qw, 64, hipMemcpyHostToDevice));
     auto enqueue = [&](int slot) -> int {
       uint64_t rg = std::min<uint64_t>(total_groups - g0, round_max);
-      job_geom jg = plan(ctx, rg, I.cycles);
+      job_geom jg = plan(ctx, rg, gpb);
       bsgs_round &R = rounds[slot];
+      R.g0 = g0;
+      R.rg = rg;
       R.t_round = g0 * 2 * H;
       R.L = jg.L;
       R.gpl = jg.gpl;
@@ -1107,25 +1156,27 @@ int kh_bsgs_scan(kh_ctx *ctx, const uint8_t start[32], uint64_t n_bases, kh_bsgs
       Aw.bd = ctx->bd[0];
       Aw.hit_count = ctx->d_cnt2[slot];
       Aw.hits = ctx->d_hits2[slot];
-      Aw.hit_cap = ctx->hit_cap;
+      Aw.hit_cap = ctx->cand_cap;
       R.launches = 0;
       R.points = 0;
       for (uint64_t gb = 0; gb < jg.gpl; gb += per_launch) {
         Aw.group_base = gb;
         Aw.groups = (uint32_t)std::min<uint64_t>(per_launch, jg.gpl - gb);
-        HIPCHK(ctx, launch_walk(KM_BSGS, Aw, ctx->stream));
+        HIPCHK(ctx, launch_walk(ctx->info.layer1_layout == KH_LAYER1_BLOCKED ? KM_BSGSB : KM_BSGS, Aw, ctx->stream));
         R.launches++;
         R.points += (uint64_t)jg.L * Aw.groups * 2 * H;
       }
       HIPCHK(ctx, hipEventRecord(ctx->ev_round[slot][2], ctx->stream));
       HIPCHK(ctx, hipMemcpyAsync(ctx->h_cnt2[slot], ctx->d_cnt2[slot], 4, hipMemcpyDeviceToHost, ctx->stream));
-      HIPCHK(ctx, hipMemcpyAsync(ctx->h_hits2[slot], ctx->d_hits2[slot], (size_t)ctx->hit_cap * sizeof(kh_dev_hit),
+      HIPCHK(ctx, hipMemcpyAsync(ctx->h_hits2[slot], ctx->d_hits2[slot],
+                                 (size_t)std::min(ctx->cand_cap, KH_CAND_EAGER) * sizeof(kh_dev_hit),
                                  hipMemcpyDeviceToHost, ctx->stream));
       HIPCHK(ctx, hipEventRecord(ctx->ev_round[slot][3], ctx->stream));
       g0 += rg;
       return KH_OK;
     };
-    // wait for round `slot`, account its time, refine its candidates in parallel
+    // wait for round `slot`, account its time, refine its candidates in parallel.  Returns 1 when
+    // the round overflowed the candidate buffer: the buffers were grown and the caller redoes it.
     auto finish = [&](int slot) -> int {
       bsgs_round &R = rounds[slot];
       // ev[3] follows the walk and the candidate copies of this round only
@@ -1140,10 +1191,14 @@ int kh_bsgs_scan(kh_ctx *ctx, const uint8_t start[32], uint64_t n_bases, kh_bsgs
       ctx->tm[2].ms += ms_walk;
       ctx->tm[2].points += R.points;
       uint32_t cnt = *ctx->h_cnt2[slot];
-      if (cnt > ctx->hit_cap) {
-        ctx->err = "device candidate buffer overflow";
-        return KH_E_OVERFLOW;
+      if (cnt > ctx->cand_cap) {
+        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));  // drain the speculative next round
+        int rr = grow_candidates(ctx, (uint64_t)cnt * 2);
+        return rr ? rr : 1;
       }
+      if (cnt > KH_CAND_EAGER)
+        HIPCHK(ctx, hipMemcpy(ctx->h_hits2[slot] + KH_CAND_EAGER, ctx->d_hits2[slot] + KH_CAND_EAGER,
+                              (size_t)(cnt - KH_CAND_EAGER) * sizeof(kh_dev_hit), hipMemcpyDeviceToHost));
       std::vector<kh_dev_hit> dh(ctx->h_hits2[slot], ctx->h_hits2[slot] + cnt);
       std::sort(dh.begin(), dh.end(), [](const kh_dev_hit &x, const kh_dev_hit &y) { return x.idx < y.idx; });
       ctx->candidates += cnt;
@@ -1194,7 +1249,13 @@ int kh_bsgs_scan(kh_ctx *ctx, const uint8_t start[32], uint64_t n_bases, kh_bsgs
         cur ^= 1;
       }
       if (pending >= 0) {
+        const uint64_t redo = rounds[pending].g0;
         r = finish(pending);
+        if (r == 1) {  // overflowed: walk again from that round with the larger buffers
+          g0 = redo;
+          pending = -1;
+          continue;
+        }
         if (r) {
           (void)hipFree(dq);
           return r;
@@ -1395,7 +1456,8 @@ int kh_bloom_check(kh_ctx *ctx, uint32_t layer, const uint8_t *items, uint32_t n
   HIPCHK(ctx, hipMalloc(&ditems, (size_t)n * len));
   HIPCHK(ctx, hipMalloc(&dout, (size_t)n * 4));
   HIPCHK(ctx, hipMemcpy(ditems, items, (size_t)n * len, hipMemcpyHostToDevice));
-  HIPCHK(ctx, launch_test_bloom(ditems, n, len, bl, d, layer ? 1 : 0, dout, ctx->stream));
+  uint32_t blocked = (layer == 1 && ctx->info.layer1_layout == KH_LAYER1_BLOCKED) ? 1 : 0;
+  HIPCHK(ctx, launch_test_bloom(ditems, n, len, bl, d, layer ? 1 : 0, blocked, dout, ctx->stream));
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
   std::vector<uint32_t> ho(n);
   HIPCHK(ctx, hipMemcpy(ho.data(), dout, (size_t)n * 4, hipMemcpyDeviceToHost));

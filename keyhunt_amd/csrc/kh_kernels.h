@@ -10,6 +10,8 @@
 #ifndef KH_WALK_H
 #define KH_WALK_H 512
 #endif
+static_assert(KH_WALK_H >= 64 && KH_WALK_H <= 512 && (512 % KH_WALK_H) == 0,
+              "2H must divide the reference's 1024-point group so lanes never straddle a BSGS base");
 
 // minimum waves per SIMD requested for the walk kernel: XPOINT/BSGS/BUILD modes (KH_WALK_LB) and
 // the hash160 modes (KH_WALK_LB_HASH).  256 / LB VGPRs per lane at most; see DESIGN.md.
@@ -24,6 +26,16 @@
 #define KH_WALK_LB_HASH 3
 #endif
 
+// Blocked layer-1 bloom (KH_LAYER1_BLOCKED): per shard, `blocks` 64-B lines, blocks =
+// ceil(KH_BLK_BITS_NUM/KH_BLK_BITS_DEN x reference bits / 512).  Item with XXH64 a = h(X, seed 0x10):
+// line a mod blocks; bit positions p_i = s_i >> 23, s_0 = a >> 32, s_{i+1} = s_i*MUL + ADD, for
+// i < hashes (the reference's k).  1.5x the reference's bits gives FP 3.9e-7 at k = 20 vs the
+// reference's 1e-6 (Poisson block load).
+#define KH_BLK_LCG_MUL 0x9E3779B1u
+#define KH_BLK_LCG_ADD 0x7F4A7C15u
+#define KH_BLK_BITS_NUM 3
+#define KH_BLK_BITS_DEN 2
+
 enum kh_walk_mode {
   KM_H160C = 0,   // hash160(02||X), hash160(03||X)          -l compress
   KM_H160U = 1,   // hash160(04||X||Y)                       -l uncompress
@@ -32,6 +44,8 @@ enum kh_walk_mode {
   KM_BSGS = 4,    // 32-byte X into the 256-shard layer-1 bloom
   KM_BUILD = 5,   // BSGS baby-step table build
   KM_DUMP = 6,    // X/Y dump (parity tests)
+  KM_BSGSB = 7,   // giant steps against the blocked layer-1 bloom (one 64-B line per probe)
+  KM_BUILDB = 8,  // baby-step build with the blocked layer-1 bloom
 };
 
 struct kh_dev_hit {
@@ -81,5 +95,5 @@ hipError_t launch_setup(const setup_args &A, hipStream_t st);
 hipError_t launch_test_hash160(const uint32_t *xs, const uint32_t *ys, uint32_t n, uint32_t *out, hipStream_t st);
 hipError_t launch_test_field(const uint32_t *a, const uint32_t *b, uint32_t n, uint32_t *out, hipStream_t st);
 hipError_t launch_test_bloom(const uint8_t *items, uint32_t n, uint32_t len, const uint8_t *bloom,
-                             const bloom_desc &bd, uint32_t sharded, uint32_t *out, hipStream_t st);
+                             const bloom_desc &bd, uint32_t sharded, uint32_t blocked, uint32_t *out, hipStream_t st);
 }  // namespace kh

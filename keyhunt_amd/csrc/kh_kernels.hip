@@ -23,6 +23,10 @@
 //   KM_XPOINT                        X[0..20) -> target bloom (keyhunt.cpp:3801-3824)
 //   KM_BSGS                          32-byte X -> bloom_bP[X[0]] (keyhunt.cpp:4819-4822)
 //   KM_BUILD                         baby X -> bloom layers 1/2/3 + bP rows (keyhunt.cpp:5394-5443)
+//   KM_BSGSB / KM_BUILDB             same with the BLOCKED layer-1 layout: an item's bits all lie in
+//                                    one 64-B line (block = XXH64 mod blocks, bit positions by
+//                                    double hashing inside the 512-bit block), so a probe costs one
+//                                    HBM line instead of ~2.1; layers 2/3 keep the reference layout
 //   KM_DUMP                          write X (and Y) -- parity tests only
 #include <hip/hip_runtime.h>
 #include "kh_math.h"
@@ -102,6 +106,30 @@ __device__ __forceinline__ void bloom_insert(uint8_t *__restrict__ bf_base, uint
   }
 }
 
+
+// Blocked layer-1 geometry (see kh_kernels.h): desc.bits = blocks per shard, desc.recip its
+// reciprocal.  The block (one 64-B line) is a mod blocks; the k bit positions inside it come from a
+// 32-bit LCG seeded with a's high word, so they are independent of each other (double hashing
+// inside a 512-bit block repeats patterns and lifts the false-positive rate ~40x).
+__device__ __forceinline__ uint64_t blk_line(uint64_t a, const bloom_desc &bd, uint32_t &seed) {
+  seed = (uint32_t)(a >> 32);
+  return mod_bits(a, bd.bits, bd.recip) * 64;
+}
+__device__ __forceinline__ uint32_t blk_next(uint32_t &seed) {
+  seed = seed * KH_BLK_LCG_MUL + KH_BLK_LCG_ADD;
+  return seed >> 23;
+}
+__device__ __forceinline__ void blk_insert(uint8_t *__restrict__ bf_base, uint64_t shard_off, const bloom_desc &bd,
+                                           uint64_t a) {
+  uint32_t seed;
+  uint64_t line = blk_line(a, bd, seed);
+  uint32_t *w = reinterpret_cast<uint32_t *>(bf_base + shard_off + line);
+  for (uint32_t i = 0; i < bd.hashes; i++) {
+    uint32_t p = blk_next(seed);
+    atomicOr(&w[p >> 5], 1u << (p & 31));
+  }
+}
+
 __device__ __forceinline__ void record_hit(const walk_args &A, uint64_t idx, uint32_t kind) {
   uint32_t slot = atomicAdd(A.hit_count, 1u);
   if (slot < A.hit_cap) {
@@ -163,14 +191,17 @@ __device__ __forceinline__ void probe_point(const walk_args &A, const fe &x, con
     const uint8_t *bf = A.bloom + (size_t)(x.d[7] >> 24) * A.bd.stride;
     if (bloom_probe_lazy(bf, A.bd, a, [&](uint64_t s) { return xxh64_32(in, s); })) record_hit(A, idx, 4);
   }
-  if constexpr (MODE == KM_BUILD) {
+  if constexpr (MODE == KM_BUILD || MODE == KM_BUILDB) {
     // baby index idx -> point (idx+1)G; layers by index (keyhunt.cpp:5394-5443)
     uint64_t in[4];
     x_bytes_u64(x, in);
     uint64_t a = xxh64_32(in, KH_BLOOM_SEED);
     uint64_t b = xxh64_32(in, a);
     uint32_t shard = x.d[7] >> 24;
-    bloom_insert(A.bl1, (uint64_t)shard * A.bd.stride, A.bd, a, b);
+    if constexpr (MODE == KM_BUILDB)
+      blk_insert(A.bl1, (uint64_t)shard * A.bd.stride, A.bd, a);
+    else
+      bloom_insert(A.bl1, (uint64_t)shard * A.bd.stride, A.bd, a, b);
     if (idx < A.m2) bloom_insert(A.bl2, (uint64_t)shard * A.bd2.stride, A.bd2, a, b);
     if (idx < A.m3) {
       bloom_insert(A.bl3, (uint64_t)shard * A.bd3.stride, A.bd3, a, b);
@@ -194,8 +225,33 @@ __device__ __forceinline__ void probe_point(const walk_args &A, const fe &x, con
 // Layer-1 probes of two giant-step points in lockstep (keyhunt.cpp:4819-4822 for each): both
 // chains issue their byte loads before either result is consumed, so every lane keeps two
 // independent HBM reads in flight.  Same result as two bloom_probe_lazy calls.
+template <bool BLK>
 __device__ __forceinline__ void probe_pair_bsgs(const walk_args &A, const fe &x1, uint64_t idx1, const fe &x2,
                                                 uint64_t idx2, bool valid2) {
+  if constexpr (BLK) {
+    // blocked layer 1: one line per item; the first byte read brings the line into L1/L2 and
+    // the remaining bit tests of that item hit there
+    uint64_t in1[4], in2[4];
+    x_bytes_u64(x1, in1);
+    x_bytes_u64(x2, in2);
+    bool alive1 = idx1 < A.n_points;
+    bool alive2 = valid2 && idx2 < A.n_points;
+    uint64_t a1 = xxh64_32(in1, KH_BLOOM_SEED), a2 = xxh64_32(in2, KH_BLOOM_SEED);
+    uint32_t s1, s2;
+    const uint64_t l1 = blk_line(a1, A.bd, s1), l2 = blk_line(a2, A.bd, s2);
+    const uint8_t *line1 = A.bloom + (size_t)(x1.d[7] >> 24) * A.bd.stride + l1;
+    const uint8_t *line2 = A.bloom + (size_t)(x2.d[7] >> 24) * A.bd.stride + l2;
+    for (uint32_t i = 0; i < A.bd.hashes && (alive1 || alive2); i++) {
+      uint32_t p1 = blk_next(s1), p2 = blk_next(s2);
+      uint32_t v1 = alive1 ? line1[p1 >> 3] : 0u;
+      uint32_t v2 = alive2 ? line2[p2 >> 3] : 0u;
+      if (alive1 && !((v1 >> (p1 & 7)) & 1)) alive1 = false;
+      if (alive2 && !((v2 >> (p2 & 7)) & 1)) alive2 = false;
+    }
+    if (alive1) record_hit(A, idx1, 4);
+    if (alive2) record_hit(A, idx2, 4);
+    return;
+  }
   uint64_t in1[4], in2[4];
   x_bytes_u64(x1, in1);
   x_bytes_u64(x2, in2);
@@ -209,8 +265,14 @@ __device__ __forceinline__ void probe_pair_bsgs(const walk_args &A, const fe &x1
   for (uint32_t i = 0; i < A.bd.hashes && (alive1 || alive2); i++) {
     uint64_t p1 = mod_bits(h1, A.bd.bits, A.bd.recip);
     uint64_t p2 = mod_bits(h2, A.bd.bits, A.bd.recip);
+#ifdef KH_TIMING_NO_PROBE_LOADS
+    // timing-only build: no HBM reads (outputs are wrong); isolates the compute cost
+    uint32_t v1 = (uint32_t)(p1 * 0x9E3779B1u) & (0xFFu >> (i + 1));
+    uint32_t v2 = (uint32_t)(p2 * 0x9E3779B1u) & (0xFFu >> (i + 1));
+#else
     uint32_t v1 = alive1 ? bf1[p1 >> 3] : 0u;
     uint32_t v2 = alive2 ? bf2[p2 >> 3] : 0u;
+#endif
     if (alive1) {
       if (!((v1 >> (p1 & 7)) & 1)) {
         alive1 = false;
@@ -289,7 +351,10 @@ __global__ void __launch_bounds__(256, walk_lb<MODE>()) k_walk(walk_args A) {
     fe_mul(inv, inv, dxn);    // 1 / prefix[H-1]
 
     // the centre itself (offset 0)
-    probe_point<MODE>(A, cx, cy, cidx);
+    if constexpr (MODE == KM_BSGSB)
+      probe_pair_bsgs<true>(A, cx, cidx, cx, cidx, false);
+    else
+      probe_point<MODE>(A, cx, cy, cidx);
 
     // backward: recover 1/dx_i and emit C - T[i] (offset -(i+1)) and C + T[i] (offset i+1).
     // Both points use the second operand (T.x, +-T.y): x3 = s^2 - C.x - T.x, y3 = s(T.x - x3) -+ T.y.
@@ -313,7 +378,7 @@ __global__ void __launch_bounds__(256, walk_lb<MODE>()) k_walk(walk_args A) {
       }
       fe nty;
       fe_neg(nty, ty);
-      if constexpr (MODE == KM_BSGS) {
+      if constexpr (MODE == KM_BSGS || MODE == KM_BSGSB) {
         // both points first, then one lockstep probe of the pair (two loads in flight per lane)
         fe xm, xp, s, dy;
         fe_sub(dy, nty, cy);
@@ -327,7 +392,7 @@ __global__ void __launch_bounds__(256, walk_lb<MODE>()) k_walk(walk_args A) {
         fe_sub(xp, xp, cx);
         fe_sub(xp, xp, tx);
         const uint64_t off = (uint64_t)(i + 1);
-        probe_pair_bsgs(A, xm, cidx - off, xp, cidx + off, i < H - 1);
+        probe_pair_bsgs<MODE == KM_BSGSB>(A, xm, cidx - off, xp, cidx + off, i < H - 1);
         continue;
       }
 #pragma unroll 1
@@ -447,7 +512,7 @@ __global__ void k_test_field(const uint32_t *a, const uint32_t *b, uint32_t n, u
 
 // bloom_check of n items of `len` bytes (20 or 32); shard = first byte when sharded.
 __global__ void k_test_bloom(const uint8_t *items, uint32_t n, uint32_t len, const uint8_t *bloom, bloom_desc bd,
-                             uint32_t sharded, uint32_t *out) {
+                             uint32_t sharded, uint32_t blocked, uint32_t *out) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint8_t *p = items + (size_t)i * len;
@@ -470,6 +535,16 @@ __global__ void k_test_bloom(const uint8_t *items, uint32_t n, uint32_t len, con
     b = xxh64_20(w, a);
   }
   const uint8_t *bf = bloom + (sharded ? (size_t)p[0] * bd.stride : 0);
+  if (blocked) {
+    uint32_t seed, ok = 1;
+    const uint64_t line = blk_line(a, bd, seed);
+    for (uint32_t k = 0; k < bd.hashes; k++) {
+      uint32_t q = blk_next(seed);
+      if (!((bf[line + (q >> 3)] >> (q & 7)) & 1)) ok = 0;
+    }
+    out[i] = ok;
+    return;
+  }
   out[i] = bloom_probe(bf, bd, a, b) ? 1u : 0u;
 }
 
@@ -493,6 +568,8 @@ hipError_t launch_walk(int mode, const walk_args &A, hipStream_t st) {
     case KM_BSGS: hipLaunchKernelGGL(k_walk<KM_BSGS>, grid, block, 0, st, A); break;
     case KM_BUILD: hipLaunchKernelGGL(k_walk<KM_BUILD>, grid, block, 0, st, A); break;
     case KM_DUMP: hipLaunchKernelGGL(k_walk<KM_DUMP>, grid, block, 0, st, A); break;
+    case KM_BSGSB: hipLaunchKernelGGL(k_walk<KM_BSGSB>, grid, block, 0, st, A); break;
+    case KM_BUILDB: hipLaunchKernelGGL(k_walk<KM_BUILDB>, grid, block, 0, st, A); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -514,8 +591,9 @@ hipError_t launch_test_field(const uint32_t *a, const uint32_t *b, uint32_t n, u
 }
 
 hipError_t launch_test_bloom(const uint8_t *items, uint32_t n, uint32_t len, const uint8_t *bloom,
-                             const bloom_desc &bd, uint32_t sharded, uint32_t *out, hipStream_t st) {
-  hipLaunchKernelGGL(k_test_bloom, dim3((n + 127) / 128), dim3(128), 0, st, items, n, len, bloom, bd, sharded, out);
+                             const bloom_desc &bd, uint32_t sharded, uint32_t blocked, uint32_t *out, hipStream_t st) {
+  hipLaunchKernelGGL(k_test_bloom, dim3((n + 127) / 128), dim3(128), 0, st, items, n, len, bloom, bd, sharded, blocked,
+                     out);
   return hipGetLastError();
 }
 

@@ -21,6 +21,7 @@ KH_MODE_ADDRESS, KH_MODE_XPOINT = 0, 1
 KH_SEARCH_COMPRESS, KH_SEARCH_UNCOMPRESS, KH_SEARCH_BOTH = 0, 1, 2
 KH_KIND_02, KH_KIND_03, KH_KIND_04, KH_KIND_XPOINT = 0, 1, 2, 3
 TIME_ADDRESS, TIME_XPOINT, TIME_BSGS, TIME_BUILD, TIME_SETUP = 0, 1, 2, 3, 4
+KH_LAYER1_REFERENCE, KH_LAYER1_BLOCKED = 0, 1
 
 ORDER_N = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141
 
@@ -37,7 +38,8 @@ class KhHit(ctypes.Structure):
 class KhBsgsInfo(ctypes.Structure):
     _fields_ = [("n", ctypes.c_uint64), ("m", ctypes.c_uint64), ("m2", ctypes.c_uint64), ("m3", ctypes.c_uint64),
                 ("aux", ctypes.c_uint64), ("cycles", ctypes.c_uint64), ("bloom_bits", ctypes.c_uint64 * 3),
-                ("bloom_bytes", ctypes.c_uint64 * 3), ("bloom_hashes", ctypes.c_uint32 * 3), ("pad", ctypes.c_uint32)]
+                ("bloom_bytes", ctypes.c_uint64 * 3), ("bloom_hashes", ctypes.c_uint32 * 3),
+                ("layer1_layout", ctypes.c_uint32)]
 
 
 class KhBsgsFound(ctypes.Structure):
@@ -78,6 +80,7 @@ def lib() -> ctypes.CDLL:
     L.kh_scan.argtypes = [P, u8p, u8p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(KhHit),
                           ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]
     L.kh_bsgs_setup.argtypes = [P, ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(KhBsgsInfo)]
+    L.kh_bsgs_set_layer1.argtypes = [P, ctypes.c_uint32]
     L.kh_bsgs_build.argtypes = [P]
     L.kh_bsgs_set_targets.argtypes = [P, u8p, ctypes.c_uint32]
     L.kh_bsgs_scan.argtypes = [P, u8p, ctypes.c_uint64, ctypes.POINTER(KhBsgsFound), ctypes.c_uint32,
@@ -172,7 +175,10 @@ class Engine:
                 for h in hits[: n.value]]
 
     # -- BSGS ----------------------------------------------------------------------------------
-    def bsgs_setup(self, n: int, k: int) -> KhBsgsInfo:
+    def bsgs_setup(self, n: int, k: int, layer1: int = None) -> KhBsgsInfo:
+        """layer1: KH_LAYER1_BLOCKED (default) or KH_LAYER1_REFERENCE (bit-identical to the reference)."""
+        if layer1 is not None:
+            self._chk(lib().kh_bsgs_set_layer1(self._ctx, layer1), "kh_bsgs_set_layer1")
         info = KhBsgsInfo()
         self._chk(lib().kh_bsgs_setup(self._ctx, n, k, ctypes.byref(info)), "kh_bsgs_setup")
         return info

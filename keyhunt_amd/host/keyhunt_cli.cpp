@@ -304,6 +304,7 @@ struct options {
   int seconds = 30;
   U stride = u_from_u64(1);
   bool matrix = false;
+  uint32_t layer1 = KH_LAYER1_BLOCKED;
 } opt;
 
 std::mutex g_keys_mtx, g_cursor_mtx;
@@ -577,7 +578,8 @@ void bsgs_worker(bsgs_job *j) {
     return;
   }
   kh_bsgs_info info;
-  r = kh_bsgs_setup(ctx, j->n, j->k, &info);
+  r = kh_bsgs_set_layer1(ctx, opt.layer1);
+  if (!r) r = kh_bsgs_setup(ctx, j->n, j->k, &info);
   if (!r) r = kh_bsgs_build(ctx);
   size_t nt = j->tx->size();
   std::vector<uint8_t> xy(64 * nt);
@@ -659,7 +661,7 @@ void bsgs_worker(bsgs_job *j) {
 
 void usage(const char *p) {
   printf("Usage: %s -m address|rmd160|xpoint|bsgs -f FILE [-b BITS | -r START:END] [-l compress|uncompress|both]\n"
-         "       [-n N] [-k K] [-I STRIDE] [-g GPUS] [-q] [-s SECONDS] [-M]\n", p);
+         "       [-n N] [-k K] [-I STRIDE] [-g GPUS] [-q] [-s SECONDS] [-M] [-L blocked|reference]\n", p);
 }
 
 }  // namespace
@@ -670,7 +672,7 @@ int main(int argc, char **argv) {
   int c;
   U order;
   u_from_hex(ORDER_HEX, order);
-  while ((c = getopt(argc, argv, "m:f:l:r:b:k:n:t:g:qs:I:MRec:B:S")) != -1) {
+  while ((c = getopt(argc, argv, "m:f:l:r:b:k:n:t:g:qs:I:L:MRec:B:S")) != -1) {
     switch (c) {
       case 'm': {
         int m = -1;
@@ -724,6 +726,11 @@ int main(int argc, char **argv) {
         break;
       }
       case 'M': opt.matrix = true; break;
+      case 'L':  // BSGS layer-1 layout on the GPU (engine option; the reference has one layout)
+        if (!strcmp(optarg, "reference")) opt.layer1 = KH_LAYER1_REFERENCE;
+        else if (!strcmp(optarg, "blocked")) opt.layer1 = KH_LAYER1_BLOCKED;
+        else { fprintf(stderr, "[E] -L reference|blocked\n"); return EXIT_FAILURE; }
+        break;
       case 'R': case 'e': case 'c': case 'B': case 'S':
         fprintf(stderr, "[E] -%c is outside the scope of this engine (sequential hot path only)\n", c);
         return EXIT_FAILURE;

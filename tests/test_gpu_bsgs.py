@@ -18,7 +18,7 @@ E2E = json.load(open(os.path.join(GOLDEN, "ref_e2e.json")))
 
 @pytest.mark.parametrize("cfg", VEC["bsgs_build"], ids=lambda c: f"n{c['n']:x}_k{c['k']}")
 def test_baby_tables_match_reference(engine, cfg):
-    info = engine.bsgs_setup(cfg["n"], cfg["k"])
+    info = engine.bsgs_setup(cfg["n"], cfg["k"], layer1=0)   # KH_LAYER1_REFERENCE: bit-identical tables
     assert (info.m, info.m2, info.m3) == (cfg["m"], cfg["m2"], cfg["m3"])
     assert list(info.bloom_bytes) == cfg["bytes"]
     engine.bsgs_build()
@@ -31,7 +31,7 @@ def test_candidates_and_key_vs_oracle(engine, oracle):
     n, k = 1 << 22, 2
     p = oracle.bsgs_params(n, k)
     tabs = oracle.BsgsTables(p)
-    engine.bsgs_setup(n, k)
+    engine.bsgs_setup(n, k, layer1=0)
     engine.bsgs_build()
     assert engine.get_bloom(1) == tabs.bf1.raw
     assert engine.get_bloom(2) == tabs.bf2.raw
@@ -87,7 +87,7 @@ def test_bsgs_multi_target_and_not_found(engine, oracle):
     """Several targets in one scan (the reference loops all targets per base); keys outside the
     scanned bases are not reported; kh_bsgs_reset_found re-arms targets."""
     n, k = 1 << 24, 4
-    engine.bsgs_setup(n, k)
+    engine.bsgs_setup(n, k, layer1=1)
     engine.bsgs_build()
     p = oracle.bsgs_params(n, k)
     start = 0x10000000000
@@ -98,3 +98,76 @@ def test_bsgs_multi_target_and_not_found(engine, oracle):
     assert engine.bsgs_scan(start, 8) == []          # already found: skipped like bsgs_found[]
     engine.bsgs_reset_found()
     assert sorted(engine.bsgs_scan(start, 8)) == found
+
+
+@pytest.mark.parametrize("layer1", [0, 1], ids=["reference", "blocked"])
+def test_layer1_layouts_no_false_negative_and_fp_rate(engine, oracle, layer1):
+    """Every baby X is in layer 1 (bloom has no false negatives) in both layouts; random X's pass at
+    a rate near the design error (reference 1e-6, blocked 3.9e-7)."""
+    import random
+    n, k = 1 << 30, 8                       # M = 2^18 babies
+    info = engine.bsgs_setup(n, k, layer1=layer1)
+    assert info.layer1_layout == layer1
+    engine.bsgs_build()
+    babies = [oracle.pubkey(i + 1)[0].to_bytes(32, "big") for i in range(0, info.m, info.m // 512)]
+    assert all(engine.bloom_check(1, babies))
+    rng = random.Random(11)
+    rnd = [rng.getrandbits(256).to_bytes(32, "big") for _ in range(200000)]
+    fp = sum(engine.bloom_check(1, rnd))
+    assert fp <= 5   # expectation 0.2 (reference) / 0.08 (blocked) false positives
+
+
+def test_blocked_and_reference_find_same_keys(engine, oracle):
+    """Found keys do not depend on the layer-1 layout (refinement uses layers 2/3 + table)."""
+    n, k = 1 << 26, 8
+    key = 0x3A5F0C3D2B1E00 + 12345
+    results = []
+    for layer1 in (0, 1):
+        p = engine.bsgs_setup(n, k, layer1=layer1)
+        engine.bsgs_build()
+        engine.bsgs_set_targets([oracle.pubkey(key)])
+        start = key - 7 * 2 * p.n - 999
+        results.append(engine.bsgs_scan(start, 16))
+    assert results[0] == results[1] == [(0, key)]
+
+
+def test_blocked_layer1_bytes_match_layout_spec(engine, oracle):
+    """The blocked layer-1 bloom is bit-exact with its specification (kh_kernels.h): line a mod
+    blocks of shard X[0], positions from the 32-bit LCG seeded with a >> 32."""
+    MUL, ADD, SEED = 0x9E3779B1, 0x7F4A7C15, 0x59F2815B16F81798
+    info = engine.bsgs_setup(1 << 20, 1, layer1=1)       # M = 1024 babies
+    engine.bsgs_build()
+    blocks = info.bloom_bits[0] // 512
+    assert info.bloom_bytes[0] == blocks * 64
+    model = bytearray(256 * blocks * 64)
+    for i in range(1, info.m + 1):
+        xb = oracle.pubkey(i)[0].to_bytes(32, "big")
+        a = oracle.xxh64(xb, SEED)
+        base = xb[0] * blocks * 64 + (a % blocks) * 64
+        s = a >> 32
+        for _ in range(info.bloom_hashes[0]):
+            s = (s * MUL + ADD) & 0xFFFFFFFF
+            q = s >> 23
+            model[base + (q >> 3)] |= 1 << (q & 7)
+    assert engine.get_bloom(1) == bytes(model)
+
+
+def test_candidate_overflow_grows_and_redoes_round(oracle, monkeypatch):
+    """A round with more first-level candidates than the buffer holds is walked again with a
+    larger buffer: same key, same candidate count as an unconstrained run."""
+    from keyhunt_amd import Engine
+    n, k = 1 << 40, 1                       # 2^20 giant points per base: a few candidates
+    key = 0x3A5F0C3D2B1E00000 + 777
+    out = []
+    for cap in (None, "2"):
+        if cap:
+            monkeypatch.setenv("KH_CAND_CAP", cap)
+        e = Engine(0)
+        p = e.bsgs_setup(n, k, layer1=0)
+        e.bsgs_build()
+        e.bsgs_set_targets([oracle.pubkey(key)])
+        start = key - 60 * 2 * p.n - 12345
+        out.append((e.bsgs_scan(start, 64), e.bsgs_candidates()))
+        e.close()
+    assert out[0][0] == out[1][0] == [(0, key)]
+    assert out[0][1] == out[1][1] > 2

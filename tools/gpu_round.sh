@@ -1,0 +1,38 @@
+#!/bin/bash
+# One GPU session: GPU tests, bench, rocprofv3 kernel-trace stats of the bench, PMC counter passes.
+# Usage (on the box, from the repo root): bash tools/gpu_round.sh TAG [parts]
+#   parts: any of tests,bench,prof,pmc (default all).  Every GPU step has its own time limit and
+#   the script stops at the first failure.
+set -o pipefail
+TAG=${1:-r01}
+PARTS=${2:-tests,bench,prof,pmc}
+R=$(pwd)
+O=$R/gpurun_out/$TAG
+mkdir -p $O
+has() { [[ ",$PARTS," == *",$1,"* ]]; }
+if has tests; then
+  timeout -k 10 900 python -m pytest tests -q -m gpu > $O/tests.log 2>&1 || { echo "tests rc=$?"; tail -30 $O/tests.log; exit 1; }
+  tail -2 $O/tests.log
+fi
+if has bench; then
+  timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err || { echo "bench rc=$?"; tail -20 $O/bench.err; exit 1; }
+  cat $O/bench.json
+fi
+cd /tmp && export TMPDIR=/tmp
+if has prof; then
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o bench -- \
+    python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $O/prof.json 2> $O/prof.err \
+    || { echo "prof rc=$?"; tail -20 $O/prof.err; exit 1; }
+  echo "prof ok"
+fi
+if has pmc; then
+  i=0
+  for c in "TCC_EA0_RDREQ_sum TCC_HIT_sum TCC_MISS_sum" "WRITE_SIZE" "FETCH_SIZE" \
+           "SQ_INSTS_VALU SQ_WAVES SQ_INSTS_SALU SQ_INSTS_SMEM" \
+           "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU"; do
+    i=$((i + 1))
+    timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d $O/pmc/p$i -o run -- \
+      python3 $R/tools/pmc_run.py > $O/pmc_p$i.log 2>&1 || { echo "pmc pass $i rc=$?"; tail -20 $O/pmc_p$i.log; exit 1; }
+  done
+  echo "pmc ok"
+fi
