@@ -1,0 +1,58 @@
+"""False-positive rate of blocked layer-1 bloom layouts: Poisson model vs simulation (development aid).
+
+python tools/sim_blocked_bloom.py  -> prints, per bit-budget multiplier, the model FP and the simulated
+FP of (a) double hashing inside the 512-bit block (the rejected draft) and (b) the LCG positions
+the engine uses (kh_kernels.h).  Items and queries are uniform 64-bit hashes a."""
+import math
+
+import numpy as np
+
+BPE = 28.7551   # bits per entry of bloom_init2(., 1e-6), bloom/bloom.cpp:163-176
+MUL, ADD = 0x9E3779B1, 0x7F4A7C15
+
+
+def model(lam: float, k: int, bb: int = 512) -> float:
+    s, p = 0.0, math.exp(-lam)
+    for n in range(0, 400):
+        if n:
+            p *= lam / n
+        s += p * (1 - math.exp(-k * n / bb)) ** k
+    return s
+
+
+def positions(a: np.ndarray, k: int, scheme: str):
+    if scheme == "double":
+        g1 = ((a >> np.uint64(41)) & np.uint64(511)).astype(np.int64)
+        g2 = (((a >> np.uint64(50)) & np.uint64(511)) | np.uint64(1)).astype(np.int64)
+        return [(g1 + i * g2) & 511 for i in range(k)]
+    s = (a >> np.uint64(32)).astype(np.uint64)
+    out = []
+    for _ in range(k):
+        s = (s * np.uint64(MUL) + np.uint64(ADD)) & np.uint64(0xFFFFFFFF)
+        out.append((s >> np.uint64(23)).astype(np.int64))
+    return out
+
+
+def simulate(items: int, mult: float, k: int, scheme: str, queries: int = 3_000_000, seed: int = 1) -> float:
+    rng = np.random.default_rng(seed)
+    blocks = math.ceil(math.ceil(items * BPE) * mult / 512)
+    filt = np.zeros((blocks, 512), dtype=bool)
+    a = rng.integers(0, 2**64 - 1, size=items, dtype=np.uint64)
+    blk = (a % np.uint64(blocks)).astype(np.int64)
+    for p in positions(a, k, scheme):
+        filt[blk, p] = True
+    q = rng.integers(0, 2**64 - 1, size=queries, dtype=np.uint64)
+    blk = (q % np.uint64(blocks)).astype(np.int64)
+    ok = np.ones(queries, dtype=bool)
+    for p in positions(q, k, scheme):
+        ok &= filt[blk, p]
+    return float(ok.mean())
+
+
+if __name__ == "__main__":
+    items = 32768
+    print(f"reference layout (unblocked) design FP: {(1 - math.exp(-20 / BPE)) ** 20:.3g}")
+    for mult in (1.0, 1.5, 2.0):
+        lam = 512 / (BPE * mult)
+        print(f"bits x{mult}: model {model(lam, 20):.3g}  double-hash sim {simulate(items, mult, 20, 'double'):.3g}"
+              f"  LCG sim {simulate(items, mult, 20, 'lcg'):.3g}")
