@@ -770,16 +770,16 @@ int kh_bsgs_setup(kh_ctx *ctx, uint64_t n, uint64_t k, kh_bsgs_info *info) {
   for (int l = 0; l < 3; l++) {
     ctx->bd[l] = bloom_size(bloom_entries(it[l]));
     if (l == 0 && ctx->l1_layout == KH_LAYER1_BLOCKED) {
-      // 1.5x the reference's bits per shard in whole 512-bit blocks (kh_kernels.h); desc.bits = blocks
-      uint64_t blocks = (ctx->bd[0].bits * KH_BLK_BITS_NUM / KH_BLK_BITS_DEN + 511) / 512;
+      // 3x the reference's bits per shard in whole 128-bit blocks (kh_kernels.h); desc.bits = blocks
+      uint64_t blocks = (ctx->bd[0].bits * KH_BLK_BITS_MUL + 127) / 128;
       ctx->bd[0].bits = blocks;
       ctx->bd[0].recip = ~0ULL / blocks;
-      ctx->bd[0].bytes = blocks * 64;
+      ctx->bd[0].bytes = blocks * 16;
     }
     ctx->bd[l].stride = (ctx->bd[l].bytes + 255) & ~255ULL;
-    I.bloom_bits[l] = (l == 0 && ctx->l1_layout == KH_LAYER1_BLOCKED) ? ctx->bd[0].bits * 512 : ctx->bd[l].bits;
+    I.bloom_bits[l] = (l == 0 && ctx->l1_layout == KH_LAYER1_BLOCKED) ? ctx->bd[0].bits * 128 : ctx->bd[l].bits;
     I.bloom_bytes[l] = ctx->bd[l].bytes;
-    I.bloom_hashes[l] = ctx->bd[l].hashes;
+    I.bloom_hashes[l] = (l == 0 && ctx->l1_layout == KH_LAYER1_BLOCKED) ? 16u : ctx->bd[l].hashes;
   }
   I.layer1_layout = ctx->l1_layout;
   for (int l = 0; l < 3; l++) {

@@ -26,15 +26,16 @@ static_assert(KH_WALK_H >= 64 && KH_WALK_H <= 512 && (512 % KH_WALK_H) == 0,
 #define KH_WALK_LB_HASH 3
 #endif
 
-// Blocked layer-1 bloom (KH_LAYER1_BLOCKED): per shard, `blocks` 64-B lines, blocks =
-// ceil(KH_BLK_BITS_NUM/KH_BLK_BITS_DEN x reference bits / 512).  Item with XXH64 a = h(X, seed 0x10):
-// line a mod blocks; bit positions p_i = s_i >> 23, s_0 = a >> 32, s_{i+1} = s_i*MUL + ADD, for
-// i < hashes (the reference's k).  1.5x the reference's bits gives FP 3.9e-7 at k = 20 vs the
-// reference's 1e-6 (Poisson block load).
+// Blocked layer-1 bloom (KH_LAYER1_BLOCKED), a split-block filter: per shard, `blocks` 16-byte
+// blocks, blocks = ceil(KH_BLK_BITS_MUL x reference bits / 128).  Item with XXH64 a = h(X, seed
+// 0x59f2815b16f81798): block a mod blocks; s_0 = a >> 32, s_{t+1} = s_t*MUL + ADD (u32) gives three
+// 5-bit fields per step, (s >> 27), (s >> 22) & 31, (s >> 17) & 31; fields 4w..4w+3 are the bits
+// set in little-endian u32 word w of the block (w < 4).  An item is present iff every word covers
+// its mask.  3x the reference's bits: FP 5.6e-7 (Poisson block load) vs the reference's 1e-6; one
+// 16-byte load per probe, so the walk issues it and tests it one step later (latency hidden).
 #define KH_BLK_LCG_MUL 0x9E3779B1u
 #define KH_BLK_LCG_ADD 0x7F4A7C15u
-#define KH_BLK_BITS_NUM 3
-#define KH_BLK_BITS_DEN 2
+#define KH_BLK_BITS_MUL 3
 
 enum kh_walk_mode {
   KM_H160C = 0,   // hash160(02||X), hash160(03||X)          -l compress
@@ -44,7 +45,7 @@ enum kh_walk_mode {
   KM_BSGS = 4,    // 32-byte X into the 256-shard layer-1 bloom
   KM_BUILD = 5,   // BSGS baby-step table build
   KM_DUMP = 6,    // X/Y dump (parity tests)
-  KM_BSGSB = 7,   // giant steps against the blocked layer-1 bloom (one 64-B line per probe)
+  KM_BSGSB = 7,   // giant steps against the blocked layer-1 bloom (one 16-B block per probe)
   KM_BUILDB = 8,  // baby-step build with the blocked layer-1 bloom
 };
 

@@ -23,10 +23,9 @@
 //   KM_XPOINT                        X[0..20) -> target bloom (keyhunt.cpp:3801-3824)
 //   KM_BSGS                          32-byte X -> bloom_bP[X[0]] (keyhunt.cpp:4819-4822)
 //   KM_BUILD                         baby X -> bloom layers 1/2/3 + bP rows (keyhunt.cpp:5394-5443)
-//   KM_BSGSB / KM_BUILDB             same with the BLOCKED layer-1 layout: an item's bits all lie in
-//                                    one 64-B line (block = XXH64 mod blocks, bit positions by
-//                                    double hashing inside the 512-bit block), so a probe costs one
-//                                    HBM line instead of ~2.1; layers 2/3 keep the reference layout
+//   KM_BSGSB / KM_BUILDB             same with the BLOCKED layer-1 layout (kh_kernels.h): an item's
+//                                    16 bits lie in one 16-byte block, so a probe is one 16-B load
+//                                    and a 4-word mask test; layers 2/3 keep the reference layout
 //   KM_DUMP                          write X (and Y) -- parity tests only
 #include <hip/hip_runtime.h>
 #include "kh_math.h"
@@ -107,27 +106,35 @@ __device__ __forceinline__ void bloom_insert(uint8_t *__restrict__ bf_base, uint
 }
 
 
-// Blocked layer-1 geometry (see kh_kernels.h): desc.bits = blocks per shard, desc.recip its
-// reciprocal.  The block (one 64-B line) is a mod blocks; the k bit positions inside it come from a
-// 32-bit LCG seeded with a's high word, so they are independent of each other (double hashing
-// inside a 512-bit block repeats patterns and lifts the false-positive rate ~40x).
-__device__ __forceinline__ uint64_t blk_line(uint64_t a, const bloom_desc &bd, uint32_t &seed) {
-  seed = (uint32_t)(a >> 32);
-  return mod_bits(a, bd.bits, bd.recip) * 64;
+// Blocked layer-1 (split-block) geometry, kh_kernels.h: desc.bits = blocks per shard, desc.recip
+// its reciprocal.  blk_masks expands the item's seed into the four word masks.
+__device__ __forceinline__ const uint4 *blk_addr(const uint8_t *bf_shard, uint64_t a, const bloom_desc &bd) {
+  return reinterpret_cast<const uint4 *>(bf_shard + mod_bits(a, bd.bits, bd.recip) * 16);
 }
-__device__ __forceinline__ uint32_t blk_next(uint32_t &seed) {
-  seed = seed * KH_BLK_LCG_MUL + KH_BLK_LCG_ADD;
-  return seed >> 23;
-}
-__device__ __forceinline__ void blk_insert(uint8_t *__restrict__ bf_base, uint64_t shard_off, const bloom_desc &bd,
-                                           uint64_t a) {
-  uint32_t seed;
-  uint64_t line = blk_line(a, bd, seed);
-  uint32_t *w = reinterpret_cast<uint32_t *>(bf_base + shard_off + line);
-  for (uint32_t i = 0; i < bd.hashes; i++) {
-    uint32_t p = blk_next(seed);
-    atomicOr(&w[p >> 5], 1u << (p & 31));
+__device__ __forceinline__ void blk_masks(uint32_t s, uint32_t m[4]) {
+  uint32_t f[18];
+#pragma unroll
+  for (int t = 0; t < 6; t++) {
+    s = s * KH_BLK_LCG_MUL + KH_BLK_LCG_ADD;
+    f[3 * t] = s >> 27;
+    f[3 * t + 1] = (s >> 22) & 31u;
+    f[3 * t + 2] = (s >> 17) & 31u;
   }
+#pragma unroll
+  for (int w = 0; w < 4; w++)
+    m[w] = (1u << f[4 * w]) | (1u << f[4 * w + 1]) | (1u << f[4 * w + 2]) | (1u << f[4 * w + 3]);
+}
+__device__ __forceinline__ bool blk_match(const uint4 &v, uint32_t seed) {
+  uint32_t m[4];
+  blk_masks(seed, m);
+  return ((v.x & m[0]) == m[0]) & ((v.y & m[1]) == m[1]) & ((v.z & m[2]) == m[2]) & ((v.w & m[3]) == m[3]);
+}
+__device__ __forceinline__ void blk_insert(uint8_t *__restrict__ bf_shard, const bloom_desc &bd, uint64_t a) {
+  uint32_t m[4];
+  blk_masks((uint32_t)(a >> 32), m);
+  uint32_t *w = reinterpret_cast<uint32_t *>(bf_shard + mod_bits(a, bd.bits, bd.recip) * 16);
+#pragma unroll
+  for (int k = 0; k < 4; k++) atomicOr(&w[k], m[k]);
 }
 
 __device__ __forceinline__ void record_hit(const walk_args &A, uint64_t idx, uint32_t kind) {
@@ -199,7 +206,7 @@ __device__ __forceinline__ void probe_point(const walk_args &A, const fe &x, con
     uint64_t b = xxh64_32(in, a);
     uint32_t shard = x.d[7] >> 24;
     if constexpr (MODE == KM_BUILDB)
-      blk_insert(A.bl1, (uint64_t)shard * A.bd.stride, A.bd, a);
+      blk_insert(A.bl1 + (size_t)shard * A.bd.stride, A.bd, a);
     else
       bloom_insert(A.bl1, (uint64_t)shard * A.bd.stride, A.bd, a, b);
     if (idx < A.m2) bloom_insert(A.bl2, (uint64_t)shard * A.bd2.stride, A.bd2, a, b);
@@ -222,36 +229,47 @@ __device__ __forceinline__ void probe_point(const walk_args &A, const fe &x, con
   }
 }
 
-// Layer-1 probes of two giant-step points in lockstep (keyhunt.cpp:4819-4822 for each): both
-// chains issue their byte loads before either result is consumed, so every lane keeps two
-// independent HBM reads in flight.  Same result as two bloom_probe_lazy calls.
-template <bool BLK>
+// Blocked layer-1 probes: each point costs one 16-byte load (its split block) and the word-mask
+// test.  The two points of a giant-step pair issue their loads together.
+typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
+// 16-byte load with the nontemporal hint: each block is read once, at a random address
+__device__ __forceinline__ uint4 ld_nt16(const uint4 *p) {
+  v4u32 v = __builtin_nontemporal_load(reinterpret_cast<const v4u32 *>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+// {global block index (shard*stride + block*16)/16, seed a >> 32} of one point
+__device__ __forceinline__ uint2 blk_record(const walk_args &A, const fe &x) {
+  uint64_t in[4];
+  x_bytes_u64(x, in);
+  const uint64_t a = xxh64_32(in, KH_BLOOM_SEED);
+  const uint64_t off = (uint64_t)(x.d[7] >> 24) * A.bd.stride + mod_bits(a, A.bd.bits, A.bd.recip) * 16;
+  return make_uint2((uint32_t)(off >> 4), (uint32_t)(a >> 32));
+}
+__device__ __forceinline__ void blk_probe_pair(const walk_args &A, const fe &x1, uint64_t idx1, const fe &x2,
+                                               uint64_t idx2, bool valid2) {
+#ifdef KH_TIMING_NO_PROBE
+  // timing-only build: no probe at all (outputs are wrong); isolates the walk
+  if ((x1.d[0] ^ x2.d[0]) == 0x9E3779B1u) record_hit(A, idx1, 4);
+  return;
+#endif
+  const uint2 r1 = blk_record(A, x1), r2 = blk_record(A, x2);
+  const uint4 *bl = reinterpret_cast<const uint4 *>(A.bloom);
+#ifdef KH_TIMING_NO_PROBE_LOADS
+  // timing-only build: no HBM reads (outputs are wrong); isolates the probe's compute
+  const uint4 v1 = make_uint4(r1.x, r1.x * 3u, r1.x * 5u, r1.x * 7u);
+  const uint4 v2 = make_uint4(r2.x, r2.x * 3u, r2.x * 5u, r2.x * 7u);
+#else
+  const uint4 v1 = ld_nt16(bl + r1.x), v2 = ld_nt16(bl + r2.x);
+#endif
+  if (idx1 < A.n_points && blk_match(v1, r1.y)) record_hit(A, idx1, 4);
+  if (valid2 && idx2 < A.n_points && blk_match(v2, r2.y)) record_hit(A, idx2, 4);
+}
+
+// Reference-layout layer-1 probes of two giant-step points in lockstep (keyhunt.cpp:4819-4822
+// for each): both chains issue their byte loads before either result is consumed, so every lane
+// keeps two independent HBM reads in flight.  Same result as two bloom_probe_lazy calls.
 __device__ __forceinline__ void probe_pair_bsgs(const walk_args &A, const fe &x1, uint64_t idx1, const fe &x2,
                                                 uint64_t idx2, bool valid2) {
-  if constexpr (BLK) {
-    // blocked layer 1: one line per item; the first byte read brings the line into L1/L2 and
-    // the remaining bit tests of that item hit there
-    uint64_t in1[4], in2[4];
-    x_bytes_u64(x1, in1);
-    x_bytes_u64(x2, in2);
-    bool alive1 = idx1 < A.n_points;
-    bool alive2 = valid2 && idx2 < A.n_points;
-    uint64_t a1 = xxh64_32(in1, KH_BLOOM_SEED), a2 = xxh64_32(in2, KH_BLOOM_SEED);
-    uint32_t s1, s2;
-    const uint64_t l1 = blk_line(a1, A.bd, s1), l2 = blk_line(a2, A.bd, s2);
-    const uint8_t *line1 = A.bloom + (size_t)(x1.d[7] >> 24) * A.bd.stride + l1;
-    const uint8_t *line2 = A.bloom + (size_t)(x2.d[7] >> 24) * A.bd.stride + l2;
-    for (uint32_t i = 0; i < A.bd.hashes && (alive1 || alive2); i++) {
-      uint32_t p1 = blk_next(s1), p2 = blk_next(s2);
-      uint32_t v1 = alive1 ? line1[p1 >> 3] : 0u;
-      uint32_t v2 = alive2 ? line2[p2 >> 3] : 0u;
-      if (alive1 && !((v1 >> (p1 & 7)) & 1)) alive1 = false;
-      if (alive2 && !((v2 >> (p2 & 7)) & 1)) alive2 = false;
-    }
-    if (alive1) record_hit(A, idx1, 4);
-    if (alive2) record_hit(A, idx2, 4);
-    return;
-  }
   uint64_t in1[4], in2[4];
   x_bytes_u64(x1, in1);
   x_bytes_u64(x2, in2);
@@ -352,25 +370,25 @@ __global__ void __launch_bounds__(256, walk_lb<MODE>()) k_walk(walk_args A) {
 
     // the centre itself (offset 0)
     if constexpr (MODE == KM_BSGSB)
-      probe_pair_bsgs<true>(A, cx, cidx, cx, cidx, false);
+      blk_probe_pair(A, cx, cidx, cx, cidx, false);
     else
       probe_point<MODE>(A, cx, cy, cidx);
 
     // backward: recover 1/dx_i and emit C - T[i] (offset -(i+1)) and C + T[i] (offset i+1).
     // Both points use the second operand (T.x, +-T.y): x3 = s^2 - C.x - T.x, y3 = s(T.x - x3) -+ T.y.
     // prefix[i-1] is fetched one iteration ahead so its HBM latency overlaps the previous pair
-    fe pre_next;
-    scr_load(pre_next, scr, (size_t)(H - 2) * L + g);
+    fe pre;
+    scr_load(pre, scr, (size_t)(H - 2) * L + g);
 #pragma unroll 1
     for (int i = H - 1; i >= 0; i--) {
       fe tx, ty, di;
       load_fe_k(tx, T + i * 16);
       load_fe_k(ty, T + i * 16 + 8);
       if (i > 0) {
-        fe pre = pre_next;
-        if (i > 1) scr_load(pre_next, scr, (size_t)(i - 2) * L + g);
         fe dx;
         fe_mul(di, inv, pre);
+        // refill `pre` for the next step right after its last use (no register copy)
+        if (i > 1) scr_load(pre, scr, (size_t)(i - 2) * L + g);
         fe_sub(dx, tx, cx);
         fe_mul(inv, inv, dx);
       } else {
@@ -392,7 +410,11 @@ __global__ void __launch_bounds__(256, walk_lb<MODE>()) k_walk(walk_args A) {
         fe_sub(xp, xp, cx);
         fe_sub(xp, xp, tx);
         const uint64_t off = (uint64_t)(i + 1);
-        probe_pair_bsgs<MODE == KM_BSGSB>(A, xm, cidx - off, xp, cidx + off, i < H - 1);
+        if constexpr (MODE == KM_BSGSB) {
+          blk_probe_pair(A, xm, cidx - off, xp, cidx + off, i < H - 1);
+        } else {
+          probe_pair_bsgs(A, xm, cidx - off, xp, cidx + off, i < H - 1);
+        }
         continue;
       }
 #pragma unroll 1
@@ -536,13 +558,7 @@ __global__ void k_test_bloom(const uint8_t *items, uint32_t n, uint32_t len, con
   }
   const uint8_t *bf = bloom + (sharded ? (size_t)p[0] * bd.stride : 0);
   if (blocked) {
-    uint32_t seed, ok = 1;
-    const uint64_t line = blk_line(a, bd, seed);
-    for (uint32_t k = 0; k < bd.hashes; k++) {
-      uint32_t q = blk_next(seed);
-      if (!((bf[line + (q >> 3)] >> (q & 7)) & 1)) ok = 0;
-    }
-    out[i] = ok;
+    out[i] = blk_match(*blk_addr(bf, a, bd), (uint32_t)(a >> 32)) ? 1u : 0u;
     return;
   }
   out[i] = bloom_probe(bf, bd, a, b) ? 1u : 0u;

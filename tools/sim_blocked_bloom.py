@@ -56,3 +56,50 @@ if __name__ == "__main__":
         lam = 512 / (BPE * mult)
         print(f"bits x{mult}: model {model(lam, 20):.3g}  double-hash sim {simulate(items, mult, 20, 'double'):.3g}"
               f"  LCG sim {simulate(items, mult, 20, 'lcg'):.3g}")
+
+
+def split128_masks(a: np.ndarray):
+    """Masks of the split-block layout (kh_kernels.h): 4 words x 4 bits from LCG fields."""
+    s = (a >> np.uint64(32)).astype(np.uint64)
+    fields = []
+    for _ in range(6):
+        s = (s * np.uint64(MUL) + np.uint64(ADD)) & np.uint64(0xFFFFFFFF)
+        fields += [(s >> np.uint64(27)), (s >> np.uint64(22)) & np.uint64(31), (s >> np.uint64(17)) & np.uint64(31)]
+    masks = []
+    for w in range(4):
+        m = np.zeros_like(s)
+        for j in range(4):
+            m |= np.uint64(1) << fields[4 * w + j]
+        masks.append(m)
+    return masks
+
+
+def simulate_split128(items: int, mult: float, queries: int = 4_000_000, seed: int = 2) -> float:
+    rng = np.random.default_rng(seed)
+    blocks = math.ceil(math.ceil(items * BPE) * mult / 128)
+    filt = np.zeros((blocks, 4), dtype=np.uint64)
+    a = rng.integers(0, 2**64 - 1, size=items, dtype=np.uint64)
+    blk = (a % np.uint64(blocks)).astype(np.int64)
+    for w, m in enumerate(split128_masks(a)):
+        np.bitwise_or.at(filt[:, w], blk, m)
+    q = rng.integers(0, 2**64 - 1, size=queries, dtype=np.uint64)
+    blk = (q % np.uint64(blocks)).astype(np.int64)
+    ok = np.ones(queries, dtype=bool)
+    for w, m in enumerate(split128_masks(q)):
+        ok &= (filt[blk, w] & m) == m
+    return float(ok.mean())
+
+
+def model_split(lam: float, words: int = 4, wbits: int = 32, per_word: int = 4) -> float:
+    s, p = 0.0, math.exp(-lam)
+    for n in range(0, 400):
+        if n:
+            p *= lam / n
+        s += p * (1 - (1 - 1 / wbits) ** (n * per_word)) ** (words * per_word)
+    return s
+
+
+if __name__ == "__main__":
+    for mult in (2.0, 3.0):
+        print(f"split-block 128 (4 words x 4 bits), bits x{mult}: model {model_split(128 / (BPE * mult)):.3g}"
+              f"  sim {simulate_split128(65536, mult):.3g}")
