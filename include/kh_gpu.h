@@ -120,6 +120,11 @@ int kh_bsgs_set_targets(kh_ctx *ctx, const uint8_t *xy, uint32_t n);
  * are skipped (like bsgs_found[]).  found: keys found by THIS call. */
 int kh_bsgs_scan(kh_ctx *ctx, const uint8_t start[32], uint64_t n_bases, kh_bsgs_found *found, uint32_t cap,
                  uint32_t *n_found);
+/* Same for an arbitrary list of bases (n_bases x 32-byte big-endian keys), e.g. the -B backward /
+ * both / random / dance schedules (keyhunt.cpp:5953, 6211, 4893, 5674): each base walks its own
+ * 2N keys exactly as in kh_bsgs_scan. */
+int kh_bsgs_scan_list(kh_ctx *ctx, const uint8_t *bases, uint64_t n_bases, kh_bsgs_found *found, uint32_t cap,
+                      uint32_t *n_found);
 int kh_bsgs_reset_found(kh_ctx *ctx);
 /* first-level bloom candidates seen so far (for stats / parity tests) */
 int kh_bsgs_candidates(kh_ctx *ctx, uint64_t *count);

@@ -1058,26 +1058,34 @@ int grow_candidates(kh_ctx *c, uint64_t need) {
 constexpr uint32_t KH_CAND_EAGER = 4096;
 
 struct bsgs_round {
-  uint64_t g0, rg;   // walk groups [g0, g0 + rg) of this call
-  uint64_t t_round;  // first giant index of the round
+  uint64_t g0, rg;   // rounds over bases: walk groups [g0, g0 + rg) of this call;
+                     // continuous mode: groups [g0, g0 + rg) of every lane
+  uint64_t t_round;  // giant index of the round's point 0 (continuous mode: 0, indices are global)
   uint32_t L;
   uint64_t gpl;
   uint32_t launches;
   uint64_t points;
+  bool setup;        // the round (re)started its lanes
 };
+
+// giant points per pipelined round (2^18 lanes x 2 groups of 1024)
+constexpr uint64_t KH_BSGS_ROUND_POINTS = 1ULL << 29;
 
 }  // namespace
 
-int kh_bsgs_scan(kh_ctx *ctx, const uint8_t start[32], uint64_t n_bases, kh_bsgs_found *found, uint32_t cap,
-                 uint32_t *n_found) {
-  if (!ctx || !start || !n_found) return KH_E_ARG;
+// The giant-step scan behind kh_bsgs_scan (bases start + b*2N) and kh_bsgs_scan_list (any bases).
+static int bsgs_scan_impl(kh_ctx *ctx, const u256 &st, const std::vector<u256> *list, uint64_t n_bases,
+                          kh_bsgs_found *found, uint32_t cap, uint32_t *n_found) {
   if (!ctx->bsgs_built) return KH_E_STATE;
   (void)hipSetDevice(ctx->device);
   *n_found = 0;
+  if (n_bases == 0) return KH_OK;
   const int H = KH_WALK_H;
   const kh_bsgs_info &I = ctx->info;
   const uint64_t A_pts = I.cycles * 1024;  // giant points walked per base (cycles x 1024)
-  u256 st = sc_reduce(u256_from_be(start));
+  auto base_of = [&](uint64_t b) {
+    return list ? (*list)[b] : sc_add(st, sc_reduce(u256_from_u128((u128)b * 2 * I.n)));
+  };
   // GSn[i] = -(i+1)*2M*G  (keyhunt.cpp:1797-1816)
   const uint32_t *tab = nullptr;
   int r = get_table(ctx, sc_neg(u256_u64(2 * I.m)), &tab);
@@ -1088,18 +1096,37 @@ int kh_bsgs_scan(kh_ctx *ctx, const uint8_t start[32], uint64_t n_bases, kh_bsgs
   }
   uint32_t nf = 0;
   const uint32_t per_launch = ctx->groups_per_launch ? ctx->groups_per_launch : 8;
+  // giant points of this call: t in [0, n_bases*A); t -> base b = t / A, a = t % A; the centre
+  // of a group whose first point is t sits at key base_b + M + 2M*(a + H).
+  const uint64_t gpb = A_pts / (2 * H);  // walk groups per base
+  const uint64_t total_groups = n_bases * gpb;
+  // Continuous mode: when a base's walk ends exactly where the next base's starts (cycles*1024 ==
+  // aux, every power-of-two k), P_t = Q - (start + M + 2M t)G is ONE progression over the whole
+  // call.  Lanes then own long runs of t, start once, and every round just continues them.
+  // Otherwise (bases overlap, SURVEY parity note 13) rounds restart lanes per base run.
+  const bool cont = !list && A_pts == I.aux;
+  job_geom jc{};
+  uint64_t gpr = 0;  // continuous mode: groups per lane per round
+  if (cont) {
+    jc = plan(ctx, total_groups, 0);
+    gpr = std::max<uint64_t>(1, KH_BSGS_ROUND_POINTS / ((uint64_t)jc.L * 2 * H));
+    gpr = std::min<uint64_t>(gpr, jc.gpl);
+  }
+  auto centre_scalar = [&](uint64_t t0) {  // -(key of the centre of the group starting at t0)
+    uint64_t b = t0 / A_pts, a0 = t0 % A_pts;
+    u256 kb = sc_add(base_of(b), sc_reduce(u256_from_u128((u128)I.m + (u128)2 * I.m * (a0 + H))));
+    return sc_neg(kb);
+  };
   for (uint32_t tgt = 0; tgt < ctx->targets.size(); tgt++) {
     if (ctx->found[tgt]) continue;
     const ge Q = ctx->targets[tgt];
-    // giant points of this call: t in [0, n_bases*A); t -> base b = t / A, a = t % A.  A lane's
-    // run of gpl groups never crosses a base (gpl divides `cycles`).  Rounds are pipelined: the
-    // GPU walks round r+1 while the host refines round r's first-level candidates.
-    // walk groups of 2H points; a base holds A = cycles*1024 giant points = gpb groups
-    const uint64_t gpb = A_pts / (2 * H);
-    const uint64_t total_groups = n_bases * gpb;
-    // rounds of at most lanes_max lanes x 2 groups, so several rounds pipeline within one call
-    const uint64_t round_max = (uint64_t)ctx->lanes_max * std::min<uint64_t>(gpb, 2);
+    // rounds are pipelined: the GPU walks round r+1 while the host refines round r's
+    // first-level candidates
+    // per-base rounds: lanes walk 1 or 2 groups (a divisor of gpb), so rounds keep ~lanes_max lanes
+    const uint64_t round_max = (uint64_t)ctx->lanes_max * (gpb % 2 == 0 ? 2 : 1);
+    const uint64_t g_end = cont ? jc.gpl : total_groups;
     uint64_t g0 = 0;
+    bool need_setup = true;  // continuous mode: (re)start the lanes at group g0
     int cur = 0, pending = -1;
     bsgs_round rounds[2];
     bool done = false;
@@ -1110,37 +1137,48 @@ int kh_bsgs_scan(kh_ctx *ctx, const uint8_t start[32], uint64_t n_bases, kh_bsgs
     HIPCHK(ctx, hipMalloc(&dq, 64));
     HIPCHK(ctx, hipMemcpy(dq, Qw, 64, hipMemcpyHostToDevice));
     auto enqueue = [&](int slot) -> int {
-      uint64_t rg = std::min<uint64_t>(total_groups - g0, round_max);
-      job_geom jg = plan(ctx, rg, gpb);
       bsgs_round &R = rounds[slot];
+      uint64_t rg;
+      job_geom jg;
+      if (cont) {
+        rg = std::min<uint64_t>(g_end - g0, gpr);
+        jg = jc;
+        R.t_round = 0;
+      } else {
+        rg = std::min<uint64_t>(g_end - g0, round_max);
+        jg = plan(ctx, rg, gpb);  // a lane's run never crosses a base
+        R.t_round = g0 * 2 * H;
+      }
       R.g0 = g0;
       R.rg = rg;
-      R.t_round = g0 * 2 * H;
       R.L = jg.L;
       R.gpl = jg.gpl;
       int rr = ensure_pipeline(ctx, jg.L);
       if (rr) return rr;
-      uint32_t *hs = ctx->h_scal2[slot];
-      for (uint32_t g = 0; g < jg.L; g++) {
-        uint64_t t0 = R.t_round + (uint64_t)g * jg.gpl * 2 * H;
-        uint64_t b = t0 / A_pts, a0 = t0 % A_pts;
-        // centre key: base_b + M + 2M*(a0 + H); lane centre = Q - key*G
-        u256 kb = sc_add(st, sc_reduce(u256_from_u128((u128)b * 2 * I.n)));
-        kb = sc_add(kb, sc_reduce(u256_from_u128((u128)I.m + (u128)2 * I.m * (a0 + H))));
-        u256_to_limbs(hs + (size_t)g * 8, sc_neg(kb));
+      if (!cont || need_setup) {
+        uint32_t *hs = ctx->h_scal2[slot];
+        for (uint32_t g = 0; g < jg.L; g++) {
+          uint64_t t0 = cont ? (uint64_t)g * jc.gpl * 2 * H + g0 * 2 * H : R.t_round + (uint64_t)g * jg.gpl * 2 * H;
+          u256_to_limbs(hs + (size_t)g * 8, centre_scalar(t0));
+        }
+        HIPCHK(ctx, hipMemcpyAsync(ctx->d_scalars, hs, (size_t)jg.L * 32, hipMemcpyHostToDevice, ctx->stream));
+        setup_args S;
+        memset(&S, 0, sizeof S);
+        S.scalars = ctx->d_scalars;
+        S.comb = ctx->d_comb;
+        S.q = dq;
+        S.has_q = 1;
+        S.L = jg.L;
+        S.cx = ctx->d_cx;
+        S.cy = ctx->d_cy;
+        HIPCHK(ctx, hipEventRecord(ctx->ev_round[slot][0], ctx->stream));
+        HIPCHK(ctx, launch_setup(S, ctx->stream));
+        need_setup = false;
+        R.setup = true;
+      } else {
+        R.setup = false;
+        HIPCHK(ctx, hipEventRecord(ctx->ev_round[slot][0], ctx->stream));
       }
-      HIPCHK(ctx, hipMemcpyAsync(ctx->d_scalars, hs, (size_t)jg.L * 32, hipMemcpyHostToDevice, ctx->stream));
-      setup_args S;
-      memset(&S, 0, sizeof S);
-      S.scalars = ctx->d_scalars;
-      S.comb = ctx->d_comb;
-      S.q = dq;
-      S.has_q = 1;
-      S.L = jg.L;
-      S.cx = ctx->d_cx;
-      S.cy = ctx->d_cy;
-      HIPCHK(ctx, hipEventRecord(ctx->ev_round[slot][0], ctx->stream));
-      HIPCHK(ctx, launch_setup(S, ctx->stream));
       HIPCHK(ctx, hipEventRecord(ctx->ev_round[slot][1], ctx->stream));
       HIPCHK(ctx, hipMemsetAsync(ctx->d_cnt2[slot], 0, 4, ctx->stream));
       walk_args Aw;
@@ -1151,7 +1189,7 @@ int kh_bsgs_scan(kh_ctx *ctx, const uint8_t start[32], uint64_t n_bases, kh_bsgs
       Aw.scratch = ctx->d_scratch;
       Aw.L = jg.L;
       Aw.lane_stride = jg.gpl * 2 * H;
-      Aw.n_points = rg * 2 * H;
+      Aw.n_points = cont ? total_groups * 2 * H : rg * 2 * H;
       Aw.bloom = ctx->d_bl[0];
       Aw.bd = ctx->bd[0];
       Aw.hit_count = ctx->d_cnt2[slot];
@@ -1159,9 +1197,10 @@ int kh_bsgs_scan(kh_ctx *ctx, const uint8_t start[32], uint64_t n_bases, kh_bsgs
       Aw.hit_cap = ctx->cand_cap;
       R.launches = 0;
       R.points = 0;
-      for (uint64_t gb = 0; gb < jg.gpl; gb += per_launch) {
+      const uint64_t gb0 = cont ? g0 : 0, gb1 = cont ? g0 + rg : jg.gpl;
+      for (uint64_t gb = gb0; gb < gb1; gb += per_launch) {
         Aw.group_base = gb;
-        Aw.groups = (uint32_t)std::min<uint64_t>(per_launch, jg.gpl - gb);
+        Aw.groups = (uint32_t)std::min<uint64_t>(per_launch, gb1 - gb);
         HIPCHK(ctx, launch_walk(ctx->info.layer1_layout == KH_LAYER1_BLOCKED ? KM_BSGSB : KM_BSGS, Aw, ctx->stream));
         R.launches++;
         R.points += (uint64_t)jg.L * Aw.groups * 2 * H;
@@ -1184,9 +1223,11 @@ int kh_bsgs_scan(kh_ctx *ctx, const uint8_t start[32], uint64_t n_bases, kh_bsgs
       float ms_setup = 0, ms_walk = 0;
       (void)hipEventElapsedTime(&ms_setup, ctx->ev_round[slot][0], ctx->ev_round[slot][1]);
       (void)hipEventElapsedTime(&ms_walk, ctx->ev_round[slot][1], ctx->ev_round[slot][2]);
-      ctx->tm[4].launches++;
-      ctx->tm[4].ms += ms_setup;
-      ctx->tm[4].points += R.L;
+      if (R.setup) {
+        ctx->tm[4].launches++;
+        ctx->tm[4].ms += ms_setup;
+        ctx->tm[4].points += R.L;
+      }
       ctx->tm[2].launches += R.launches;
       ctx->tm[2].ms += ms_walk;
       ctx->tm[2].points += R.points;
@@ -1211,8 +1252,7 @@ int kh_bsgs_scan(kh_ctx *ctx, const uint8_t start[32], uint64_t n_bases, kh_bsgs
           if (i >= dh.size()) break;
           uint64_t t = R.t_round + dh[i].idx;
           uint64_t b = t / A_pts, a = t % A_pts;
-          u256 base = sc_add(st, sc_reduce(u256_from_u128((u128)b * 2 * I.n)));
-          ok[i] = second_check(ctx, base, a, Q, keys[i]) ? 1 : 0;
+          ok[i] = second_check(ctx, base_of(b), a, Q, keys[i]) ? 1 : 0;
         }
       };
       unsigned nt = std::min<unsigned>(ctx->refine_threads, (unsigned)dh.size());
@@ -1237,9 +1277,9 @@ int kh_bsgs_scan(kh_ctx *ctx, const uint8_t start[32], uint64_t n_bases, kh_bsgs
         }
       return KH_OK;
     };
-    while ((g0 < total_groups || pending >= 0) && !done) {
+    while ((g0 < g_end || pending >= 0) && !done) {
       int nxt = -1;
-      if (g0 < total_groups) {
+      if (g0 < g_end) {
         r = enqueue(cur);
         if (r) {
           (void)hipFree(dq);
@@ -1253,6 +1293,7 @@ int kh_bsgs_scan(kh_ctx *ctx, const uint8_t start[32], uint64_t n_bases, kh_bsgs
         r = finish(pending);
         if (r == 1) {  // overflowed: walk again from that round with the larger buffers
           g0 = redo;
+          need_setup = true;  // continuous mode: the lanes already moved past it
           pending = -1;
           continue;
         }
@@ -1268,6 +1309,20 @@ int kh_bsgs_scan(kh_ctx *ctx, const uint8_t start[32], uint64_t n_bases, kh_bsgs
   }
   *n_found = nf;
   return nf > cap ? KH_E_OVERFLOW : KH_OK;
+}
+
+int kh_bsgs_scan(kh_ctx *ctx, const uint8_t start[32], uint64_t n_bases, kh_bsgs_found *found, uint32_t cap,
+                 uint32_t *n_found) {
+  if (!ctx || !start || !n_found) return KH_E_ARG;
+  return bsgs_scan_impl(ctx, sc_reduce(u256_from_be(start)), nullptr, n_bases, found, cap, n_found);
+}
+
+int kh_bsgs_scan_list(kh_ctx *ctx, const uint8_t *bases, uint64_t n_bases, kh_bsgs_found *found, uint32_t cap,
+                      uint32_t *n_found) {
+  if (!ctx || (!bases && n_bases) || !n_found) return KH_E_ARG;
+  std::vector<u256> list(n_bases);
+  for (uint64_t b = 0; b < n_bases; b++) list[b] = sc_reduce(u256_from_be(bases + 32 * b));
+  return bsgs_scan_impl(ctx, u256{}, &list, n_bases, found, cap, n_found);
 }
 
 // ---------------------------------------------------------------------------------------------

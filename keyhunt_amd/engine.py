@@ -85,6 +85,8 @@ def lib() -> ctypes.CDLL:
     L.kh_bsgs_set_targets.argtypes = [P, u8p, ctypes.c_uint32]
     L.kh_bsgs_scan.argtypes = [P, u8p, ctypes.c_uint64, ctypes.POINTER(KhBsgsFound), ctypes.c_uint32,
                                ctypes.POINTER(ctypes.c_uint32)]
+    L.kh_bsgs_scan_list.argtypes = [P, u8p, ctypes.c_uint64, ctypes.POINTER(KhBsgsFound), ctypes.c_uint32,
+                                    ctypes.POINTER(ctypes.c_uint32)]
     L.kh_bsgs_reset_found.argtypes = [P]
     L.kh_bsgs_candidates.argtypes = [P, ctypes.POINTER(ctypes.c_uint64)]
     L.kh_kernel_time.argtypes = [P, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_double),
@@ -194,6 +196,14 @@ class Engine:
         out = (KhBsgsFound * cap)()
         n = ctypes.c_uint32(0)
         self._chk(lib().kh_bsgs_scan(self._ctx, be32(start), n_bases, out, cap, ctypes.byref(n)), "kh_bsgs_scan")
+        return [(f.target, int.from_bytes(bytes(f.key), "big")) for f in out[: n.value]]
+
+    def bsgs_scan_list(self, bases: list[int], cap: int = 1024) -> list[tuple[int, int]]:
+        """Scan an arbitrary list of bases (each walks its own 2N keys)."""
+        out = (KhBsgsFound * cap)()
+        n = ctypes.c_uint32(0)
+        buf = b"".join(be32(b) for b in bases)
+        self._chk(lib().kh_bsgs_scan_list(self._ctx, buf, len(bases), out, cap, ctypes.byref(n)), "kh_bsgs_scan_list")
         return [(f.target, int.from_bytes(bytes(f.key), "big")) for f in out[: n.value]]
 
     def bsgs_reset_found(self) -> None:

@@ -6,8 +6,9 @@
 // and the stats line follow keyhunt.cpp:6891-6923 (writekey), 4825-4858 (BSGS) and 2850-2962.
 // Sequential scans consume the range in whole N_SEQUENTIAL_MAX chunks (keyhunt.cpp:3314-3330) and
 // BSGS in whole 2N bases (keyhunt.cpp:4600-4617), exactly as the reference's cursors do.
-// Random modes (-R, -B random/dance...), endomorphism (-e), vanity, minikeys, ETH and the table
-// persistence flags are outside this engine's scope and are rejected.
+// BSGS base schedules -B sequential|backward|both|random|dance|angrygiant and random chunks (-R)
+// follow the reference's cursors (see take_bases).  Endomorphism (-e), -B ggsb, vanity, minikeys,
+// ETH and the table persistence flags are outside this engine's scope and are rejected.
 #include <getopt.h>
 #include <pthread.h>
 #include <stdint.h>
@@ -18,6 +19,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <random>
 #include <atomic>
 #include <mutex>
 #include <string>
@@ -99,6 +101,29 @@ U u_divmod_u64(const U &a, uint64_t b, uint64_t *rem) {
   }
   if (rem) *rem = (uint64_t)r;
   return q;
+}
+int u_bitlen(const U &a) {
+  for (int i = 4; i >= 0; i--)
+    if (a.v[i]) return 64 * i + 64 - __builtin_clzll(a.v[i]);
+  return 0;
+}
+// uniform in [a, b) by rejection over bitlen(b - a) bits (the reference's Int::Rand(a, b) draws
+// from MT19937 seeded by getrandom, keyhunt.cpp:697-715; not reproducible there either)
+std::mt19937_64 g_rng{std::random_device{}()};
+std::mutex g_rng_mtx;
+U u_rand_range(const U &a, const U &b) {
+  if (u_cmp(b, a) <= 0) return a;
+  U span = u_sub(b, a), r;
+  int bits = u_bitlen(span);
+  std::lock_guard<std::mutex> lk(g_rng_mtx);
+  do {
+    for (int i = 0; i < 5; i++) {
+      int lo = 64 * i;
+      r.v[i] = lo >= bits ? 0 : g_rng();
+      if (lo < bits && bits - lo < 64) r.v[i] &= (1ULL << (bits - lo)) - 1;
+    }
+  } while (u_cmp(r, span) >= 0);
+  return u_add(a, r);
 }
 bool u_from_hex(const char *s, U &r) {
   r = U();
@@ -305,7 +330,12 @@ struct options {
   U stride = u_from_u64(1);
   bool matrix = false;
   uint32_t layer1 = KH_LAYER1_BLOCKED;
+  bool random = false;  // -R
+  int bsgs_mode = 0;    // -B, index into BSGS_MODES
 } opt;
+// keyhunt.cpp:419; ggsb (re-blocked baby tables) is not provided, angrygiant walks like sequential
+const char *BSGS_MODES[7] = {"sequential", "backward", "both", "random", "dance", "ggsb", "angrygiant"};
+enum { BM_SEQUENTIAL, BM_BACKWARD, BM_BOTH, BM_RANDOM, BM_DANCE, BM_GGSB, BM_ANGRYGIANT };
 
 std::mutex g_keys_mtx, g_cursor_mtx;
 std::atomic<uint64_t> g_groups_done{0};  // 1024-key groups (address family)
@@ -537,9 +567,13 @@ void addr_worker(addr_job *j) {
     U base;
     {
       std::lock_guard<std::mutex> lk(g_cursor_mtx);
-      if (u_cmp(g_cursor, g_end) >= 0) break;
-      base = g_cursor;
-      g_cursor = u_add(g_cursor, span);
+      if (opt.random) {
+        base = u_rand_range(g_cursor, g_end);  // key_mpz.Rand(start, end) per chunk (keyhunt.cpp:3309-3311)
+      } else {
+        if (u_cmp(g_cursor, g_end) >= 0) break;
+        base = g_cursor;
+        g_cursor = u_add(g_cursor, span);
+      }
     }
     if (opt.matrix) printf("Base key: %s gpu %d\n", u_hex(base).c_str(), j->device);
     u_to_be32(base, st_be);
@@ -569,6 +603,56 @@ struct bsgs_job {
 std::vector<uint8_t> g_found;  // bsgs_found[]
 std::mutex g_found_mtx;
 
+// Base schedules of -B (one call takes up to `want` bases under the cursor lock, as the
+// reference's threads take one each):
+//   sequential / angrygiant  BSGS_CURRENT += 2N while < end           keyhunt.cpp:4600-4617
+//   backward                 end -= 2N; base = max(end, start)          keyhunt.cpp:5995-6014
+//   both                     rand()%2 picks TOP (as backward, against BSGS_CURRENT) or BOTTOM
+//                            (as sequential, against the moving end)    keyhunt.cpp:6257-6300
+//   random                   Rand(start, end), endless                  keyhunt.cpp:4934-4952
+//   dance                    rand()%3: TOP, BOTTOM or Rand(current, end) keyhunt.cpp:5706-5750
+// g_cursor plays BSGS_CURRENT (and n_range_start), g_top n_range_end.
+U g_top;
+bool take_bases(const U &twoN, uint64_t want, std::vector<U> &out) {
+  out.clear();
+  std::lock_guard<std::mutex> lk(g_cursor_mtx);
+  auto top = [&]() {
+    if (u_cmp(g_top, g_cursor) <= 0) return false;
+    g_top = u_sub(g_top, twoN);
+    out.push_back(u_cmp(g_top, g_cursor) < 0 ? g_cursor : g_top);
+    return true;
+  };
+  auto bottom = [&]() {
+    if (u_cmp(g_cursor, g_top) >= 0) return false;
+    out.push_back(g_cursor);
+    g_cursor = u_add(g_cursor, twoN);
+    return true;
+  };
+  int mode = opt.bsgs_mode;
+  if (mode == BM_SEQUENTIAL || mode == BM_ANGRYGIANT || mode == BM_BACKWARD) {
+    while (out.size() < want && (mode == BM_BACKWARD ? top() : bottom())) {
+    }
+    return !out.empty();
+  }
+  if (mode == BM_RANDOM) {
+    while (out.size() < want) out.push_back(u_rand_range(g_cursor, g_top));
+    return true;
+  }
+  // both / dance: one draw per batch (the reference draws per base; the set of bases is the same)
+  int pick = rand() % (mode == BM_DANCE ? 3 : 2);
+  if (pick == 2) {
+    while (out.size() < want) out.push_back(u_rand_range(g_cursor, g_top));
+    return true;
+  }
+  while (out.size() < want && (pick == 0 ? top() : bottom())) {
+  }
+  if (out.empty()) {  // this side is exhausted; the other may not be
+    while (out.size() < want && (pick == 0 ? bottom() : top())) {
+    }
+  }
+  return !out.empty();
+}
+
 void bsgs_worker(bsgs_job *j) {
   kh_ctx *ctx = nullptr;
   int r = kh_open(j->device, &ctx);
@@ -590,30 +674,25 @@ void bsgs_worker(bsgs_job *j) {
   if (!r) r = kh_bsgs_set_targets(ctx, xy.data(), (uint32_t)nt);
   const U twoN = u_mul_u64(u_from_u64(info.n), 2);
   std::vector<kh_bsgs_found> found(nt + 1);
+  std::vector<U> bases;
+  std::vector<uint8_t> list_be;
   while (!r) {
-    U base;
-    uint64_t nb;
-    {
-      std::lock_guard<std::mutex> lk(g_cursor_mtx);
-      if (u_cmp(g_cursor, g_end) >= 0) break;
-      base = g_cursor;
-      // whole bases while base < end (keyhunt.cpp:4600-4617)
-      U left = u_sub(g_end, g_cursor);
-      uint64_t rem;
-      U q = u_divmod_u64(left, 1, &rem);
-      (void)q;
-      nb = 0;
-      U c = g_cursor;
-      while (nb < j->bases_per_call && u_cmp(c, g_end) < 0) {
-        c = u_add(c, twoN);
-        nb++;
-      }
-      g_cursor = c;
-    }
-    uint8_t st_be[32];
-    u_to_be32(base, st_be);
+    if (!take_bases(twoN, j->bases_per_call, bases)) break;
+    const uint64_t nb = bases.size();
+    // consecutive ascending bases go through kh_bsgs_scan (one progression), others as a list
+    std::sort(bases.begin(), bases.end(), [](const U &a, const U &b) { return u_cmp(a, b) < 0; });
+    bool consecutive = true;
+    for (uint64_t i = 1; i < nb && consecutive; i++) consecutive = u_cmp(u_sub(bases[i], bases[i - 1]), twoN) == 0;
     uint32_t nf = 0;
-    r = kh_bsgs_scan(ctx, st_be, nb, found.data(), (uint32_t)found.size(), &nf);
+    if (consecutive) {
+      uint8_t st_be[32];
+      u_to_be32(bases[0], st_be);
+      r = kh_bsgs_scan(ctx, st_be, nb, found.data(), (uint32_t)found.size(), &nf);
+    } else {
+      list_be.resize(32 * nb);
+      for (uint64_t i = 0; i < nb; i++) u_to_be32(bases[i], &list_be[32 * i]);
+      r = kh_bsgs_scan_list(ctx, list_be.data(), nb, found.data(), (uint32_t)found.size(), &nf);
+    }
     if (r) {
       fprintf(stderr, "[E] kh_bsgs_scan: %s (%s)\n", kh_strerror(r), kh_last_error(ctx));
       break;
@@ -731,12 +810,32 @@ int main(int argc, char **argv) {
         else if (!strcmp(optarg, "blocked")) opt.layer1 = KH_LAYER1_BLOCKED;
         else { fprintf(stderr, "[E] -L reference|blocked\n"); return EXIT_FAILURE; }
         break;
-      case 'R': case 'e': case 'c': case 'B': case 'S':
-        fprintf(stderr, "[E] -%c is outside the scope of this engine (sequential hot path only)\n", c);
+      case 'R':  // keyhunt.cpp:1019-1023
+        printf("[+] Random mode\n");
+        opt.random = true;
+        opt.bsgs_mode = BM_RANDOM;
+        break;
+      case 'B': {  // keyhunt.cpp:841-853
+        int idx = -1;
+        for (int i = 0; i < 7; i++)
+          if (!strcmp(optarg, BSGS_MODES[i])) idx = i;
+        if (idx < 0) {
+          fprintf(stderr, "[W] Ignoring unknow bsgs mode %s\n", optarg);
+        } else if (idx == BM_GGSB) {
+          fprintf(stderr, "[E] -B ggsb is not provided by this engine\n");
+          return EXIT_FAILURE;
+        } else {
+          opt.bsgs_mode = idx;
+        }
+        break;
+      }
+      case 'e': case 'c': case 'S':
+        fprintf(stderr, "[E] -%c is outside the scope of this engine\n", c);
         return EXIT_FAILURE;
       default: usage(argv[0]); return EXIT_FAILURE;
     }
   }
+  if (opt.mode == MODE_BSGS) printf("[+] Mode BSGS %s\n", BSGS_MODES[opt.bsgs_mode]);  // keyhunt.cpp:1209-1211
   if (!opt.file) {
     fprintf(stderr, "[E] -f FILE is required\n");
     return EXIT_FAILURE;
@@ -778,6 +877,7 @@ int main(int argc, char **argv) {
   printf("[+] GPUs : %d\n", gpus);
   g_cursor = opt.start;
   g_end = opt.end;
+  g_top = opt.end;
   U twoN;
   std::vector<std::thread> th;
   std::vector<addr_job> aj(gpus);
@@ -854,7 +954,11 @@ int main(int argc, char **argv) {
       bj[d].comp = &comp;
       bj[d].n = n;
       bj[d].k = opt.kfactor;
-      bj[d].bases_per_call = 64;
+      // ~2^31 giant points per engine call: enough lanes to fill the GPU, ~0.1 s per call
+      {
+        uint64_t aux = Nr / M, pts = ((aux + 1023) / 1024) * 1024;
+        bj[d].bases_per_call = std::max<uint64_t>(1, (1ULL << 31) / pts);
+      }
       th.emplace_back(bsgs_worker, &bj[d]);
     }
   }

@@ -43,6 +43,12 @@ E2E_RUNS = [
     ("bsgs_63_window", ["-m", "bsgs", "-f", "63.pub", "-r", "7cce5a0000000000:7cce9a0000000000", "-t", "8"], 300),
     ("bsgs_test120_b120", ["-m", "bsgs", "-f", "test120.txt", "-b", "120", "-t", "8"], 300),
     ("bsgs_63_small_n_k4", ["-m", "bsgs", "-f", "63.pub", "-n", "0x1000000", "-k", "4", "-r", "7cce5efdac000000:7cce5efdad000000", "-t", "8"], 300),
+    # non-power-of-two k: bases overlap (cycles*1024 > aux, SURVEY.md 8a parity note 13)
+    ("bsgs_63_k20", ["-m", "bsgs", "-f", "63.pub", "-k", "20", "-r", "7cce5a0000000000:7cce9a0000000000", "-t", "8"], 300),
+    ("bsgs_63_small_n_k3", ["-m", "bsgs", "-f", "63.pub", "-n", "0x1000000", "-k", "3", "-r", "7cce5efdac000000:7cce5efdad000000", "-t", "8"], 300),
+    # deterministic base schedules (keyhunt.cpp:5953 backward, 6211 both)
+    ("bsgs_63_backward", ["-m", "bsgs", "-f", "63.pub", "-B", "backward", "-r", "7cce5a0000000000:7cce9a0000000000", "-t", "8"], 300),
+    ("bsgs_63_both", ["-m", "bsgs", "-f", "63.pub", "-B", "both", "-r", "7cce5a0000000000:7cce9a0000000000", "-t", "8"], 300),
 ]
 
 

@@ -27,8 +27,9 @@ def test_baby_tables_match_reference(engine, cfg):
     assert hashlib.sha256(engine.get_bsgs_table()).hexdigest() == cfg["sha256_table"]
 
 
-def test_candidates_and_key_vs_oracle(engine, oracle):
-    n, k = 1 << 22, 2
+@pytest.mark.parametrize("n,k", [(1 << 22, 2), (1 << 24, 3)], ids=["k2_continuous", "k3_overlapping_bases"])
+def test_candidates_and_key_vs_oracle(engine, oracle, n, k):
+    """k = 3 is the non-power-of-two case: cycles*1024 > aux, bases overlap (SURVEY 8a note 13)."""
     p = oracle.bsgs_params(n, k)
     tabs = oracle.BsgsTables(p)
     engine.bsgs_setup(n, k, layer1=0)
@@ -39,7 +40,8 @@ def test_candidates_and_key_vs_oracle(engine, oracle):
     assert engine.get_bsgs_table() == tabs.table_bytes()
     key = 0x5A5A5A5A123456
     q = oracle.pubkey(key)
-    start = key - 3 * 2 * p.n - 12345
+    # the key sits near the END of the 4th base (beyond the 3rd base's overlap when k = 3)
+    start = key - 4 * 2 * p.n + 12345
     # no hit in the first 3 bases: identical candidate counts; found in the 4th
     engine.bsgs_set_targets([q])
     c0 = engine.bsgs_candidates()
@@ -174,3 +176,29 @@ def test_candidate_overflow_grows_and_redoes_round(oracle, monkeypatch):
         e.close()
     assert out[0][0] == out[1][0] == [(0, key)]
     assert out[0][1] == out[1][1] > 2
+
+
+def test_scan_list_equals_scan(engine, oracle):
+    """kh_bsgs_scan_list over the same consecutive bases = kh_bsgs_scan (keys and candidates), and a
+    shuffled, non-consecutive list finds the key in whichever base holds it."""
+    import random
+    n, k = 1 << 26, 4
+    p = engine.bsgs_setup(n, k, layer1=0)
+    engine.bsgs_build()
+    key = 0x7CCE5EFDACCF6808
+    engine.bsgs_set_targets([oracle.pubkey(key)])
+    start = key - 5 * 2 * p.n - 4242
+    c0 = engine.bsgs_candidates()
+    a = engine.bsgs_scan(start, 8)
+    c1 = engine.bsgs_candidates()
+    engine.bsgs_reset_found()
+    b = engine.bsgs_scan_list([start + i * 2 * p.n for i in range(8)])
+    c2 = engine.bsgs_candidates()
+    assert a == b == [(0, key)]
+    assert c1 - c0 == c2 - c1
+    engine.bsgs_reset_found()
+    bases = [start + i * 2 * p.n for i in (11, 5, 2, 40, 7)]
+    random.Random(3).shuffle(bases)
+    assert engine.bsgs_scan_list(bases) == [(0, key)]
+    engine.bsgs_reset_found()
+    assert engine.bsgs_scan_list([start + 3 * 2 * p.n, start + 9 * 2 * p.n]) == []
