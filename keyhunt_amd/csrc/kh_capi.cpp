@@ -772,6 +772,10 @@ int kh_bsgs_setup(kh_ctx *ctx, uint64_t n, uint64_t k, kh_bsgs_info *info) {
     if (l == 0 && ctx->l1_layout == KH_LAYER1_BLOCKED) {
       // 3x the reference's bits per shard in whole 128-bit blocks (kh_kernels.h); desc.bits = blocks
       uint64_t blocks = (ctx->bd[0].bits * KH_BLK_BITS_MUL + 127) / 128;
+      if (blocks >> 32) {  // block index is a 32-bit multiply-high
+        ctx->err = "blocked layer 1 needs < 2^32 blocks per shard; use KH_LAYER1_REFERENCE";
+        return KH_E_ARG;
+      }
       ctx->bd[0].bits = blocks;
       ctx->bd[0].recip = ~0ULL / blocks;
       ctx->bd[0].bytes = blocks * 16;

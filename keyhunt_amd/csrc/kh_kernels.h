@@ -26,13 +26,14 @@ static_assert(KH_WALK_H >= 64 && KH_WALK_H <= 512 && (512 % KH_WALK_H) == 0,
 #define KH_WALK_LB_HASH 3
 #endif
 
-// Blocked layer-1 bloom (KH_LAYER1_BLOCKED), a split-block filter: per shard, `blocks` 16-byte
-// blocks, blocks = ceil(KH_BLK_BITS_MUL x reference bits / 128).  Item with XXH64 a = h(X, seed
-// 0x59f2815b16f81798): block a mod blocks; s_0 = a >> 32, s_{t+1} = s_t*MUL + ADD (u32) gives three
-// 5-bit fields per step, (s >> 27), (s >> 22) & 31, (s >> 17) & 31; fields 4w..4w+3 are the bits
-// set in little-endian u32 word w of the block (w < 4).  An item is present iff every word covers
-// its mask.  3x the reference's bits: FP 5.6e-7 (Poisson block load) vs the reference's 1e-6; one
-// 16-byte load per probe, so the walk issues it and tests it one step later (latency hidden).
+// Blocked layer-1 bloom (KH_LAYER1_BLOCKED), a split-block filter: per shard X[0], `blocks` 16-byte
+// blocks, blocks = ceil(KH_BLK_BITS_MUL x reference bits / 128).  An item X (an x-coordinate, so
+// already uniform) uses its own words instead of a hash: with u = big-endian u32 of X[8..12) and
+// s_0 = big-endian u32 of X[12..16), the block is (u * blocks) >> 32, and the LCG
+// s_{t+1} = s_t*MUL + ADD (u32) gives three 5-bit fields per step, (s >> 27), (s >> 22) & 31,
+// (s >> 17) & 31; fields 4w..4w+3 are the bits set in little-endian u32 word w of the block
+// (w < 4).  An item is present iff every word covers its mask.  3x the reference's bits: FP 5.6e-7
+// (Poisson block load) vs the reference's 1e-6; one 16-byte load per probe and no XXH64.
 #define KH_BLK_LCG_MUL 0x9E3779B1u
 #define KH_BLK_LCG_ADD 0x7F4A7C15u
 #define KH_BLK_BITS_MUL 3

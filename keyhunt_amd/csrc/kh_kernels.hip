@@ -106,10 +106,11 @@ __device__ __forceinline__ void bloom_insert(uint8_t *__restrict__ bf_base, uint
 }
 
 
-// Blocked layer-1 (split-block) geometry, kh_kernels.h: desc.bits = blocks per shard, desc.recip
-// its reciprocal.  blk_masks expands the item's seed into the four word masks.
-__device__ __forceinline__ const uint4 *blk_addr(const uint8_t *bf_shard, uint64_t a, const bloom_desc &bd) {
-  return reinterpret_cast<const uint4 *>(bf_shard + mod_bits(a, bd.bits, bd.recip) * 16);
+// Blocked layer-1 (split-block) geometry, kh_kernels.h: desc.bits = blocks per shard.  The item
+// is an x-coordinate, already uniform, so the block and the seed are taken from its words directly
+// (no XXH64): block = (X[8..12) * blocks) >> 32, seed = X[12..16) (big-endian u32s = limbs 5, 4).
+__device__ __forceinline__ uint32_t blk_index(uint32_t w5, const bloom_desc &bd) {
+  return (uint32_t)(((uint64_t)w5 * bd.bits) >> 32);
 }
 __device__ __forceinline__ void blk_masks(uint32_t s, uint32_t m[4]) {
   uint32_t f[18];
@@ -129,10 +130,10 @@ __device__ __forceinline__ bool blk_match(const uint4 &v, uint32_t seed) {
   blk_masks(seed, m);
   return ((v.x & m[0]) == m[0]) & ((v.y & m[1]) == m[1]) & ((v.z & m[2]) == m[2]) & ((v.w & m[3]) == m[3]);
 }
-__device__ __forceinline__ void blk_insert(uint8_t *__restrict__ bf_shard, const bloom_desc &bd, uint64_t a) {
+__device__ __forceinline__ void blk_insert(uint8_t *__restrict__ bf_shard, const bloom_desc &bd, const fe &x) {
   uint32_t m[4];
-  blk_masks((uint32_t)(a >> 32), m);
-  uint32_t *w = reinterpret_cast<uint32_t *>(bf_shard + mod_bits(a, bd.bits, bd.recip) * 16);
+  blk_masks(x.d[4], m);
+  uint32_t *w = reinterpret_cast<uint32_t *>(bf_shard + (size_t)blk_index(x.d[5], bd) * 16);
 #pragma unroll
   for (int k = 0; k < 4; k++) atomicOr(&w[k], m[k]);
 }
@@ -200,15 +201,16 @@ __device__ __forceinline__ void probe_point(const walk_args &A, const fe &x, con
   }
   if constexpr (MODE == KM_BUILD || MODE == KM_BUILDB) {
     // baby index idx -> point (idx+1)G; layers by index (keyhunt.cpp:5394-5443)
+    uint32_t shard = x.d[7] >> 24;
+    if constexpr (MODE == KM_BUILDB) {
+      blk_insert(A.bl1 + (size_t)shard * A.bd.stride, A.bd, x);
+      if (idx >= A.m2) return;  // layers 2/3 hold only the first M2 / M3 babies
+    }
     uint64_t in[4];
     x_bytes_u64(x, in);
     uint64_t a = xxh64_32(in, KH_BLOOM_SEED);
     uint64_t b = xxh64_32(in, a);
-    uint32_t shard = x.d[7] >> 24;
-    if constexpr (MODE == KM_BUILDB)
-      blk_insert(A.bl1 + (size_t)shard * A.bd.stride, A.bd, a);
-    else
-      bloom_insert(A.bl1, (uint64_t)shard * A.bd.stride, A.bd, a, b);
+    if constexpr (MODE == KM_BUILD) bloom_insert(A.bl1, (uint64_t)shard * A.bd.stride, A.bd, a, b);
     if (idx < A.m2) bloom_insert(A.bl2, (uint64_t)shard * A.bd2.stride, A.bd2, a, b);
     if (idx < A.m3) {
       bloom_insert(A.bl3, (uint64_t)shard * A.bd3.stride, A.bd3, a, b);
@@ -237,13 +239,10 @@ __device__ __forceinline__ uint4 ld_nt16(const uint4 *p) {
   v4u32 v = __builtin_nontemporal_load(reinterpret_cast<const v4u32 *>(p));
   return make_uint4(v.x, v.y, v.z, v.w);
 }
-// {global block index (shard*stride + block*16)/16, seed a >> 32} of one point
+// {global block index (shard*stride + block*16)/16, seed} of one point
 __device__ __forceinline__ uint2 blk_record(const walk_args &A, const fe &x) {
-  uint64_t in[4];
-  x_bytes_u64(x, in);
-  const uint64_t a = xxh64_32(in, KH_BLOOM_SEED);
-  const uint64_t off = (uint64_t)(x.d[7] >> 24) * A.bd.stride + mod_bits(a, A.bd.bits, A.bd.recip) * 16;
-  return make_uint2((uint32_t)(off >> 4), (uint32_t)(a >> 32));
+  const uint64_t off = (uint64_t)(x.d[7] >> 24) * A.bd.stride + (uint64_t)blk_index(x.d[5], A.bd) * 16;
+  return make_uint2((uint32_t)(off >> 4), x.d[4]);
 }
 __device__ __forceinline__ void blk_probe_pair(const walk_args &A, const fe &x1, uint64_t idx1, const fe &x2,
                                                uint64_t idx2, bool valid2) {
@@ -558,7 +557,10 @@ __global__ void k_test_bloom(const uint8_t *items, uint32_t n, uint32_t len, con
   }
   const uint8_t *bf = bloom + (sharded ? (size_t)p[0] * bd.stride : 0);
   if (blocked) {
-    out[i] = blk_match(*blk_addr(bf, a, bd), (uint32_t)(a >> 32)) ? 1u : 0u;
+    // X[8..12) and X[12..16) as big-endian u32s (limbs 5 and 4)
+    const uint32_t w5 = ((uint32_t)p[8] << 24) | ((uint32_t)p[9] << 16) | ((uint32_t)p[10] << 8) | p[11];
+    const uint32_t w4 = ((uint32_t)p[12] << 24) | ((uint32_t)p[13] << 16) | ((uint32_t)p[14] << 8) | p[15];
+    out[i] = blk_match(reinterpret_cast<const uint4 *>(bf)[blk_index(w5, bd)], w4) ? 1u : 0u;
     return;
   }
   out[i] = bloom_probe(bf, bd, a, b) ? 1u : 0u;

@@ -135,9 +135,9 @@ def test_blocked_and_reference_find_same_keys(engine, oracle):
 
 def test_blocked_layer1_bytes_match_layout_spec(engine, oracle):
     """The blocked (split-block) layer-1 bloom is bit-exact with its specification (kh_kernels.h):
-    16-byte block a mod blocks of shard X[0]; four little-endian u32 words, each with the 4 bits
-    given by 5-bit fields of a 32-bit LCG seeded with a >> 32."""
-    MUL, ADD, SEED = 0x9E3779B1, 0x7F4A7C15, 0x59F2815B16F81798
+    shard X[0]; 16-byte block (u * blocks) >> 32 with u = X[8..12); four little-endian u32 words,
+    each with the 4 bits given by 5-bit fields of a 32-bit LCG seeded with X[12..16)."""
+    MUL, ADD = 0x9E3779B1, 0x7F4A7C15
     info = engine.bsgs_setup(1 << 20, 1, layer1=1)       # M = 1024 babies
     engine.bsgs_build()
     blocks = info.bloom_bits[0] // 128
@@ -145,9 +145,9 @@ def test_blocked_layer1_bytes_match_layout_spec(engine, oracle):
     model = bytearray(256 * blocks * 16)
     for i in range(1, info.m + 1):
         xb = oracle.pubkey(i)[0].to_bytes(32, "big")
-        a = oracle.xxh64(xb, SEED)
-        base = xb[0] * blocks * 16 + (a % blocks) * 16
-        s, fields = a >> 32, []
+        u, s = int.from_bytes(xb[8:12], "big"), int.from_bytes(xb[12:16], "big")
+        base = xb[0] * blocks * 16 + ((u * blocks) >> 32) * 16
+        fields = []
         for _ in range(6):
             s = (s * MUL + ADD) & 0xFFFFFFFF
             fields += [s >> 27, (s >> 22) & 31, (s >> 17) & 31]
