@@ -232,7 +232,8 @@ __device__ __forceinline__ void probe_point(const walk_args &A, const fe &x, con
 }
 
 // Blocked layer-1 probes: each point costs one 16-byte load (its split block) and the word-mask
-// test.  The two points of a giant-step pair issue their loads together.
+// test.  The walk issues a pair's loads one step later and tests them after that step's field
+// math (see k_walk).
 typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
 // 16-byte load with the nontemporal hint: each block is read once, at a random address
 __device__ __forceinline__ uint4 ld_nt16(const uint4 *p) {
@@ -244,24 +245,18 @@ __device__ __forceinline__ uint2 blk_record(const walk_args &A, const fe &x) {
   const uint64_t off = (uint64_t)(x.d[7] >> 24) * A.bd.stride + (uint64_t)blk_index(x.d[5], A.bd) * 16;
   return make_uint2((uint32_t)(off >> 4), x.d[4]);
 }
-__device__ __forceinline__ void blk_probe_pair(const walk_args &A, const fe &x1, uint64_t idx1, const fe &x2,
-                                               uint64_t idx2, bool valid2) {
-#ifdef KH_TIMING_NO_PROBE
-  // timing-only build: no probe at all (outputs are wrong); isolates the walk
-  if ((x1.d[0] ^ x2.d[0]) == 0x9E3779B1u) record_hit(A, idx1, 4);
-  return;
-#endif
-  const uint2 r1 = blk_record(A, x1), r2 = blk_record(A, x2);
-  const uint4 *bl = reinterpret_cast<const uint4 *>(A.bloom);
+__device__ __forceinline__ uint4 blk_load(const walk_args &A, const uint2 &r) {
 #ifdef KH_TIMING_NO_PROBE_LOADS
   // timing-only build: no HBM reads (outputs are wrong); isolates the probe's compute
-  const uint4 v1 = make_uint4(r1.x, r1.x * 3u, r1.x * 5u, r1.x * 7u);
-  const uint4 v2 = make_uint4(r2.x, r2.x * 3u, r2.x * 5u, r2.x * 7u);
+  return make_uint4(r.x, r.x * 3u, r.x * 5u, r.x * 7u);
 #else
-  const uint4 v1 = ld_nt16(bl + r1.x), v2 = ld_nt16(bl + r2.x);
+  return ld_nt16(reinterpret_cast<const uint4 *>(A.bloom) + r.x);
 #endif
-  if (idx1 < A.n_points && blk_match(v1, r1.y)) record_hit(A, idx1, 4);
-  if (valid2 && idx2 < A.n_points && blk_match(v2, r2.y)) record_hit(A, idx2, 4);
+}
+// one blocked probe, in place (the group centre)
+__device__ __forceinline__ void blk_probe(const walk_args &A, const fe &x, uint64_t idx) {
+  const uint2 r = blk_record(A, x);
+  if (idx < A.n_points && blk_match(blk_load(A, r), r.y)) record_hit(A, idx, 4);
 }
 
 // Reference-layout layer-1 probes of two giant-step points in lockstep (keyhunt.cpp:4819-4822
@@ -369,13 +364,16 @@ __global__ void __launch_bounds__(256, walk_lb<MODE>()) k_walk(walk_args A) {
 
     // the centre itself (offset 0)
     if constexpr (MODE == KM_BSGSB)
-      blk_probe_pair(A, cx, cidx, cx, cidx, false);
+      blk_probe(A, cx, cidx);
     else
       probe_point<MODE>(A, cx, cy, cidx);
 
     // backward: recover 1/dx_i and emit C - T[i] (offset -(i+1)) and C + T[i] (offset i+1).
     // Both points use the second operand (T.x, +-T.y): x3 = s^2 - C.x - T.x, y3 = s(T.x - x3) -+ T.y.
     // prefix[i-1] is fetched one iteration ahead so its HBM latency overlaps the previous pair
+    uint2 pm = make_uint2(0u, 0u), pp = make_uint2(0u, 0u);  // KM_BSGSB: previous pair's probe records
+    uint64_t poff = 0;
+    uint32_t plive = 0;
     fe pre;
     scr_load(pre, scr, (size_t)(H - 2) * L + g);
 #pragma unroll 1
@@ -395,7 +393,32 @@ __global__ void __launch_bounds__(256, walk_lb<MODE>()) k_walk(walk_args A) {
       }
       fe nty;
       fe_neg(nty, ty);
-      if constexpr (MODE == KM_BSGS || MODE == KM_BSGSB) {
+      if constexpr (MODE == KM_BSGSB) {
+        // The previous pair's block loads are issued first and tested after this pair's field
+        // math: the loads fly during it.  Only their addresses cross the loop edge (ALU values),
+        // never an in-flight load destination.
+        const uint4 vm = blk_load(A, pm), vp = blk_load(A, pp);
+        fe xm, xp, s, dy;
+        fe_add(dy, ty, cy);  // -(dy of C - T[i]); only s^2 is needed, so the sign drops out
+        fe_mul(s, dy, di);
+        fe_sqr(xm, s);
+        fe_sub(xm, xm, cx);
+        fe_sub(xm, xm, tx);
+        fe_sub(dy, ty, cy);
+        fe_mul(s, dy, di);
+        fe_sqr(xp, s);
+        fe_sub(xp, xp, cx);
+        fe_sub(xp, xp, tx);
+        if ((plive & 1u) && blk_match(vm, pm.y)) record_hit(A, cidx - poff, 4);
+        if ((plive & 2u) && blk_match(vp, pp.y)) record_hit(A, cidx + poff, 4);
+        const uint64_t off = (uint64_t)(i + 1);
+        pm = blk_record(A, xm);
+        pp = blk_record(A, xp);
+        poff = off;
+        plive = (cidx - off < A.n_points ? 1u : 0u) | (i < H - 1 && cidx + off < A.n_points ? 2u : 0u);
+        continue;
+      }
+      if constexpr (MODE == KM_BSGS) {
         // both points first, then one lockstep probe of the pair (two loads in flight per lane)
         fe xm, xp, s, dy;
         fe_sub(dy, nty, cy);
@@ -409,11 +432,7 @@ __global__ void __launch_bounds__(256, walk_lb<MODE>()) k_walk(walk_args A) {
         fe_sub(xp, xp, cx);
         fe_sub(xp, xp, tx);
         const uint64_t off = (uint64_t)(i + 1);
-        if constexpr (MODE == KM_BSGSB) {
-          blk_probe_pair(A, xm, cidx - off, xp, cidx + off, i < H - 1);
-        } else {
-          probe_pair_bsgs(A, xm, cidx - off, xp, cidx + off, i < H - 1);
-        }
+        probe_pair_bsgs(A, xm, cidx - off, xp, cidx + off, i < H - 1);
         continue;
       }
 #pragma unroll 1
@@ -436,6 +455,10 @@ __global__ void __launch_bounds__(256, walk_lb<MODE>()) k_walk(walk_args A) {
         const uint64_t off = (uint64_t)(i + 1);
         probe_point<MODE>(A, x, y, side ? cidx + off : cidx - off);
       }
+    }
+    if constexpr (MODE == KM_BSGSB) {  // the last pair of the group
+      if ((plive & 1u) && blk_match(blk_load(A, pm), pm.y)) record_hit(A, cidx - poff, 4);
+      if ((plive & 2u) && blk_match(blk_load(A, pp), pp.y)) record_hit(A, cidx + poff, 4);
     }
     // next centre C += T[H]  (keyhunt.cpp:3840-3855)
     {
