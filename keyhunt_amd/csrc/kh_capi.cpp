@@ -102,6 +102,16 @@ u256 sc_mul_u64(const u256 &a, uint64_t m) {
   }
   return r;
 }
+// a * b mod n (double-and-add; only used per confirmed hit)
+u256 sc_mul(const u256 &a, const u256 &b) {
+  u256 r = u256_u64(0), x = a;
+  for (int i = 0; i < 4; i++)
+    for (int j = 0; j < 64; j++) {
+      if ((b.v[i] >> j) & 1) r = sc_add(r, x);
+      x = sc_add(x, x);
+    }
+  return r;
+}
 void u256_to_limbs(uint32_t out[8], const u256 &a) {
   for (int i = 0; i < 4; i++) {
     out[2 * i] = (uint32_t)a.v[i];
@@ -629,6 +639,8 @@ int kh_set_targets(kh_ctx *ctx, const uint8_t *rows, uint64_t n, uint64_t bloom_
 int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride_be[32], uint64_t n_keys, uint32_t mode,
             uint32_t search, kh_hit *hits, uint32_t cap, uint32_t *n_hits) {
   if (!ctx || !start || !n_hits || (n_keys % (2 * KH_WALK_H)) || n_keys == 0) return KH_E_ARG;
+  const bool endo = (mode & KH_MODE_ENDO) != 0;
+  mode &= ~(uint32_t)KH_MODE_ENDO;
   if (mode > KH_MODE_XPOINT || search > KH_SEARCH_BOTH) return KH_E_ARG;
   if (!ctx->d_tbloom) return KH_E_STATE;
   (void)hipSetDevice(ctx->device);
@@ -668,6 +680,7 @@ int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride_be[32], u
          : search == KH_SEARCH_COMPRESS ? KM_H160C
          : search == KH_SEARCH_UNCOMPRESS ? KM_H160U
                                           : KM_H160B;
+  if (endo) km |= KM_ENDO;
   walk_args A;
   memset(&A, 0, sizeof A);
   A.tab = tab;
@@ -689,11 +702,27 @@ int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride_be[32], u
   r = fetch_hits(ctx, nd);
   if (r) return r;
 
-  // confirm each bloom hit against the sorted table and resolve the key (keyhunt.cpp:3619-3636)
+  // Confirm each bloom hit against the sorted table and resolve the key: parity fix-up
+  // (keyhunt.cpp:3619-3636); with -e the image e gives key * lambda^e, and the 04 variants with
+  // -Y the negated key (keyhunt.cpp:3525-3700, 3765-3800).  Hits come out in the order one
+  // reference thread prints them: per point, compressed variants (image-major), then
+  // uncompressed, then xpoint.
+  auto order = [](uint32_t kind) {
+    uint32_t base = kind & 15u, e = (kind >> KH_DKIND_ENDO_SHIFT) & 3u, neg = (kind & KH_DKIND_NEG) ? 1u : 0u;
+    return base < 2 ? 2 * e + base : base == 2 ? 6 + 2 * e + neg : 12 + e;
+  };
   std::vector<kh_dev_hit> dh(ctx->h_hits.begin(), ctx->h_hits.begin() + nd);
-  std::sort(dh.begin(), dh.end(), [](const kh_dev_hit &a, const kh_dev_hit &b) {
-    return a.idx != b.idx ? a.idx < b.idx : a.kind < b.kind;
+  std::sort(dh.begin(), dh.end(), [&](const kh_dev_hit &a, const kh_dev_hit &b) {
+    return a.idx != b.idx ? a.idx < b.idx : order(a.kind) < order(b.kind);
   });
+  static const u256 LAMBDA[3] = {
+      u256_u64(1),
+      u256{{0xdf02967c1b23bd72ULL, 0x122e22ea20816678ULL, 0xa5261c028812645aULL, 0x5363ad4cc05c30e0ULL}},
+      u256{{0xe0cfc810b51283ceULL, 0xa880b9fc8ec739c2ULL, 0x5ad9e3fd77ed9ba4ULL, 0xac9c52b33fa3cf1fULL}}};
+  static const fe BETA[3] = {
+      fe{{1, 0, 0, 0, 0, 0, 0, 0}},
+      fe{{0x719501eeu, 0xc1396c28u, 0x12f58995u, 0x9cf04975u, 0xac3434e9u, 0x6e64479eu, 0x657c0710u, 0x7ae96a2bu}},
+      fe{{0x8e6afa40u, 0x3ec693d6u, 0xed0a766au, 0x630fb68au, 0x53cbcb16u, 0x919bb861u, 0x9a83f8efu, 0x851695d4u}}};
   std::vector<kh_hit> out;
   for (auto &h : dh) {
     u256 k = sc_add(st, sc_reduce(u256_from_u128((u128)h.idx)));
@@ -707,25 +736,33 @@ int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride_be[32], u
     }
     ge P;
     if (!ctx->comb.mult(P, k)) continue;
+    const uint32_t base = h.kind & 15u, e = (h.kind >> KH_DKIND_ENDO_SHIFT) & 3u;
+    const bool neg = (h.kind & KH_DKIND_NEG) != 0;
+    if (e > 2) continue;
+    fe xe = P.x, ye = P.y;
+    if (e) fe_mul(xe, P.x, BETA[e]);
+    if (neg) fe_neg(ye, P.y);
     uint8_t probe[20];
     uint32_t w[5];
     bool compressed = false;
-    if (h.kind == KH_KIND_02 || h.kind == KH_KIND_03) {
-      hash160_comp(P.x, 2 + h.kind, w);
+    if (base == KH_KIND_02 || base == KH_KIND_03) {
+      hash160_comp(xe, 2 + base, w);
       compressed = true;
-    } else if (h.kind == KH_KIND_04) {
-      hash160_uncomp(P.x, P.y, w);
+    } else if (base == KH_KIND_04) {
+      hash160_uncomp(xe, ye, w);
     } else {
-      for (int j = 0; j < 5; j++) w[j] = bswap32(P.x.d[7 - j]);
+      for (int j = 0; j < 5; j++) w[j] = bswap32(xe.d[7 - j]);
     }
     memcpy(probe, w, 20);
     if (!searchbinary(ctx->rows.data(), (int64_t)ctx->n_rows, probe, 20, 0)) continue;
     kh_hit o;
     memset(&o, 0, sizeof o);
-    u256 kr = k;
+    u256 kr = e ? sc_mul(k, LAMBDA[e]) : k;  // (beta^e x, y) = lambda^e * (x, y)
     if (compressed) {
-      uint32_t odd = P.y.d[0] & 1;
-      if (odd != (h.kind == KH_KIND_03 ? 1u : 0u)) kr = sc_neg(k);
+      uint32_t odd = P.y.d[0] & 1;  // the image keeps Y
+      if (odd != (base == KH_KIND_03 ? 1u : 0u)) kr = sc_neg(kr);
+    } else if (neg) {
+      kr = sc_neg(kr);
     }
     u256_to_be(o.key, kr);
     o.offset = h.idx;

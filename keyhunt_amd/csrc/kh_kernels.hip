@@ -154,43 +154,104 @@ __device__ __forceinline__ void x_bytes_u64(const fe &x, uint64_t in[4]) {
     in[k] = (uint64_t)bswap32(x.d[7 - 2 * k]) | ((uint64_t)bswap32(x.d[6 - 2 * k]) << 32);
 }
 
+// hash160(02||X) and hash160(03||X) of one x-coordinate into the target bloom; kinds 0/1 | tag
+__device__ __forceinline__ void probe_comp(const walk_args &A, const fe &x, uint64_t idx, uint32_t tag) {
+#if KH_HASH_PAIR
+  uint32_t hh[2][5];
+  hash160_comp2(x, hh[0], hh[1]);
+#pragma unroll 1
+  for (uint32_t k = 0; k < 2; k++) {
+    uint32_t h[5];
+#pragma unroll
+    for (int q = 0; q < 5; q++) h[q] = k ? hh[1][q] : hh[0][q];
+    uint64_t a = xxh64_20(h, KH_BLOOM_SEED);
+    if (bloom_probe_lazy(A.bloom, A.bd, a, [&](uint64_t s) { return xxh64_20(h, s); })) record_hit(A, idx, k | tag);
+  }
+#else
+#pragma unroll 1
+  for (uint32_t pfx = 2; pfx <= 3; pfx++) {
+    uint32_t h[5];
+    hash160_comp(x, pfx, h);
+    uint64_t a = xxh64_20(h, KH_BLOOM_SEED);
+    if (bloom_probe_lazy(A.bloom, A.bd, a, [&](uint64_t s) { return xxh64_20(h, s); }))
+      record_hit(A, idx, (pfx - 2) | tag);
+  }
+#endif
+}
+// hash160(04||X||Y); kind 2 | tag
+__device__ __forceinline__ void probe_uncomp(const walk_args &A, const fe &x, const fe &y, uint64_t idx, uint32_t tag) {
+  uint32_t h[5];
+  hash160_uncomp(x, y, h);
+  uint64_t a = xxh64_20(h, KH_BLOOM_SEED);
+  if (bloom_probe_lazy(A.bloom, A.bd, a, [&](uint64_t s) { return xxh64_20(h, s); })) record_hit(A, idx, 2 | tag);
+}
+// X[0..20); kind 3 | tag
+__device__ __forceinline__ void probe_xpoint(const walk_args &A, const fe &x, uint64_t idx, uint32_t tag) {
+  uint32_t w[5];
+#pragma unroll
+  for (int j = 0; j < 5; j++) w[j] = bswap32(x.d[7 - j]);
+  uint64_t a = xxh64_20(w, KH_BLOOM_SEED);
+  if (bloom_probe_lazy(A.bloom, A.bd, a, [&](uint64_t s) { return xxh64_20(w, s); })) record_hit(A, idx, 3 | tag);
+}
+// beta and beta^2 (cube roots of unity mod p): lambda*(x, y) = (beta*x, y) (-e, keyhunt.cpp:926-930)
+__device__ __forceinline__ void endo_beta(fe &b, int e) {
+  const uint32_t B1[8] = {0x719501eeu, 0xc1396c28u, 0x12f58995u, 0x9cf04975u,
+                          0xac3434e9u, 0x6e64479eu, 0x657c0710u, 0x7ae96a2bu};
+  const uint32_t B2[8] = {0x8e6afa40u, 0x3ec693d6u, 0xed0a766au, 0x630fb68au,
+                          0x53cbcb16u, 0x919bb861u, 0x9a83f8efu, 0x851695d4u};
+#pragma unroll
+  for (int i = 0; i < 8; i++) b.d[i] = e == 1 ? B1[i] : B2[i];
+}
+
 template <int MODE>
 __device__ __forceinline__ void probe_point(const walk_args &A, const fe &x, const fe &y, uint64_t idx) {
   if (idx >= A.n_points) return;
-  if constexpr (MODE == KM_H160C || MODE == KM_H160B) {
-#if KH_HASH_PAIR
-    uint32_t hh[2][5];
-    hash160_comp2(x, hh[0], hh[1]);
+  constexpr int BASE = MODE & 15;
+  constexpr bool ENDO = (MODE & KM_ENDO) != 0;
+  if constexpr (BASE == KM_H160C || BASE == KM_H160B || BASE == KM_H160U || BASE == KM_XPOINT) {
+    // images e = 0 (X), then with -e: 1 (beta*X) and 2 (beta^2*X); per point the reference
+    // checks every compressed variant before the uncompressed ones (keyhunt.cpp:3476-3700)
+    if constexpr (BASE == KM_H160C || BASE == KM_H160B) {
+      probe_comp(A, x, idx, 0);
+      if constexpr (ENDO) {
 #pragma unroll 1
-    for (uint32_t k = 0; k < 2; k++) {
-      uint32_t h[5];
-#pragma unroll
-      for (int q = 0; q < 5; q++) h[q] = k ? hh[1][q] : hh[0][q];
-      uint64_t a = xxh64_20(h, KH_BLOOM_SEED);
-      if (bloom_probe_lazy(A.bloom, A.bd, a, [&](uint64_t s) { return xxh64_20(h, s); })) record_hit(A, idx, k);
+        for (int e = 1; e <= 2; e++) {
+          fe b, xe;
+          endo_beta(b, e);
+          fe_mul(xe, x, b);
+          probe_comp(A, xe, idx, (uint32_t)e << KH_DKIND_ENDO_SHIFT);
+        }
+      }
     }
-#else
+    if constexpr (BASE == KM_H160U || BASE == KM_H160B) {
+      probe_uncomp(A, x, y, idx, 0);
+      if constexpr (ENDO) {  // (X, -Y) and both images with +-Y
+        fe ny;
+        fe_neg(ny, y);
+        probe_uncomp(A, x, ny, idx, KH_DKIND_NEG);
 #pragma unroll 1
-    for (uint32_t pfx = 2; pfx <= 3; pfx++) {
-      uint32_t h[5];
-      hash160_comp(x, pfx, h);
-      uint64_t a = xxh64_20(h, KH_BLOOM_SEED);
-      if (bloom_probe_lazy(A.bloom, A.bd, a, [&](uint64_t s) { return xxh64_20(h, s); })) record_hit(A, idx, pfx - 2);
+        for (int e = 1; e <= 2; e++) {
+          fe b, xe;
+          endo_beta(b, e);
+          fe_mul(xe, x, b);
+          probe_uncomp(A, xe, y, idx, (uint32_t)e << KH_DKIND_ENDO_SHIFT);
+          probe_uncomp(A, xe, ny, idx, ((uint32_t)e << KH_DKIND_ENDO_SHIFT) | KH_DKIND_NEG);
+        }
+      }
     }
-#endif
-  }
-  if constexpr (MODE == KM_H160U || MODE == KM_H160B) {
-    uint32_t h[5];
-    hash160_uncomp(x, y, h);
-    uint64_t a = xxh64_20(h, KH_BLOOM_SEED);
-    if (bloom_probe_lazy(A.bloom, A.bd, a, [&](uint64_t s) { return xxh64_20(h, s); })) record_hit(A, idx, 2);
-  }
-  if constexpr (MODE == KM_XPOINT) {
-    uint32_t w[5];
-#pragma unroll
-    for (int j = 0; j < 5; j++) w[j] = bswap32(x.d[7 - j]);
-    uint64_t a = xxh64_20(w, KH_BLOOM_SEED);
-    if (bloom_probe_lazy(A.bloom, A.bd, a, [&](uint64_t s) { return xxh64_20(w, s); })) record_hit(A, idx, 3);
+    if constexpr (BASE == KM_XPOINT) {
+      probe_xpoint(A, x, idx, 0);
+      if constexpr (ENDO) {
+#pragma unroll 1
+        for (int e = 1; e <= 2; e++) {
+          fe b, xe;
+          endo_beta(b, e);
+          fe_mul(xe, x, b);
+          probe_xpoint(A, xe, idx, (uint32_t)e << KH_DKIND_ENDO_SHIFT);
+        }
+      }
+    }
+    return;
   }
   if constexpr (MODE == KM_BSGS) {
     uint64_t in[4];
@@ -308,7 +369,7 @@ __device__ __forceinline__ void probe_pair_bsgs(const walk_args &A, const fe &x1
 
 template <int MODE>
 constexpr bool needs_y() {
-  return MODE == KM_H160U || MODE == KM_H160B || MODE == KM_DUMP;
+  return (MODE & 15) == KM_H160U || (MODE & 15) == KM_H160B || MODE == KM_DUMP;
 }
 
 }  // namespace
@@ -320,7 +381,7 @@ constexpr bool needs_y() {
 // 4 waves/SIMD even with a few spills; the hash160 modes prefer 3).
 template <int MODE>
 constexpr int walk_lb() {
-  return (MODE == KM_H160C || MODE == KM_H160U || MODE == KM_H160B) ? KH_WALK_LB_HASH
+  return ((MODE & 15) == KM_H160C || (MODE & 15) == KM_H160U || (MODE & 15) == KM_H160B) ? KH_WALK_LB_HASH
          : MODE == KM_DUMP                                          ? 2
                                                                     : KH_WALK_LB;
 }
@@ -611,6 +672,10 @@ hipError_t launch_walk(int mode, const walk_args &A, hipStream_t st) {
     case KM_DUMP: hipLaunchKernelGGL(k_walk<KM_DUMP>, grid, block, 0, st, A); break;
     case KM_BSGSB: hipLaunchKernelGGL(k_walk<KM_BSGSB>, grid, block, 0, st, A); break;
     case KM_BUILDB: hipLaunchKernelGGL(k_walk<KM_BUILDB>, grid, block, 0, st, A); break;
+    case KM_H160C | KM_ENDO: hipLaunchKernelGGL(k_walk<KM_H160C | KM_ENDO>, grid, block, 0, st, A); break;
+    case KM_H160U | KM_ENDO: hipLaunchKernelGGL(k_walk<KM_H160U | KM_ENDO>, grid, block, 0, st, A); break;
+    case KM_H160B | KM_ENDO: hipLaunchKernelGGL(k_walk<KM_H160B | KM_ENDO>, grid, block, 0, st, A); break;
+    case KM_XPOINT | KM_ENDO: hipLaunchKernelGGL(k_walk<KM_XPOINT | KM_ENDO>, grid, block, 0, st, A); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

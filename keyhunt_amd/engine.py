@@ -18,8 +18,10 @@ LIB_PATH = os.environ.get("KH_LIB") or os.path.join(PKG, "lib", "libkh_gpu.so")
 HEADER = os.path.join(REPO, "include", "kh_gpu.h")
 
 KH_MODE_ADDRESS, KH_MODE_XPOINT = 0, 1
+KH_MODE_ENDO = 0x10  # OR into mode: -e
 KH_SEARCH_COMPRESS, KH_SEARCH_UNCOMPRESS, KH_SEARCH_BOTH = 0, 1, 2
 KH_KIND_02, KH_KIND_03, KH_KIND_04, KH_KIND_XPOINT = 0, 1, 2, 3
+KH_KIND_ENDO1, KH_KIND_ENDO2, KH_KIND_NEGY = 0x10, 0x20, 0x40
 TIME_ADDRESS, TIME_XPOINT, TIME_BSGS, TIME_BUILD, TIME_SETUP = 0, 1, 2, 3, 4
 KH_LAYER1_REFERENCE, KH_LAYER1_BLOCKED = 0, 1
 
@@ -168,10 +170,12 @@ class Engine:
         self._chk(lib().kh_set_targets(self._ctx, buf, len(rows), bloom_items), "kh_set_targets")
 
     def scan(self, start: int, n_keys: int, mode: int = KH_MODE_ADDRESS, search: int = KH_SEARCH_BOTH,
-             stride: int = 1, cap: int = 4096) -> list[ScanHit]:
+             stride: int = 1, cap: int = 4096, endo: bool = False) -> list[ScanHit]:
+        """endo: -e (also the endomorphism images; hit kinds then carry KH_KIND_ENDO1/2, KH_KIND_NEGY)."""
         hits = (KhHit * cap)()
         n = ctypes.c_uint32(0)
-        r = lib().kh_scan(self._ctx, be32(start), be32(stride), n_keys, mode, search, hits, cap, ctypes.byref(n))
+        r = lib().kh_scan(self._ctx, be32(start), be32(stride), n_keys, mode | (KH_MODE_ENDO if endo else 0), search,
+                          hits, cap, ctypes.byref(n))
         self._chk(r, "kh_scan")
         return [ScanHit(int.from_bytes(bytes(h.key), "big"), h.offset, h.kind, bool(h.compressed))
                 for h in hits[: n.value]]

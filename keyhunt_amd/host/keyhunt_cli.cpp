@@ -331,6 +331,8 @@ struct options {
   bool matrix = false;
   uint32_t layer1 = KH_LAYER1_BLOCKED;
   bool random = false;  // -R
+  bool endo = false;    // -e
+  bool stride_set = false;
   int bsgs_mode = 0;    // -B, index into BSGS_MODES
 } opt;
 // keyhunt.cpp:419; ggsb (re-blocked baby tables) is not provided, angrygiant walks like sequential
@@ -534,7 +536,10 @@ U keys_done(const U &twoN) {
     return t;
   }
   U t = u_mul_u64(u_from_u64(1024), g_groups_done.load());
-  if (opt.search == KH_SEARCH_COMPRESS) t = u_mul_u64(t, 2);
+  if (opt.endo)  // keyhunt.cpp:2883-2891
+    t = u_mul_u64(t, opt.mode == MODE_XPOINT ? 3 : 6);
+  else if (opt.search == KH_SEARCH_COMPRESS)
+    t = u_mul_u64(t, 2);
   return t;
 }
 
@@ -578,7 +583,8 @@ void addr_worker(addr_job *j) {
     if (opt.matrix) printf("Base key: %s gpu %d\n", u_hex(base).c_str(), j->device);
     u_to_be32(base, st_be);
     uint32_t nh = 0;
-    r = kh_scan(ctx, st_be, stride_be, j->nseq, opt.mode == MODE_XPOINT ? KH_MODE_XPOINT : KH_MODE_ADDRESS,
+    r = kh_scan(ctx, st_be, stride_be, j->nseq,
+                (opt.mode == MODE_XPOINT ? KH_MODE_XPOINT : KH_MODE_ADDRESS) | (opt.endo ? KH_MODE_ENDO : 0),
                 (uint32_t)opt.search, hits.data(), (uint32_t)hits.size(), &nh);
     if (r) {
       fprintf(stderr, "[E] kh_scan: %s (%s)\n", kh_strerror(r), kh_last_error(ctx));
@@ -802,6 +808,7 @@ int main(int argc, char **argv) {
         bool ok = (optarg[0] == '0' && optarg[1] == 'x') ? u_from_hex(optarg, s) : u_from_dec(optarg, s);
         if (!ok || u_is_zero(s)) { fprintf(stderr, "[E] invalid stride %s\n", optarg); return EXIT_FAILURE; }
         opt.stride = s;
+        opt.stride_set = true;
         break;
       }
       case 'M': opt.matrix = true; break;
@@ -829,7 +836,11 @@ int main(int argc, char **argv) {
         }
         break;
       }
-      case 'e': case 'c': case 'S':
+      case 'e':  // keyhunt.cpp:925-931
+        opt.endo = true;
+        printf("[+] Endomorphism enabled\n");
+        break;
+      case 'c': case 'S':
         fprintf(stderr, "[E] -%c is outside the scope of this engine\n", c);
         return EXIT_FAILURE;
       default: usage(argv[0]); return EXIT_FAILURE;
@@ -844,7 +855,13 @@ int main(int argc, char **argv) {
   uint64_t nk_n = 0x100000000000ULL;
   if (opt.flag_n) nk_n = (opt.str_n[0] == '0' && (opt.str_n[1] == 'x' || opt.str_n[1] == 'X')) ? strtoull(opt.str_n + 2, nullptr, 16) : strtoull(opt.str_n, nullptr, 10);
   if (!validate_nk(nk_n, opt.kfactor)) return EXIT_FAILURE;
-  if (opt.mode == MODE_BSGS && u_cmp(opt.stride, u_from_u64(1)) != 0) {
+  // keyhunt.cpp:1185-1193 compares the -B index with MODE_BSGS (2), i.e. these two guards fire
+  // for -B both whatever -m is (SURVEY 8a parity note 7); BSGS itself ignores -e and -I
+  if (opt.bsgs_mode == BM_BOTH && opt.endo) {
+    fprintf(stderr, "[E] Endomorphism doesn't work with BSGS\n");
+    return EXIT_FAILURE;
+  }
+  if (opt.bsgs_mode == BM_BOTH && opt.stride_set) {
     fprintf(stderr, "[E] Stride doesn't work with BSGS\n");
     return EXIT_FAILURE;
   }

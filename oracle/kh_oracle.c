@@ -276,6 +276,15 @@ static void sc_neg(fe *r, const fe *a) {
   if (u256_is_zero(a)) { *r = *a; return; }
   u256_sub(r, &SC_N, a);
 }
+/* r = a * b mod n (Int::ModMulK1order, used with lambda for -e) by double-and-add */
+static void sc_mul(fe *r, const fe *a, const fe *b) {
+  fe acc = {{0, 0, 0, 0}}, x = *a;
+  for (int i = 0; i < 256; i++) {
+    if ((b->v[i >> 6] >> (i & 63)) & 1) sc_add(&acc, &acc, &x);
+    sc_add(&x, &x, &x);
+  }
+  *r = acc;
+}
 
 /* ------------------------------------------------------------------------------------------ */
 /* SHA-256 (FIPS 180-4), RIPEMD-160 (Dobbertin/Bosselaers/Preneel).  Reference: hash/sha256.cpp */
@@ -667,50 +676,99 @@ typedef struct {
   int32_t kind;   /* 0 = 02||X, 1 = 03||X, 2 = 04||X||Y, 3 = xpoint */
 } or_hit;
 
-int or_scan_chunk(int mode, int search, const uint8_t start_be[32], uint64_t n_keys,
-                  const uint8_t *rows, int64_t n_rows, const uint8_t *bf, uint64_t bits, uint32_t hashes,
-                  or_hit *hits, int cap) {
+/* -e constants (keyhunt.cpp:926-930): lambda*(x, y) = (beta*x, y) */
+static const fe END_BETA[3] = {{{1, 0, 0, 0}},
+                               {{0xc1396c28719501eeULL, 0x9cf0497512f58995ULL, 0x6e64479eac3434e9ULL, 0x7ae96a2b657c0710ULL}},
+                               {{0x3ec693d68e6afa40ULL, 0x630fb68aed0a766aULL, 0x919bb86153cbcb16ULL, 0x851695d49a83f8efULL}}};
+static const fe END_LAMBDA[3] = {{{1, 0, 0, 0}},
+                                 {{0xdf02967c1b23bd72ULL, 0x122e22ea20816678ULL, 0xa5261c028812645aULL, 0x5363ad4cc05c30e0ULL}},
+                                 {{0xe0cfc810b51283ceULL, 0xa880b9fc8ec739c2ULL, 0x5ad9e3fd77ed9ba4ULL, 0xac9c52b33fa3cf1fULL}}};
+
+static void push_hit(or_hit *hits, int cap, int *nh, const fe *k, int compressed, int kind) {
+  if (*nh < cap) { fe_to_be(hits[*nh].key, k); hits[*nh].compressed = compressed; hits[*nh].kind = kind; }
+  (*nh)++;
+}
+
+/* thread_process for one chunk (keyhunt.cpp:3349-3830): per point, the compressed variants, then
+ * the uncompressed ones; with endo (-e) each over the images e = 0, 1, 2 (beta^e * X), the 04
+ * variants also over (X, -Y).  Kinds: base (0: 02, 1: 03, 2: 04, 3: xpoint) | e << 4 | neg << 6.
+ * scan_groups does groups [g0, g1) of the chunk into its own hit list. */
+typedef struct {
+  int mode, search, endo;
+  fe start;
+  uint64_t g0, g1;
+  const uint8_t *rows; int64_t n_rows; const uint8_t *bf; uint64_t bits; uint32_t hashes;
+  or_hit *hits; int cap, nh;
+} scan_job;
+
+static void *scan_groups(void *arg) {
+  scan_job *J = (scan_job *)arg;
+  const int mode = J->mode, search = J->search, endo = J->endo;
+  const uint8_t *rows = J->rows, *bf = J->bf;
+  const int64_t n_rows = J->n_rows;
+  const uint64_t bits = J->bits;
+  const uint32_t hashes = J->hashes;
+  or_hit *hits = J->hits;
+  const int cap = J->cap;
   int nh = 0;
   int need_y = (search == 1 || search == 2);
+  int ne = endo ? 3 : 1;
   fe key, one = {{1, 0, 0, 0}};
-  fe_from_be(&key, start_be);
+  u256_add_u64(&key, &J->start, J->g0 * GRP);
   uint8_t onebe[32]; fe_to_be(onebe, &one);
-  uint64_t groups = n_keys / GRP;
   uint8_t *xs = (uint8_t *)malloc(GRP * 32), *ys = (uint8_t *)malloc(GRP * 32);
-  for (uint64_t g = 0; g < groups; g++) {
+  for (uint64_t g = J->g0; g < J->g1; g++) {
     uint8_t kb[32]; fe_to_be(kb, &key);
     or_walk_points(kb, onebe, 1, xs, need_y ? ys : 0);
     for (int t = 0; t < GRP; t++) {
-      const uint8_t *x = xs + t * 32;
       fe kf; u256_add_u64(&kf, &key, (uint64_t)t);
-      if (mode == 1) {
-        if (or_bloom_check(bf, bits, hashes, x, 20) && or_searchbinary(rows, n_rows, x, 20, 0)) {
-          if (nh < cap) { fe_to_be(hits[nh].key, &kf); hits[nh].compressed = 0; hits[nh].kind = 3; }
-          nh++;
-        }
+      fe x0; fe_from_be(&x0, xs + t * 32);
+      uint8_t xe[3][32];
+      for (int e = 0; e < ne; e++) { fe v; fe_mul(&v, &x0, &END_BETA[e]); fe_to_be(xe[e], &v); }
+      if (mode == 1) {  /* xpoint (keyhunt.cpp:3801-3824) */
+        for (int e = 0; e < ne; e++)
+          if (or_bloom_check(bf, bits, hashes, xe[e], 20) && or_searchbinary(rows, n_rows, xe[e], 20, 0)) {
+            fe kr; sc_mul(&kr, &kf, &END_LAMBDA[e]);
+            push_hit(hits, cap, &nh, &kr, 0, 3 | (e << 4));
+          }
         continue;
       }
       if (search == 0 || search == 2) {
-        for (int l = 0; l < 2; l++) {
+        for (int l = 0; l < 2 * ne; l++) {
+          int e = l / 2, pfx = l % 2;
           uint8_t h[20];
-          or_hash160_comp(x, (uint8_t)(2 + l), h);
+          or_hash160_comp(xe[e], (uint8_t)(2 + pfx), h);
           if (or_bloom_check(bf, bits, hashes, h, 20) && or_searchbinary(rows, n_rows, h, 20, 0)) {
-            /* keyhunt.cpp:3619-3636: recompute the pubkey, negate the key if the parity differs */
+            /* keyhunt.cpp:3525-3600 / 3619-3636: the image keeps Y; negate when its parity
+               disagrees with the matched prefix */
             ge P; scalar_mult_g(&P, &kf);
+            fe kr; sc_mul(&kr, &kf, &END_LAMBDA[e]);
             int odd = (int)(P.y.v[0] & 1);
-            fe kr = kf;
-            if (odd != l) sc_neg(&kr, &kf);
-            if (nh < cap) { fe_to_be(hits[nh].key, &kr); hits[nh].compressed = 1; hits[nh].kind = l; }
-            nh++;
+            if (odd != pfx) sc_neg(&kr, &kr);
+            push_hit(hits, cap, &nh, &kr, 1, pfx | (e << 4));
           }
         }
       }
       if (search == 1 || search == 2) {
-        uint8_t h[20];
-        or_hash160_uncomp(x, ys + t * 32, h);
-        if (or_bloom_check(bf, bits, hashes, h, 20) && or_searchbinary(rows, n_rows, h, 20, 0)) {
-          if (nh < cap) { fe_to_be(hits[nh].key, &kf); hits[nh].compressed = 0; hits[nh].kind = 2; }
-          nh++;
+        fe y0; fe_from_be(&y0, ys + t * 32);
+        fe ny; fe_neg(&ny, &y0);
+        uint8_t yb[2][32];
+        fe_to_be(yb[0], &y0); fe_to_be(yb[1], &ny);
+        for (int l = 0; l < (endo ? 6 : 1); l++) {
+          int e = l / 2, neg = l % 2;
+          uint8_t h[20];
+          or_hash160_uncomp(xe[e], yb[neg], h);
+          if (or_bloom_check(bf, bits, hashes, h, 20) && or_searchbinary(rows, n_rows, h, 20, 0)) {
+            fe kr; sc_mul(&kr, &kf, &END_LAMBDA[e]);
+            if (endo) {  /* keyhunt.cpp:3643-3680: keep the key whose 04-hash is the match */
+              ge P; scalar_mult_g(&P, &kr);
+              uint8_t px[32], py[32], h2[20];
+              fe_to_be(px, &P.x); fe_to_be(py, &P.y);
+              or_hash160_uncomp(px, py, h2);
+              if (memcmp(h2, h, 20) != 0) sc_neg(&kr, &kr);
+            }
+            push_hit(hits, cap, &nh, &kr, 0, 2 | (e << 4) | (neg << 6));
+          }
         }
       }
     }
@@ -718,7 +776,44 @@ int or_scan_chunk(int mode, int search, const uint8_t start_be[32], uint64_t n_k
     u256_add(&key, &key, &k1024);
   }
   free(xs); free(ys);
+  J->nh = nh;
+  return 0;
+}
+
+/* the chunk on up to 16 threads (contiguous group ranges, hits concatenated in key order) */
+int or_scan_chunk2(int mode, int search, int endo, const uint8_t start_be[32], uint64_t n_keys,
+                   const uint8_t *rows, int64_t n_rows, const uint8_t *bf, uint64_t bits, uint32_t hashes,
+                   or_hit *hits, int cap) {
+  uint64_t groups = n_keys / GRP;
+  int nt = (int)(groups < 16 ? (groups ? groups : 1) : 16);
+  scan_job *jobs = (scan_job *)calloc(nt, sizeof(scan_job));
+  pthread_t *th = (pthread_t *)calloc(nt, sizeof(pthread_t));
+  for (int i = 0; i < nt; i++) {
+    scan_job *J = &jobs[i];
+    J->mode = mode; J->search = search; J->endo = endo;
+    fe_from_be(&J->start, start_be);
+    J->g0 = groups * i / nt; J->g1 = groups * (i + 1) / nt;
+    J->rows = rows; J->n_rows = n_rows; J->bf = bf; J->bits = bits; J->hashes = hashes;
+    J->cap = cap; J->hits = (or_hit *)calloc(cap > 0 ? cap : 1, sizeof(or_hit));
+    pthread_create(&th[i], 0, scan_groups, J);
+  }
+  int nh = 0;
+  for (int i = 0; i < nt; i++) {
+    pthread_join(th[i], 0);
+    for (int j = 0; j < jobs[i].nh; j++) {
+      if (nh < cap && j < jobs[i].cap) hits[nh] = jobs[i].hits[j];
+      nh++;
+    }
+    free(jobs[i].hits);
+  }
+  free(jobs); free(th);
   return nh;
+}
+
+int or_scan_chunk(int mode, int search, const uint8_t start_be[32], uint64_t n_keys,
+                  const uint8_t *rows, int64_t n_rows, const uint8_t *bf, uint64_t bits, uint32_t hashes,
+                  or_hit *hits, int cap) {
+  return or_scan_chunk2(mode, search, 0, start_be, n_keys, rows, n_rows, bf, bits, hashes, hits, cap);
 }
 
 /* ------------------------------------------------------------------------------------------ */

@@ -37,6 +37,14 @@ E2E_RUNS = [
     ("address_66_window", ["-m", "address", "-f", "66.txt", "-l", "compress", "-r", "2832ed74f2b400000:2832ed74f2b7fffff", "-n", "0x100000", "-t", "8"], 600),
     ("rmd160_64_window", ["-m", "rmd160", "-f", "64.rmd", "-l", "compress", "-r", "f7051f27b0000000:f7051f27b0ffffff", "-n", "0x100000", "-t", "8"], 600),
     ("xpoint_63_window", ["-m", "xpoint", "-f", "63.pub", "-r", "7cce5efdac000000:7cce5efdacffffff", "-n", "0x100000", "-t", "8"], 600),
+    # -e (endomorphism: (beta*X, Y) and (beta^2*X, Y) checked too, keyhunt.cpp:3408-3830)
+    ("address_1to32_2p20_endo", ["-m", "address", "-f", "1to32.txt", "-r", "1:100000", "-n", "0x100000", "-e", "-t", "8"], 300),
+    ("rmd160_1to32_compress_2p20_endo", ["-m", "rmd160", "-f", "1to32.rmd", "-l", "compress", "-r", "1:100000", "-n", "0x100000", "-e", "-t", "8"], 300),
+    ("xpoint_1to63_65_2p20_endo", ["-m", "xpoint", "-f", "1to63_65.txt", "-r", "1:100000", "-n", "0x100000", "-e", "-t", "8"], 300),
+    # targets built from lambda-multiples of small keys (tests/golden/make_endo_targets.py)
+    ("address_endo_targets", ["-m", "address", "-f", "endo_addr.txt", "-r", "1:100000", "-n", "0x100000", "-e", "-t", "8"], 300),
+    ("address_endo_targets_no_e", ["-m", "address", "-f", "endo_addr.txt", "-r", "1:100000", "-n", "0x100000", "-t", "8"], 300),
+    ("xpoint_endo_targets", ["-m", "xpoint", "-f", "endo_x.txt", "-r", "1:100000", "-n", "0x100000", "-e", "-t", "8"], 300),
     ("bsgs_120_window", ["-m", "bsgs", "-f", "120.txt", "-r", "b10f22572c497a836e9d0000000000:b10f22572c497a836edd0000000000", "-t", "8"], 300),
     ("bsgs_125_window", ["-m", "bsgs", "-f", "125.txt", "-r", "1c533b6bb7f0804e0995fe0000000000:1c533b6bb7f0804e09963e0000000000", "-t", "8"], 300),
     ("bsgs_130_window", ["-m", "bsgs", "-f", "130.txt", "-r", "33e7665705359f04f28b8880000000000:33e7665705359f04f28b8c80000000000", "-t", "8"], 300),

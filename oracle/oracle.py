@@ -183,15 +183,18 @@ MODE_XPOINT = 1
 SEARCH_COMPRESS, SEARCH_UNCOMPRESS, SEARCH_BOTH = 0, 1, 2
 
 
-def scan_chunk(mode: int, search: int, start: int, n_keys: int, rows: list[bytes], cap: int = 4096):
-    """Reference hit list for one chunk (thread_process).  rows: 20-byte targets (unsorted ok)."""
+def scan_chunk(mode: int, search: int, start: int, n_keys: int, rows: list[bytes], cap: int = 4096,
+               endo: bool = False):
+    """Reference hit list for one chunk (thread_process).  rows: 20-byte targets (unsorted ok).
+    endo: -e (kinds then carry the image e << 4 and, for 04 hashes, the Y sign << 6)."""
     srt = sorted(rows)
     table = b"".join(srt)
     bloom = Bloom(len(srt))
     for r in srt:
         bloom.add(r)
     hits = (OrHit * cap)()
-    n = lib().or_scan_chunk(ctypes.c_int(mode), ctypes.c_int(search), be32(start), ctypes.c_uint64(n_keys),
+    n = lib().or_scan_chunk2(ctypes.c_int(mode), ctypes.c_int(search), ctypes.c_int(1 if endo else 0), be32(start),
+                             ctypes.c_uint64(n_keys),
                             table, ctypes.c_int64(len(srt)), bloom.bf, ctypes.c_uint64(bloom.bits),
                             ctypes.c_uint32(bloom.hashes), hits, ctypes.c_int(cap))
     return [(int.from_bytes(bytes(h.key), "big"), bool(h.compressed), int(h.kind)) for h in hits[: min(n, cap)]]

@@ -48,7 +48,12 @@ def test_cli_rejects_out_of_scope_and_bad_nk(tmp_path):
     assert r.returncode == 1 and "n must be at least 2^20" in r.stderr
     r = subprocess.run([cli, "-m", "bsgs", "-f", "x", "-k", "5000", "-b", "66"], capture_output=True, text=True)
     assert r.returncode == 1 and "too large" in r.stderr
-    r = subprocess.run([cli, "-m", "address", "-f", "x", "-e"], capture_output=True, text=True)
+    r = subprocess.run([cli, "-m", "address", "-f", "x", "-S"], capture_output=True, text=True)
     assert r.returncode == 1
     r = subprocess.run([cli, "-m", "bsgs", "-f", "x", "-B", "ggsb"], capture_output=True, text=True)
     assert r.returncode == 1 and "ggsb" in r.stderr
+    # keyhunt.cpp:1185-1193 test the -B index against MODE_BSGS: -B both + -e / -I fail in any mode
+    r = subprocess.run([cli, "-m", "address", "-f", "x", "-B", "both", "-e"], capture_output=True, text=True)
+    assert r.returncode == 1 and "Endomorphism doesn't work with BSGS" in r.stderr
+    r = subprocess.run([cli, "-m", "address", "-f", "x", "-B", "both", "-I", "3"], capture_output=True, text=True)
+    assert r.returncode == 1 and "Stride doesn't work with BSGS" in r.stderr

@@ -94,8 +94,8 @@ def _read_rows(oracle, fn, mode):
     for line in open(os.path.join(DATA, fn)):
         s = line.strip()
         if mode == "xpoint":
-            if len(s) == 66:
-                rows.append(bytes.fromhex(s[2:])[:20])
+            if len(s) in (64, 66):
+                rows.append(bytes.fromhex(s[-64:])[:20])
             continue
         if len(s) == 40:
             rows.append(bytes.fromhex(s))
@@ -106,14 +106,20 @@ def _read_rows(oracle, fn, mode):
     return rows
 
 
-@pytest.mark.parametrize("name,fn,mode,search", [
-    ("rmd160_1to32_compress_2p20", "1to32.rmd", 0, 0),
-    ("xpoint_1to63_65_2p20", "1to63_65.txt", 1, 2),
+@pytest.mark.parametrize("name,fn,mode,search,endo", [
+    ("rmd160_1to32_compress_2p20", "1to32.rmd", 0, 0, False),
+    ("xpoint_1to63_65_2p20", "1to63_65.txt", 1, 2, False),
+    ("rmd160_1to32_compress_2p20_endo", "1to32.rmd", 0, 0, True),
+    ("xpoint_1to63_65_2p20_endo", "1to63_65.txt", 1, 2, True),
+    ("address_endo_targets", "endo_addr.txt", 0, 2, True),
+    ("address_endo_targets_no_e", "endo_addr.txt", 0, 2, False),
+    ("xpoint_endo_targets", "endo_x.txt", 1, 2, True),
 ])
-def test_oracle_scan_vs_reference_cli(oracle, name, fn, mode, search):
-    """Keys 1..2^20 (one 2^20 chunk): the oracle's hit list equals the reference CLI's."""
+def test_oracle_scan_vs_reference_cli(oracle, name, fn, mode, search, endo):
+    """Keys 1..2^20 (one 2^20 chunk): the oracle's hit list equals the reference CLI's, with and
+    without -e (endo_*.txt hold lambda-multiples of small keys, tests/golden/make_endo_targets.py)."""
     rows = _read_rows(oracle, fn, "xpoint" if mode == 1 else "addr")
-    hits = oracle.scan_chunk(mode, search, 1, 1 << 20, rows)
+    hits = oracle.scan_chunk(mode, search, 1, 1 << 20, rows, endo=endo)
     assert [f"{k:x}" for k in sorted(k for k, _, _ in hits)] == [x["key"] for x in E2E[name]["hits"]]
 
 
