@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
-"""Generate keyhunt_amd/csrc/kh_field_asm.h: secp256k1 field multiplication and squaring for gfx950
-as single inline-asm statements (development tool; the generated header is committed).
+"""Generate tools/kh_field_asm.h: secp256k1 field multiplication and squaring for gfx950 as single
+inline-asm statements (development study; the engine keeps hipcc's code).
 
 Why: gfx950 needs 2 wait states between a VALU instruction that writes an SGPR carry mask and a
 VALU instruction that reads it (v_add_co -> v_addc).  hipcc pads every such pair in a carry chain
@@ -20,8 +20,10 @@ Arithmetic (same value as kh_math.h's portable fe_mul / fe_sqr, secp256k1/IntMod
   The statement returns a flag word = max(and(r2..r7), u3): it is 0xFFFFFFFF only if limb 3 could
   have carried on (u3 = ~0) or the result may be >= p (r2..r7 all ones); the caller then recomputes
   with the portable code (probability ~2^-32 per product).
-Scratch VGPRs are fixed registers named in the clobber list, so pairs and their halves can both be
-addressed in the text.
+The two 64-bit accumulator pairs per product are fixed VGPRs named in the clobber list, so pairs and
+their halves can both be addressed in the text; everything else is compiler-allocated operands.
+Result on the MI355X: 16% fewer cycles per multiplication in isolation (tools/ubench_field4.hip),
+no gain inside the BSGS walk (opaque to hipcc's scheduler; the paired form spills).
 """
 import os
 import sys
@@ -36,9 +38,11 @@ class Stream:
         self.tag = tag
         self.ins = []          # (text, sgpr_writes, sgpr_reads)
         self.vbase = vbase     # first fixed scratch VGPR: T[0..15] = vbase..vbase+15, A, B pairs after
-        self.T = [f"v{vbase + i}" for i in range(16)]
-        self.A = (f"v{vbase + 16}", f"v{vbase + 17}")
-        self.B = (f"v{vbase + 18}", f"v{vbase + 19}")
+        # the 512-bit intermediate lives in compiler-allocated operands; only the two accumulator
+        # pairs are fixed registers (their halves must be addressable)
+        self.T = [f"%[{tag}t{i}]" for i in range(16)]
+        self.A = (f"v{vbase}", f"v{vbase + 1}")
+        self.B = (f"v{vbase + 2}", f"v{vbase + 3}")
         self.c = [f"%[{tag}c{i}]" for i in range(3)]
         self.cn = 0
 
@@ -236,7 +240,7 @@ def fe_ops(name):
 def gen_function(fname, kind, nstreams, part="all"):
     """kind: 'mul' or 'sqr'.  part (timing experiments only): 'all', 'prod' (no reduction: r = t_lo),
     'red' (reduction of t = a || b)."""
-    vbases = [108, 88][:nstreams]
+    vbases = [124, 120][:nstreams]
     streams = []
     for s in range(nstreams):
         st = Stream(f"s{s}", vbases[s])
@@ -261,12 +265,13 @@ def gen_function(fname, kind, nstreams, part="all"):
     body = schedule(streams)
     clob = []
     for vb in vbases:
-        clob += [f'"v{vb + i}"' for i in range(20)]
+        clob += [f'"v{vb + i}"' for i in range(4)]
     outs, ins = [], ['[k977] "s"(977u)']
     for s in range(nstreams):
         outs += [f'[r{s}_{i}] "=&v"(r{s}.d[{i}])' for i in range(8)]
         outs.append(f'[f{s}] "=&v"(f{s})')
         outs += [f'[s{s}c{i}] "=&s"(c{s}_{i})' for i in range(3)]
+        outs += [f'[s{s}t{i}] "=&v"(t{s}[{i}])' for i in range(16)]
         ins += [f'[a{s}_{i}] "v"(a{s}.d[{i}])' for i in range(8)]
         if kind == "mul":
             ins += [f'[b{s}_{i}] "v"(b{s}.d[{i}])' for i in range(8)]
@@ -283,9 +288,10 @@ def gen_function(fname, kind, nstreams, part="all"):
     lines.append(f"__device__ __forceinline__ uint32_t {fname}({', '.join(args)}) {{")
     fl = ", ".join(f"f{s}" for s in range(nstreams))
     lines.append(f"  uint32_t {fl};")
+    lines.append("#if defined(__HIP_DEVICE_COMPILE__)")
     for s in range(nstreams):
         lines.append(f"  uint64_t c{s}_0, c{s}_1, c{s}_2;")
-    lines.append("#if defined(__HIP_DEVICE_COMPILE__)")
+        lines.append(f"  uint32_t t{s}[16];")
     lines.append("  asm volatile(")
     for t in body:
         lines.append(f'      "{t}\\n"')
@@ -294,6 +300,7 @@ def gen_function(fname, kind, nstreams, part="all"):
     lines.append(f"      : {', '.join(clob)});")
     lines.append("#else")
     lines.append("  " + " ".join(f"f{s} = 0xFFFFFFFFu;" for s in range(nstreams)) + "  // host pass: never called")
+    lines.append("  " + " ".join(f"(void)r{s}; (void)a{s};" + (f" (void)b{s};" if kind == "mul" else "") for s in range(nstreams)))
     lines.append("#endif")
     if nstreams == 1:
         lines.append("  return f0;")
@@ -305,7 +312,7 @@ def gen_function(fname, kind, nstreams, part="all"):
 
 def main():
     out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(
-        os.path.dirname(os.path.abspath(__file__)), "..", "keyhunt_amd", "csrc", "kh_field_asm.h")
+        os.path.dirname(os.path.abspath(__file__)), "kh_field_asm.h")
     parts = ["// GENERATED by tools/gen_field_asm.py -- do not edit.  See that file for the algorithm.",
              "// Device-only: secp256k1 field mul/sqr as single gfx950 inline-asm statements.",
              "#pragma once", "#if defined(__HIPCC__)", "namespace kh {"]

@@ -8,7 +8,7 @@
 #include <stdio.h>
 #include <vector>
 #include "../keyhunt_amd/csrc/kh_math.h"
-#include "../keyhunt_amd/csrc/kh_field_asm.h"
+#include "kh_field_asm.h"
 
 using namespace kh;
 

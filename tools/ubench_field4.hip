@@ -6,8 +6,9 @@
 #include <stdio.h>
 #include <vector>
 #include "../keyhunt_amd/csrc/kh_math.h"
-#include "kh_field_asm_x.h"
+#include "kh_field_asm_x.h"  // includes the experiment functions too
 using namespace kh;
+__device__ __noinline__ void fe_mul_slow(fe &r, const fe &a, const fe &b) { fe_mul(r, a, b); }
 template <int V>
 __global__ __launch_bounds__(256, 4) void k_bench(const uint32_t *in, uint32_t *out, int iters) {
   uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
@@ -22,6 +23,20 @@ __global__ __launch_bounds__(256, 4) void k_bench(const uint32_t *in, uint32_t *
     if (V == 3) { acc += fe_red_asm(r, a, b); acc += fe_red_asm(s, c, d); }
     if (V == 4) { acc += fe_sqr_asm(r, a); acc += fe_sqr_asm(s, c); }
     if (V == 5) { acc += fe_mul2_asm(r, a, b, s, c, d); }
+    if (V == 6) {  // with the portable fallback on a set flag, as the walk would use it
+      fe t, u;
+      if (fe_mul_asm(t, a, b) == 0xFFFFFFFFu) fe_mul(t, a, b);
+      if (fe_mul_asm(u, c, d) == 0xFFFFFFFFu) fe_mul(u, c, d);
+      r = t;
+      s = u;
+    }
+    if (V == 7) {  // fallback through a non-inlined call
+      fe t, u;
+      if (fe_mul_asm(t, a, b) == 0xFFFFFFFFu) fe_mul_slow(t, a, b);
+      if (fe_mul_asm(u, c, d) == 0xFFFFFFFFu) fe_mul_slow(u, c, d);
+      r = t;
+      s = u;
+    }
     b = a; d = c; a = r; c = s;
   }
   for (int i = 0; i < 8; i++) { out[g * 16 + i] = a.d[i] + acc; out[g * 16 + 8 + i] = c.d[i]; }
@@ -36,13 +51,13 @@ int main() {
   (void)hipMalloc(&dout, (size_t)lanes * 64);
   (void)hipMemcpy(din, h.data(), h.size() * 4, hipMemcpyHostToDevice);
   hipEvent_t e0, e1; (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
-  const char *names[] = {"hipcc fe_mul", "asm mul", "asm product only", "asm reduce only", "asm sqr", "asm mul2"};
-  for (int v = 0; v < 6; v++) {
+  const char *names[] = {"hipcc fe_mul", "asm mul", "asm product only", "asm reduce only", "asm sqr", "asm mul2", "asm mul + fallback", "asm mul + call"};
+  for (int v = 0; v < 8; v++) {
     for (int rep = 0; rep < 2; rep++) {
       (void)hipEventRecord(e0);
       switch (v) {
 #define L(n) case n: hipLaunchKernelGGL(k_bench<n>, dim3(lanes / 256), dim3(256), 0, 0, din, dout, iters); break;
-        L(0) L(1) L(2) L(3) L(4) L(5)
+        L(0) L(1) L(2) L(3) L(4) L(5) L(6) L(7)
       }
       (void)hipEventRecord(e1); (void)hipEventSynchronize(e1);
       float ms; (void)hipEventElapsedTime(&ms, e0, e1);
