@@ -12,7 +12,7 @@
  *   kh_bsgs_setup      <- BSGS parameter block                            keyhunt.cpp:1454-1842
  *   kh_bsgs_build      <- thread_bPload / thread_bPload_2blooms + bsgs_sort keyhunt.cpp:5284-5644, 2466-2503
  *   kh_bsgs_scan       <- thread_process_bsgs (sequential), bases of 2N   keyhunt.cpp:4549-4888
- *                         with bsgs_secondcheck / bsgs_thirdcheck          keyhunt.cpp:5151-5248
+ *                         with bsgs_secondcheck (GPU) / bsgs_thirdcheck    keyhunt.cpp:5151-5248
  *
  * Conventions: plain C types only; 256-bit scalars and coordinates are 32-byte BIG-endian
  * (Int::Get32Bytes); every call returns 0 on success or a negative KH_E* code (never exits);
@@ -52,9 +52,10 @@ extern "C" {
 
 /* layer-1 (bloom_bP) layouts for kh_bsgs_set_layer1 */
 #define KH_LAYER1_REFERENCE 0  /* the reference's bit layout (bloom/bloom.cpp): bit-identical tables */
-#define KH_LAYER1_BLOCKED 1    /* default: all of an item's bits in one 64-B line (same XXH64 and k, 1.5x the
-                                  bits per shard, FP 3.9e-7 vs 1e-6); one HBM line per probe.  Layers 2/3
-                                  stay in the reference layout, so refinement and found keys are unchanged */
+#define KH_LAYER1_BLOCKED 1    /* default: split-block filter, an item's 16 bits in one 16-byte block chosen by
+                                  the x-coordinate's own words (3x the bits per shard, FP 5.6e-7 vs 1e-6); one
+                                  16-B load per probe.  Layers 2/3 stay in the reference layout, so refinement
+                                  and found keys are unchanged */
 
 /* hit kinds */
 #define KH_KIND_02 0       /* hash160(02||X) matched */
@@ -134,6 +135,10 @@ int kh_bsgs_scan_list(kh_ctx *ctx, const uint8_t *bases, uint64_t n_bases, kh_bs
 int kh_bsgs_reset_found(kh_ctx *ctx);
 /* first-level bloom candidates seen so far (for stats / parity tests) */
 int kh_bsgs_candidates(kh_ctx *ctx, uint64_t *count);
+/* first-level candidates and layer-2 hits of their second checks (bsgs_secondcheck's bloom_check
+ * positives, keyhunt.cpp:5177-5180) since kh_bsgs_setup.  The second check runs on the GPU
+ * (k_refine) unless the environment sets KH_REFINE=host at kh_open; both give the same counts. */
+int kh_bsgs_refine_stats(kh_ctx *ctx, uint64_t *first_level, uint64_t *second_level);
 
 /* ---- measurement -------------------------------------------------------------------------- */
 /* Accumulated device time of walk launches of one kind since the last reset, measured with
@@ -156,6 +161,11 @@ int kh_field_ops(kh_ctx *ctx, const uint8_t *a, const uint8_t *b, uint32_t n, ui
 int kh_bloom_check(kh_ctx *ctx, uint32_t layer, const uint8_t *items, uint32_t n, uint32_t len, uint8_t *out);
 /* copy a bloom back: layer 0 = target bloom, 1..3 = BSGS layers (256 shards concatenated, unpadded) */
 int kh_get_bloom(kh_ctx *ctx, uint32_t layer, uint8_t *buf, uint64_t cap, uint64_t *bytes);
+/* bsgs_secondcheck's layer-2 hit mask for n base keys (32-byte big-endian each) against target
+ * `target`, from the GPU kernel (k_refine) and from the host code: bit i set when the point
+ * Q - base_key*G + AMP2[i] passes bloom_bPx2nd (keyhunt.cpp:5151-5184) */
+int kh_bsgs_second_masks(kh_ctx *ctx, uint32_t target, const uint8_t *base_keys, uint32_t n, uint32_t *gpu_mask,
+                         uint32_t *host_mask);
 /* sorted bP table as the reference's 16-byte bsgs_xvalue rows {value[6], pad[2], index u64 LE} */
 int kh_get_bsgs_table(kh_ctx *ctx, uint8_t *buf, uint64_t cap_rows, uint64_t *rows);
 

@@ -288,6 +288,9 @@ struct timing {
 struct kh_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  // BSGS rounds: the second check and the candidate copies of round r run on this high-priority
+  // stream, so they start alongside round r+1's walk instead of in front of it
+  hipStream_t side = nullptr;
   std::string err;
   comb_table comb;
   uint32_t *d_comb = nullptr;
@@ -328,6 +331,13 @@ struct kh_ctx {
   std::vector<ge> targets;
   std::vector<uint8_t> found;
   uint64_t candidates = 0;
+  uint64_t second_hits = 0;          // layer-2 positives of the second check (all candidates)
+  // second check on the GPU (k_refine) unless KH_REFINE=host
+  bool refine_host = false;
+  uint32_t *d_amp2 = nullptr;        // 32 x {x[8], y[8]}
+  uint32_t *d_ref_start = nullptr;   // 8 limbs
+  uint32_t *d_ref_list = nullptr;    // list mode bases
+  uint64_t ref_list_cap = 0;
 
   // timing
   hipEvent_t ev_a = nullptr, ev_b = nullptr;
@@ -369,6 +379,9 @@ kh_ctx::~kh_ctx() {
   (void)hipFree(d_hits);
   (void)hipFree(d_tbloom);
   for (int i = 0; i < 3; i++) (void)hipFree(d_bl[i]);
+  (void)hipFree(d_amp2);
+  (void)hipFree(d_ref_start);
+  (void)hipFree(d_ref_list);
   for (int i = 0; i < 2; i++) {
     (void)hipFree(d_cnt2[i]);
     (void)hipFree(d_hits2[i]);
@@ -380,6 +393,10 @@ kh_ctx::~kh_ctx() {
   }
   if (ev_a) (void)hipEventDestroy(ev_a);
   if (ev_b) (void)hipEventDestroy(ev_b);
+  if (side) {
+    (void)hipStreamSynchronize(side);
+    (void)hipStreamDestroy(side);
+  }
   if (stream) (void)hipStreamDestroy(stream);
 }
 
@@ -575,6 +592,11 @@ int kh_open(int device, kh_ctx **out) {
   };
   if (hipSetDevice(device) != hipSuccess) return fail(KH_E_HIP);
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return fail(KH_E_HIP);
+  {
+    int lo = 0, hi = 0;
+    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) lo = hi = 0;
+    if (hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, hi) != hipSuccess) return fail(KH_E_HIP);
+  }
   if (hipEventCreate(&c->ev_a) != hipSuccess || hipEventCreate(&c->ev_b) != hipSuccess) return fail(KH_E_HIP);
   c->comb.build();
   std::vector<uint32_t> h((size_t)32 * 256 * 16, 0);
@@ -587,6 +609,8 @@ int kh_open(int device, kh_ctx **out) {
   if (hipMemcpy(c->d_comb, h.data(), h.size() * 4, hipMemcpyHostToDevice) != hipSuccess) return fail(KH_E_HIP);
   // test hook: a small initial BSGS candidate buffer exercises the grow-and-redo path
   if (const char *e = getenv("KH_CAND_CAP")) c->cand_cap = std::max<uint32_t>(1, (uint32_t)strtoul(e, nullptr, 0));
+  // A/B and parity hook: KH_REFINE=host runs the second check on host threads instead of k_refine
+  if (const char *e = getenv("KH_REFINE")) c->refine_host = strcmp(e, "host") == 0;
   if (hipMalloc(&c->d_hit_count, 4) != hipSuccess) return fail(KH_E_NOMEM);
   if (hipMalloc(&c->d_hits, (size_t)c->hit_cap * sizeof(kh_dev_hit)) != hipSuccess) return fail(KH_E_NOMEM);
   *out = c;
@@ -609,6 +633,7 @@ int kh_synchronize(kh_ctx *ctx) {
   if (!ctx) return KH_E_ARG;
   (void)hipSetDevice(ctx->device);
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  HIPCHK(ctx, hipStreamSynchronize(ctx->side));
   return KH_OK;
 }
 
@@ -842,9 +867,21 @@ int kh_bsgs_setup(kh_ctx *ctx, uint64_t n, uint64_t k, kh_bsgs_info *info) {
     fe_neg(a.y, a.y);
     ctx->amp3[i] = a;
   }
+  {
+    std::vector<uint32_t> w(32 * 16);
+    for (int i = 0; i < 32; i++) {
+      memcpy(&w[i * 16], ctx->amp2[i].x.d, 32);
+      memcpy(&w[i * 16 + 8], ctx->amp2[i].y.d, 32);
+    }
+    if (!ctx->d_amp2) HIPCHK(ctx, hipMalloc(&ctx->d_amp2, w.size() * 4));
+    if (!ctx->d_ref_start) HIPCHK(ctx, hipMalloc(&ctx->d_ref_start, 32));
+    HIPCHK(ctx, hipMemcpy(ctx->d_amp2, w.data(), w.size() * 4, hipMemcpyHostToDevice));
+  }
+  ctx->second_hits = 0;
   ctx->bsgs_ready = true;
   ctx->bsgs_built = false;
   ctx->candidates = 0;
+  ctx->second_hits = 0;
   if (info) *info = I;
   return KH_OK;
 }
@@ -945,6 +982,13 @@ int kh_bsgs_reset_found(kh_ctx *ctx) {
   return KH_OK;
 }
 
+int kh_bsgs_refine_stats(kh_ctx *ctx, uint64_t *first_level, uint64_t *second_level) {
+  if (!ctx || !first_level || !second_level) return KH_E_ARG;
+  *first_level = ctx->candidates;
+  *second_level = ctx->second_hits;
+  return KH_OK;
+}
+
 int kh_bsgs_candidates(kh_ctx *ctx, uint64_t *count) {
   if (!ctx || !count) return KH_E_ARG;
   *count = ctx->candidates;
@@ -1028,23 +1072,31 @@ bool third_check(const kh_ctx *c, const u256 &base_key, uint32_t a, const ge &Q,
   return false;
 }
 
-// bsgs_secondcheck (keyhunt.cpp:5151-5184)
-bool second_check(const kh_ctx *c, const u256 &base, uint64_t a, const ge &Q, u256 &key) {
-  const kh_bsgs_info &I = c->info;
-  u256 base_key = sc_add(base, sc_reduce(u256_from_u128((u128)a * 2 * I.m)));
+// bsgs_secondcheck (keyhunt.cpp:5151-5184) in two halves.  second_mask: the layer-2 hits of the
+// 32 points S + AMP2[i] (S = Q - base_key*G) as a bit mask -- the host twin of k_refine;
+// second_finish: the reference's loop over those hits, calling bsgs_thirdcheck in order.
+u256 second_base_key(const kh_ctx *c, const u256 &base, uint64_t a) {
+  return sc_add(base, sc_reduce(u256_from_u128((u128)a * 2 * c->info.m)));
+}
+uint32_t second_mask(const kh_ctx *c, const u256 &base_key, const ge &Q) {
   ge bp;
-  if (!c->comb.mult(bp, base_key)) return false;
+  if (!c->comb.mult(bp, base_key)) return 0;
   fe_neg(bp.y, bp.y);
   ge S;
   ge_add(S, Q, bp);
   fe xs[32];
   add32_x(S, c->amp2, xs);
+  uint32_t mask = 0;
   for (int i = 0; i < 32; i++) {
     uint8_t xr[32];
     fe_to_be(xr, xs[i]);
-    if (host_bloom_check(c->h_bl[1].data() + (size_t)xr[0] * c->bd[1].stride, c->bd[1], xr, 32))
-      if (third_check(c, base_key, (uint32_t)i, Q, key)) return true;
+    if (host_bloom_check(c->h_bl[1].data() + (size_t)xr[0] * c->bd[1].stride, c->bd[1], xr, 32)) mask |= 1u << i;
   }
+  return mask;
+}
+bool second_finish(const kh_ctx *c, const u256 &base_key, uint32_t mask, const ge &Q, u256 &key) {
+  for (int i = 0; i < 32; i++)
+    if (((mask >> i) & 1) && third_check(c, base_key, (uint32_t)i, Q, key)) return true;
   return false;
 }
 
@@ -1153,6 +1205,25 @@ static int bsgs_scan_impl(kh_ctx *ctx, const u256 &st, const std::vector<u256> *
     gpr = std::max<uint64_t>(1, KH_BSGS_ROUND_POINTS / ((uint64_t)jc.L * 2 * H));
     gpr = std::min<uint64_t>(gpr, jc.gpl);
   }
+  // second check on the GPU: the kernel derives base_key from the candidate's giant index
+  const bool gpu_refine = !ctx->refine_host;
+  if (gpu_refine) {
+    uint32_t sl[8];
+    u256_to_limbs(sl, st);
+    HIPCHK(ctx, hipMemcpyAsync(ctx->d_ref_start, sl, 32, hipMemcpyHostToDevice, ctx->stream));
+    if (list) {
+      if (n_bases > ctx->ref_list_cap) {
+        (void)hipFree(ctx->d_ref_list);
+        ctx->d_ref_list = nullptr;
+        ctx->ref_list_cap = 0;
+        HIPCHK(ctx, hipMalloc(&ctx->d_ref_list, (size_t)n_bases * 32));
+        ctx->ref_list_cap = n_bases;
+      }
+      std::vector<uint32_t> lw((size_t)n_bases * 8);
+      for (uint64_t b = 0; b < n_bases; b++) u256_to_limbs(&lw[b * 8], (*list)[b]);
+      HIPCHK(ctx, hipMemcpy(ctx->d_ref_list, lw.data(), lw.size() * 4, hipMemcpyHostToDevice));
+    }
+  }
   auto centre_scalar = [&](uint64_t t0) {  // -(key of the centre of the group starting at t0)
     uint64_t b = t0 / A_pts, a0 = t0 % A_pts;
     u256 kb = sc_add(base_of(b), sc_reduce(u256_from_u128((u128)I.m + (u128)2 * I.m * (a0 + H))));
@@ -1247,11 +1318,32 @@ static int bsgs_scan_impl(kh_ctx *ctx, const u256 &st, const std::vector<u256> *
         R.points += (uint64_t)jg.L * Aw.groups * 2 * H;
       }
       HIPCHK(ctx, hipEventRecord(ctx->ev_round[slot][2], ctx->stream));
-      HIPCHK(ctx, hipMemcpyAsync(ctx->h_cnt2[slot], ctx->d_cnt2[slot], 4, hipMemcpyDeviceToHost, ctx->stream));
+      HIPCHK(ctx, hipStreamWaitEvent(ctx->side, ctx->ev_round[slot][2], 0));
+      if (gpu_refine) {  // second check of this round's candidates, in place (aux = layer-2 mask)
+        refine_args Ra;
+        memset(&Ra, 0, sizeof Ra);
+        Ra.cands = ctx->d_hits2[slot];
+        Ra.count = ctx->d_cnt2[slot];
+        Ra.cap = ctx->cand_cap;
+        Ra.list_mode = list ? 1 : 0;
+        Ra.t_round = R.t_round;
+        Ra.a_pts = A_pts;
+        Ra.two_n = 2 * I.n;
+        Ra.two_m = 2 * I.m;
+        Ra.start = ctx->d_ref_start;
+        Ra.list = ctx->d_ref_list;
+        Ra.comb = ctx->d_comb;
+        Ra.q = dq;
+        Ra.amp2 = ctx->d_amp2;
+        Ra.bloom2 = ctx->d_bl[1];
+        Ra.bd2 = ctx->bd[1];
+        HIPCHK(ctx, launch_refine(Ra, ctx->side));
+      }
+      HIPCHK(ctx, hipMemcpyAsync(ctx->h_cnt2[slot], ctx->d_cnt2[slot], 4, hipMemcpyDeviceToHost, ctx->side));
       HIPCHK(ctx, hipMemcpyAsync(ctx->h_hits2[slot], ctx->d_hits2[slot],
                                  (size_t)std::min(ctx->cand_cap, KH_CAND_EAGER) * sizeof(kh_dev_hit),
-                                 hipMemcpyDeviceToHost, ctx->stream));
-      HIPCHK(ctx, hipEventRecord(ctx->ev_round[slot][3], ctx->stream));
+                                 hipMemcpyDeviceToHost, ctx->side));
+      HIPCHK(ctx, hipEventRecord(ctx->ev_round[slot][3], ctx->side));
       g0 += rg;
       return KH_OK;
     };
@@ -1275,6 +1367,7 @@ static int bsgs_scan_impl(kh_ctx *ctx, const u256 &st, const std::vector<u256> *
       uint32_t cnt = *ctx->h_cnt2[slot];
       if (cnt > ctx->cand_cap) {
         HIPCHK(ctx, hipStreamSynchronize(ctx->stream));  // drain the speculative next round
+        HIPCHK(ctx, hipStreamSynchronize(ctx->side));
         int rr = grow_candidates(ctx, (uint64_t)cnt * 2);
         return rr ? rr : 1;
       }
@@ -1286,23 +1379,37 @@ static int bsgs_scan_impl(kh_ctx *ctx, const u256 &st, const std::vector<u256> *
       ctx->candidates += cnt;
       std::vector<uint8_t> ok(dh.size(), 0);
       std::vector<u256> keys(dh.size());
-      std::atomic<size_t> next{0};
-      auto work = [&]() {
-        for (;;) {
-          size_t i = next++;
-          if (i >= dh.size()) break;
-          uint64_t t = R.t_round + dh[i].idx;
-          uint64_t b = t / A_pts, a = t % A_pts;
-          ok[i] = second_check(ctx, base_of(b), a, Q, keys[i]) ? 1 : 0;
-        }
+      auto key_of = [&](size_t i) {
+        uint64_t t = R.t_round + dh[i].idx;
+        return second_base_key(ctx, base_of(t / A_pts), t % A_pts);
       };
-      unsigned nt = std::min<unsigned>(ctx->refine_threads, (unsigned)dh.size());
-      if (nt <= 1) {
-        work();
-      } else {
-        std::vector<std::thread> th;
-        for (unsigned k = 0; k < nt; k++) th.emplace_back(work);
-        for (auto &x : th) x.join();
+      if (!gpu_refine) {  // layer-2 masks on host threads (KH_REFINE=host)
+        std::atomic<size_t> next{0};
+        auto work = [&]() {
+          for (;;) {
+            size_t i = next++;
+            if (i >= dh.size()) break;
+            dh[i].aux = second_mask(ctx, key_of(i), Q);
+          }
+        };
+        unsigned nt = std::min<unsigned>(ctx->refine_threads, (unsigned)dh.size());
+        if (nt <= 1) {
+          work();
+        } else {
+          std::vector<std::thread> th;
+          for (unsigned k = 0; k < nt; k++) th.emplace_back(work);
+          for (auto &x : th) x.join();
+        }
+      }
+      // third checks for the (rare) layer-2 hits, in giant-step order; stop at the first key
+      for (size_t i = 0; i < dh.size(); i++) {
+        if (!dh[i].aux) continue;
+        ctx->second_hits += (uint64_t)__builtin_popcount(dh[i].aux);
+        const u256 bk = key_of(i);
+        if (second_finish(ctx, bk, dh[i].aux, Q, keys[i])) {
+          ok[i] = 1;
+          break;
+        }
       }
       for (size_t i = 0; i < dh.size(); i++)
         if (ok[i]) {  // the first candidate (in giant-step order) that refines to a key
@@ -1345,7 +1452,10 @@ static int bsgs_scan_impl(kh_ctx *ctx, const u256 &st, const std::vector<u256> *
       }
       pending = nxt;
     }
-    if (pending >= 0 && done) (void)hipStreamSynchronize(ctx->stream);  // drain the speculative round
+    if (pending >= 0 && done) {  // drain the speculative round
+      (void)hipStreamSynchronize(ctx->stream);
+      (void)hipStreamSynchronize(ctx->side);
+    }
     (void)hipFree(dq);
   }
   *n_found = nf;
@@ -1369,6 +1479,74 @@ int kh_bsgs_scan_list(kh_ctx *ctx, const uint8_t *bases, uint64_t n_bases, kh_bs
 // ---------------------------------------------------------------------------------------------
 // measurement
 // ---------------------------------------------------------------------------------------------
+int kh_bsgs_second_masks(kh_ctx *ctx, uint32_t target, const uint8_t *base_keys, uint32_t n, uint32_t *gpu_mask,
+                         uint32_t *host_mask) {
+  if (!ctx || !base_keys || !gpu_mask || !host_mask) return KH_E_ARG;
+  if (!ctx->bsgs_built || target >= ctx->targets.size()) return KH_E_STATE;
+  (void)hipSetDevice(ctx->device);
+  if (n == 0) return KH_OK;
+  const ge &Q = ctx->targets[target];
+  std::vector<uint32_t> lw((size_t)n * 8);
+  std::vector<kh_dev_hit> c(n);
+  for (uint32_t j = 0; j < n; j++) {
+    u256 k = sc_reduce(u256_from_be(base_keys + (size_t)j * 32));
+    u256_to_limbs(&lw[(size_t)j * 8], k);
+    c[j].idx = j;  // list mode with one point per base: t = j -> base j, a = 0
+    c[j].kind = 4;
+    c[j].aux = 0xFFFFFFFFu;
+    host_mask[j] = second_mask(ctx, k, Q);
+  }
+  uint32_t Qw[16];
+  memcpy(Qw, Q.x.d, 32);
+  memcpy(Qw + 8, Q.y.d, 32);
+  uint32_t *d_list = nullptr, *d_q = nullptr, *d_cnt = nullptr;
+  kh_dev_hit *d_c = nullptr;
+  int rc = KH_OK;
+  auto chk = [&](hipError_t e, const char *what) {
+    if (e != hipSuccess && rc == KH_OK) {
+      ctx->err = std::string(what) + ": " + hipGetErrorString(e);
+      rc = KH_E_HIP;
+    }
+  };
+  chk(hipMalloc(&d_list, lw.size() * 4), "hipMalloc");
+  chk(hipMalloc(&d_q, 64), "hipMalloc");
+  chk(hipMalloc(&d_cnt, 4), "hipMalloc");
+  chk(hipMalloc(&d_c, (size_t)n * sizeof(kh_dev_hit)), "hipMalloc");
+  if (rc == KH_OK) {
+    chk(hipMemcpy(d_list, lw.data(), lw.size() * 4, hipMemcpyHostToDevice), "hipMemcpy");
+    chk(hipMemcpy(d_q, Qw, 64, hipMemcpyHostToDevice), "hipMemcpy");
+    chk(hipMemcpy(d_cnt, &n, 4, hipMemcpyHostToDevice), "hipMemcpy");
+    chk(hipMemcpy(d_c, c.data(), (size_t)n * sizeof(kh_dev_hit), hipMemcpyHostToDevice), "hipMemcpy");
+  }
+  if (rc == KH_OK) {
+    refine_args Ra;
+    memset(&Ra, 0, sizeof Ra);
+    Ra.cands = d_c;
+    Ra.count = d_cnt;
+    Ra.cap = n;
+    Ra.list_mode = 1;
+    Ra.a_pts = 1;
+    Ra.two_n = 2 * ctx->info.n;
+    Ra.two_m = 2 * ctx->info.m;
+    Ra.start = ctx->d_ref_start;
+    Ra.list = d_list;
+    Ra.comb = ctx->d_comb;
+    Ra.q = d_q;
+    Ra.amp2 = ctx->d_amp2;
+    Ra.bloom2 = ctx->d_bl[1];
+    Ra.bd2 = ctx->bd[1];
+    chk(launch_refine(Ra, ctx->stream), "k_refine");
+    chk(hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
+    chk(hipMemcpy(c.data(), d_c, (size_t)n * sizeof(kh_dev_hit), hipMemcpyDeviceToHost), "hipMemcpy");
+    for (uint32_t j = 0; j < n; j++) gpu_mask[j] = c[j].aux;
+  }
+  (void)hipFree(d_list);
+  (void)hipFree(d_q);
+  (void)hipFree(d_cnt);
+  (void)hipFree(d_c);
+  return rc;
+}
+
 int kh_kernel_time(kh_ctx *ctx, uint32_t kind, uint64_t *launches, double *ms, uint64_t *points) {
   if (!ctx || kind > 4) return KH_E_ARG;
   if (launches) *launches = ctx->tm[kind].launches;

@@ -98,8 +98,31 @@ struct setup_args {
   uint32_t *cx, *cy;
 };
 
+// BSGS second check on the GPU (bsgs_secondcheck, keyhunt.cpp:5151-5184).  Per first-level
+// candidate (giant index t = t_round + idx, base b = t / a_pts, a = t % a_pts):
+// base_key = base(b) + a*2M (mod n), S = Q - base_key*G, and the 32 points S + AMP2[i] are probed
+// against layer 2 (reference layout); the candidate's aux receives the mask of layer-2 hits.
+// The host then runs bsgs_thirdcheck for the set bits only, in bit order.
+struct refine_args {
+  kh_dev_hit *cands;       // in: idx; out: aux = layer-2 mask
+  const uint32_t *count;   // candidates recorded in the round (device)
+  uint32_t cap;            // entries in cands
+  uint32_t list_mode;      // 0: base(b) = start + b*2N; 1: base(b) = list[b]
+  uint64_t t_round;        // giant index of the round's point 0
+  uint64_t a_pts;          // giant points walked per base
+  uint64_t two_n, two_m;
+  const uint32_t *start;   // 8 LE u32 limbs, < n
+  const uint32_t *list;    // list mode: bases x 8 LE u32 limbs, each < n
+  const uint32_t *comb;    // 32 x 256 x 16 words
+  const uint32_t *q;       // target {x[8], y[8]}
+  const uint32_t *amp2;    // 32 x {x[8], y[8]}: BSGS_AMP2 (keyhunt.cpp:1818-1842)
+  const uint8_t *bloom2;   // layer 2, 256 shards at bd2.stride
+  kh::bloom_desc bd2;
+};
+
 namespace kh {
 hipError_t launch_walk(int mode, const walk_args &A, hipStream_t st);
+hipError_t launch_refine(const refine_args &A, hipStream_t st);
 hipError_t launch_setup(const setup_args &A, hipStream_t st);
 hipError_t launch_test_hash160(const uint32_t *xs, const uint32_t *ys, uint32_t n, uint32_t *out, hipStream_t st);
 hipError_t launch_test_field(const uint32_t *a, const uint32_t *b, uint32_t n, uint32_t *out, hipStream_t st);

@@ -547,24 +547,31 @@ __global__ void __launch_bounds__(256, walk_lb<MODE>()) k_walk(walk_args A) {
 // the doubling or inverse case (scalars are < n).  One Fermat inversion per lane to go affine,
 // one more when adding Q (the BSGS target).
 // ------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_setup(setup_args A) {
-  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= A.L) return;
-  const uint32_t *s = A.scalars + (size_t)g * 8;  // 8 LE u32 limbs
+// s*G for a scalar s != 0 given as 8 LE u32 limbs
+__device__ __forceinline__ void comb_mult(ge &r, const uint32_t s[8], const uint32_t *__restrict__ comb) {
   gej acc;
   acc.inf = true;
   for (int j = 0; j < 32; j++) {
     uint32_t v = (s[j >> 2] >> ((j & 3) * 8)) & 0xFFu;
     if (v) {
       ge q;
-      const uint32_t *c = A.comb + ((size_t)j * 256 + v) * 16;
+      const uint32_t *c = comb + ((size_t)j * 256 + v) * 16;
       load_fe(q.x, c);
       load_fe(q.y, c + 8);
       gej_add_ge(acc, q);
     }
   }
-  ge r;
   gej_to_ge(r, acc);
+}
+
+__global__ void __launch_bounds__(256) k_setup(setup_args A) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= A.L) return;
+  uint32_t s[8];  // 8 LE u32 limbs
+#pragma unroll
+  for (int i = 0; i < 8; i++) s[i] = A.scalars[(size_t)g * 8 + i];
+  ge r;
+  comb_mult(r, s, A.comb);
   if (A.has_q) {
     ge q;
     load_fe(q.x, A.q);
@@ -573,6 +580,115 @@ __global__ void __launch_bounds__(256) k_setup(setup_args A) {
   }
   store_soa(A.cx, A.L, g, r.x);
   store_soa(A.cy, A.L, g, r.y);
+}
+
+// ------------------------------------------------------------------------------------------
+// BSGS second check (bsgs_secondcheck, keyhunt.cpp:5151-5184), one candidate per lane.
+// ------------------------------------------------------------------------------------------
+namespace {
+// secp256k1 group order n, LE u32 limbs
+__device__ __forceinline__ uint32_t order_limb(int i) {
+  const uint32_t N[8] = {0xD0364141u, 0xBFD25E8Cu, 0xAF48A03Bu, 0xBAAEDCE6u,
+                         0xFFFFFFFEu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+  return N[i];
+}
+// r = (a + v) mod n for a < n and v = v0 + v1*2^64 + v2*2^128 < n (v2 <= 1)
+__device__ void sc_add_small(uint32_t r[8], const uint32_t a[8], uint64_t v0, uint64_t v1, uint32_t v2) {
+  const uint32_t v[8] = {(uint32_t)v0, (uint32_t)(v0 >> 32), (uint32_t)v1, (uint32_t)(v1 >> 32), v2, 0, 0, 0};
+  uint32_t c = 0;
+  for (int i = 0; i < 8; i++) r[i] = addc(a[i], v[i], c, c);
+  bool ge_n = c != 0;
+  if (!ge_n) {  // r >= n ?
+    ge_n = true;
+    for (int i = 7; i >= 0; i--) {
+      if (r[i] != order_limb(i)) {
+        ge_n = r[i] > order_limb(i);
+        break;
+      }
+    }
+  }
+  if (ge_n) {
+    uint32_t bo = 0;
+    for (int i = 0; i < 8; i++) r[i] = subb(r[i], order_limb(i), bo, bo);
+  }
+}
+}  // namespace
+
+__global__ void __launch_bounds__(64) k_refine(refine_args A) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t n = min(*A.count, A.cap);
+  if (j >= n) return;
+  const uint64_t t = A.t_round + A.cands[j].idx;
+  const uint64_t b = t / A.a_pts, a = t % A.a_pts;
+  uint32_t base[8];
+  uint64_t v0 = 0, v1 = 0;
+  if (A.list_mode) {
+    for (int i = 0; i < 8; i++) base[i] = A.list[b * 8 + i];
+  } else {
+    for (int i = 0; i < 8; i++) base[i] = A.start[i];
+    v0 = b * A.two_n;  // b*2N as 128 bits
+    v1 = __umul64hi(b, A.two_n);
+  }
+  const uint64_t w0 = a * A.two_m, w1 = __umul64hi(a, A.two_m);  // a*2M
+  const uint64_t s0 = v0 + w0;
+  const uint64_t c0 = s0 < v0 ? 1 : 0;
+  const uint64_t s1 = v1 + w1 + c0;
+  const uint32_t s2 = (s1 < v1 || (s1 == v1 && (w1 | c0) != 0)) ? 1u : 0u;
+  uint32_t sk[8];
+  sc_add_small(sk, base, s0, s1, s2);  // base_key (keyhunt.cpp:5159-5161)
+  uint32_t nz = 0;
+  for (int i = 0; i < 8; i++) nz |= sk[i];
+  if (!nz) {  // base_key == 0: no point (the host's comb mult refuses it the same way)
+    A.cands[j].aux = 0;
+    return;
+  }
+  ge bp, Q, S;
+  comb_mult(bp, sk, A.comb);
+  fe_neg(bp.y, bp.y);
+  load_fe(Q.x, A.q);
+  load_fe(Q.y, A.q + 8);
+  ge_add(S, Q, bp);  // BSGS_S = Q - base_key*G (AddDirect, keyhunt.cpp:5172)
+  // S + AMP2[i], i < 32: one batched inversion; a zero difference keeps inverse 0, which is what
+  // each of the reference's AddDirect calls computes for it
+  fe pre[32];
+  fe acc;
+  fe_set_u32(acc, 1);
+  for (int i = 0; i < 32; i++) {
+    fe ax, dx;
+    load_fe(ax, A.amp2 + i * 16);
+    fe_sub(dx, ax, S.x);
+    if (!fe_is_zero(dx)) fe_mul(acc, acc, dx);
+    pre[i] = acc;
+  }
+  fe inv;
+  fe_inv(inv, acc);
+  uint32_t mask = 0;
+  for (int i = 31; i >= 0; i--) {
+    fe ax, ay, dx, di, dy, s, x;
+    load_fe(ax, A.amp2 + i * 16);
+    load_fe(ay, A.amp2 + i * 16 + 8);
+    fe_sub(dx, ax, S.x);
+    if (fe_is_zero(dx)) {
+      fe_set_u32(di, 0);
+    } else {
+      if (i == 0)
+        fe_set_u32(di, 1);
+      else
+        di = pre[i - 1];
+      fe_mul(di, di, inv);
+      fe_mul(inv, inv, dx);
+    }
+    fe_sub(dy, ay, S.y);
+    fe_mul(s, dy, di);
+    fe_sqr(x, s);
+    fe_sub(x, x, S.x);
+    fe_sub(x, x, ax);
+    uint64_t in[4];
+    x_bytes_u64(x, in);
+    const uint64_t ha = xxh64_32(in, KH_BLOOM_SEED), hb = xxh64_32(in, ha);
+    if (bloom_probe(A.bloom2 + (size_t)(x.d[7] >> 24) * A.bd2.stride, A.bd2, ha, hb)) mask |= 1u << i;
+  }
+  A.cands[j].aux = mask;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -678,6 +794,11 @@ hipError_t launch_walk(int mode, const walk_args &A, hipStream_t st) {
     case KM_XPOINT | KM_ENDO: hipLaunchKernelGGL(k_walk<KM_XPOINT | KM_ENDO>, grid, block, 0, st, A); break;
     default: return hipErrorInvalidValue;
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_refine(const refine_args &A, hipStream_t st) {
+  hipLaunchKernelGGL(k_refine, dim3((A.cap + 63) / 64), dim3(64), 0, st, A);
   return hipGetLastError();
 }
 

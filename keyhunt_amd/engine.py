@@ -91,6 +91,9 @@ def lib() -> ctypes.CDLL:
                                     ctypes.POINTER(ctypes.c_uint32)]
     L.kh_bsgs_reset_found.argtypes = [P]
     L.kh_bsgs_candidates.argtypes = [P, ctypes.POINTER(ctypes.c_uint64)]
+    L.kh_bsgs_refine_stats.argtypes = [P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+    L.kh_bsgs_second_masks.argtypes = [P, ctypes.c_uint32, u8p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32),
+                                       ctypes.POINTER(ctypes.c_uint32)]
     L.kh_kernel_time.argtypes = [P, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_double),
                                  ctypes.POINTER(ctypes.c_uint64)]
     L.kh_kernel_time_reset.argtypes = [P]
@@ -217,6 +220,20 @@ class Engine:
         c = ctypes.c_uint64()
         self._chk(lib().kh_bsgs_candidates(self._ctx, ctypes.byref(c)), "kh_bsgs_candidates")
         return c.value
+
+    def bsgs_refine_stats(self) -> tuple[int, int]:
+        """(first-level candidates, layer-2 hits of their second checks) since bsgs_setup."""
+        a, b = ctypes.c_uint64(), ctypes.c_uint64()
+        self._chk(lib().kh_bsgs_refine_stats(self._ctx, ctypes.byref(a), ctypes.byref(b)), "kh_bsgs_refine_stats")
+        return a.value, b.value
+
+    def bsgs_second_masks(self, target: int, base_keys: list[int]) -> tuple[list[int], list[int]]:
+        """(GPU, host) layer-2 masks of bsgs_secondcheck for each base key (parity hook)."""
+        n = len(base_keys)
+        buf = b"".join(be32(k) for k in base_keys) or bytes(32)
+        g, h = (ctypes.c_uint32 * max(n, 1))(), (ctypes.c_uint32 * max(n, 1))()
+        self._chk(lib().kh_bsgs_second_masks(self._ctx, target, buf, n, g, h), "kh_bsgs_second_masks")
+        return list(g[:n]), list(h[:n])
 
     # -- measurement ---------------------------------------------------------------------------
     def kernel_time(self, kind: int) -> tuple[int, float, int]:

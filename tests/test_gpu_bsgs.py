@@ -56,6 +56,7 @@ def test_candidates_and_key_vs_oracle(engine, oracle, n, k):
 
 
 BSGS_CASES = [k for k in E2E if k.startswith("bsgs")]
+SECP_N = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141
 
 
 @pytest.mark.parametrize("name", BSGS_CASES)
@@ -202,3 +203,55 @@ def test_scan_list_equals_scan(engine, oracle):
     assert engine.bsgs_scan_list(bases) == [(0, key)]
     engine.bsgs_reset_found()
     assert engine.bsgs_scan_list([start + 3 * 2 * p.n, start + 9 * 2 * p.n]) == []
+
+
+def test_second_check_masks_gpu_equal_host(engine, oracle):
+    """k_refine (the GPU second check) against the host's bsgs_secondcheck twin, bit for bit: base
+    keys inside the target's 2M window (true layer-2 hits, one bit each) and random ones (FPs only)."""
+    import random
+    rnd = random.Random(1234)
+    n, k = 1 << 22, 2
+    p = oracle.bsgs_params(n, k)
+    engine.bsgs_setup(n, k)
+    engine.bsgs_build()
+    key = 0x3F00DEADBEEF0123
+    engine.bsgs_set_targets([oracle.pubkey(key)])
+    near = [key - rnd.randrange(0, 2 * p.m) for _ in range(600)]
+    far = [rnd.getrandbits(255) for _ in range(400)]
+    edge = [key, key - 2 * p.m, key - 2 * p.m + 1, 1, SECP_N - 1, 0]
+    bases = near + far + edge
+    g, h = engine.bsgs_second_masks(0, bases)
+    assert g == h
+    hits = [m for m in g[: len(near)] if m]
+    assert len(hits) >= 590   # d in [1, 2M): the AMP2 step covering d hits layer 2
+    assert all(bin(m).count("1") <= 2 for m in hits)
+    assert g[len(near) + len(far) + 5] == 0  # base key 0: no point
+
+
+@pytest.mark.parametrize("mode", ["continuous", "per_base", "list"])
+def test_gpu_refine_equals_host_refine(mode, oracle, monkeypatch):
+    """Same found keys and the same first/second-level counts whether the second check runs in
+    k_refine or on host threads (KH_REFINE=host), in the three scan modes."""
+    import keyhunt_amd as K
+    n, k = (1 << 22, 2) if mode != "per_base" else (1 << 24, 3)
+    p = oracle.bsgs_params(n, k)
+    keys = [0x1234567890ABCDE, 0x1234567890ABCDE + 7 * 2 * p.n + 99]
+    start = keys[0] - 3 * 2 * p.n - 777
+    res = []
+    for how in ("gpu", "host"):
+        if how == "host":
+            monkeypatch.setenv("KH_REFINE", "host")
+        else:
+            monkeypatch.delenv("KH_REFINE", raising=False)
+        with K.Engine(0) as e:
+            e.bsgs_setup(n, k)
+            e.bsgs_build()
+            e.bsgs_set_targets([oracle.pubkey(x) for x in keys])
+            if mode == "list":
+                found = e.bsgs_scan_list([start + b * 2 * p.n for b in range(12)])
+            else:
+                found = e.bsgs_scan(start, 12)
+            res.append((sorted(found), e.bsgs_refine_stats()))
+    assert res[0] == res[1]
+    assert sorted(res[0][0]) == [(0, keys[0]), (1, keys[1])]
+    assert res[0][1][1] >= 2
