@@ -40,6 +40,8 @@ extern "C" {
 #define KH_E_OVERFLOW -5   /* caller's output array too small (count is still reported) */
 #define KH_E_BSGS_N -6     /* BSGS: n has no exact square root / sqrt(n) not a multiple of 1024 */
 #define KH_E_RANGE -7      /* BSGS: range smaller than N ("[E] the given range is small") */
+#define KH_E_IO -8         /* table file missing, short or not writable (see kh_last_error) */
+#define KH_E_FORMAT -9     /* table file of another N/k, or its sha256 checksum does not match */
 
 /* scan modes (-m) and search kinds (-l) */
 #define KH_MODE_ADDRESS 0  /* -m address / -m rmd160: hash160 probes */
@@ -121,6 +123,16 @@ int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride[32], uint
 int kh_bsgs_set_layer1(kh_ctx *ctx, uint32_t layout);
 int kh_bsgs_setup(kh_ctx *ctx, uint64_t n, uint64_t k, kh_bsgs_info *info);
 int kh_bsgs_build(kh_ctx *ctx);                  /* baby-step blooms + sorted bP table on the GPU */
+/* -S table files in the reference's formats (keyhunt.cpp:2504-2652 write, 1983-2230 read), in dir
+ * (NULL -> "."): keyhunt_bsgs_4_<M>.blm, keyhunt_bsgs_6_<M2>.blm, keyhunt_bsgs_7_<M3>.blm (256 x
+ * {struct bloom, bits, sha256 x2}) and keyhunt_bsgs_2_<M3>.tbl (sorted 16-byte rows + sha256).
+ * Files are byte-identical to the reference's except the heap pointer it stores in each struct
+ * bloom.  kh_bsgs_save needs kh_bsgs_build (or _load) first; with the blocked layer 1 it builds the
+ * reference-layout layer 1 for the file.  kh_bsgs_load replaces kh_bsgs_build after kh_bsgs_setup;
+ * with the blocked layout it checks the layer-1 file and rebuilds the blocked layer on the GPU. */
+#define KH_LOAD_SKIP_CHECKSUM 1   /* the reference's -6 */
+int kh_bsgs_save(kh_ctx *ctx, const char *dir);
+int kh_bsgs_load(kh_ctx *ctx, const char *dir, uint32_t flags);
 /* targets: n x {x[32], y[32]} affine points (big-endian) */
 int kh_bsgs_set_targets(kh_ctx *ctx, const uint8_t *xy, uint32_t n);
 /* Walk n_bases bases start, start + 2N, ... for every target not yet found.  Keys already found

@@ -324,6 +324,8 @@ struct kh_ctx {
   bool bsgs_ready = false, bsgs_built = false;
   kh_bsgs_info info{};
   bloom_desc bd[3]{};
+  bloom_desc bd_ref1{};      // layer 1 in the reference layout (what its files hold)
+  uint64_t entries[3]{};     // bloom_init2 entries per layer (file headers)
   uint8_t *d_bl[3] = {nullptr, nullptr, nullptr};
   std::vector<uint8_t> h_bl[3];  // layers 2 and 3 on the host for refinement (index 1, 2)
   std::vector<uint8_t> h_rows;   // sorted 16-byte bsgs_xvalue rows
@@ -565,6 +567,8 @@ const char *kh_strerror(int code) {
     case KH_E_OVERFLOW: return "output buffer too small";
     case KH_E_BSGS_N: return "BSGS n has no exact square root or sqrt(n) is not a multiple of 1024";
     case KH_E_RANGE: return "the given range is small";
+    case KH_E_IO: return "file missing, short or not writable";
+    case KH_E_FORMAT: return "file does not match the BSGS geometry or its checksum";
     default: return "unknown error";
   }
 }
@@ -819,6 +823,7 @@ int kh_bsgs_setup(kh_ctx *ctx, uint64_t n, uint64_t k, kh_bsgs_info *info) {
   if (n % m) n = m * aux;
   kh_bsgs_info &I = ctx->info;
   memset(&I, 0, sizeof I);
+  ctx->entries[0] = ctx->entries[1] = ctx->entries[2] = 0;
   I.n = n;
   I.m = m;
   I.m2 = m2;
@@ -830,7 +835,10 @@ int kh_bsgs_setup(kh_ctx *ctx, uint64_t n, uint64_t k, kh_bsgs_info *info) {
   it[1] = (m2 / 256 > 1000) ? (m2 / 256 + (m2 % 256 ? 1 : 0)) : 1000;
   it[2] = (m3 / 256 > 1000) ? (m3 / 256 + (m3 % 256 ? 1 : 0)) : 1000;
   for (int l = 0; l < 3; l++) {
-    ctx->bd[l] = bloom_size(bloom_entries(it[l]));
+    ctx->entries[l] = bloom_entries(it[l]);
+    ctx->bd[l] = bloom_size(ctx->entries[l]);
+    ctx->bd_ref1 = l == 0 ? ctx->bd[0] : ctx->bd_ref1;
+    ctx->bd_ref1.stride = (ctx->bd_ref1.bytes + 255) & ~255ULL;
     if (l == 0 && ctx->l1_layout == KH_LAYER1_BLOCKED) {
       // 3x the reference's bits per shard in whole 128-bit blocks (kh_kernels.h); desc.bits = blocks
       uint64_t blocks = (ctx->bd[0].bits * KH_BLK_BITS_MUL + 127) / 128;
@@ -892,10 +900,10 @@ int kh_bsgs_set_layer1(kh_ctx *ctx, uint32_t layout) {
   return KH_OK;
 }
 
-int kh_bsgs_build(kh_ctx *ctx) {
-  if (!ctx) return KH_E_ARG;
-  if (!ctx->bsgs_ready) return KH_E_STATE;
-  (void)hipSetDevice(ctx->device);
+namespace {
+// the baby-step walk (thread_bPload, keyhunt.cpp:5284-5472): babies (i+1)G, i < M, into layer 1
+// (bl1/bd1, reference or blocked layout by `mode`), layers 2/3 (the context's) and the bP rows
+int build_walk(kh_ctx *ctx, int mode, uint8_t *bl1, const bloom_desc &bd1, uint64_t *d_key, uint32_t *d_val) {
   const int H = KH_WALK_H;
   const kh_bsgs_info &I = ctx->info;
   const uint32_t *tab = nullptr;
@@ -907,10 +915,6 @@ int kh_bsgs_build(kh_ctx *ctx) {
   for (uint32_t g = 0; g < jg.L; g++) s[g] = u256_u64(1 + (uint64_t)g * jg.gpl * 2 * H + H);  // baby i <-> key i+1
   r = run_setup(ctx, s, nullptr);
   if (r) return r;
-  uint64_t *d_key = nullptr;
-  uint32_t *d_val = nullptr;
-  HIPCHK(ctx, hipMalloc(&d_key, I.m3 * 8));
-  HIPCHK(ctx, hipMalloc(&d_val, I.m3 * 4));
   walk_args A;
   memset(&A, 0, sizeof A);
   A.tab = tab;
@@ -920,17 +924,31 @@ int kh_bsgs_build(kh_ctx *ctx) {
   A.L = jg.L;
   A.lane_stride = jg.gpl * 2 * H;
   A.n_points = I.m;
-  A.bl1 = ctx->d_bl[0];
+  A.bl1 = bl1;
   A.bl2 = ctx->d_bl[1];
   A.bl3 = ctx->d_bl[2];
-  A.bd = ctx->bd[0];
+  A.bd = bd1;
   A.bd2 = ctx->bd[1];
   A.bd3 = ctx->bd[2];
   A.m2 = I.m2;
   A.m3 = I.m3;
   A.rows_key = d_key;
   A.rows_val = d_val;
-  r = run_walk(ctx, ctx->l1_layout == KH_LAYER1_BLOCKED ? KM_BUILDB : KM_BUILD, 3, A, jg.gpl, 4);
+  return run_walk(ctx, mode, 3, A, jg.gpl, 4);
+}
+}  // namespace
+
+int kh_bsgs_build(kh_ctx *ctx) {
+  if (!ctx) return KH_E_ARG;
+  if (!ctx->bsgs_ready) return KH_E_STATE;
+  (void)hipSetDevice(ctx->device);
+  const kh_bsgs_info &I = ctx->info;
+  int r;
+  uint64_t *d_key = nullptr;
+  uint32_t *d_val = nullptr;
+  HIPCHK(ctx, hipMalloc(&d_key, I.m3 * 8));
+  HIPCHK(ctx, hipMalloc(&d_val, I.m3 * 4));
+  r = build_walk(ctx, ctx->l1_layout == KH_LAYER1_BLOCKED ? KM_BUILDB : KM_BUILD, ctx->d_bl[0], ctx->bd[0], d_key, d_val);
   if (r) {
     (void)hipFree(d_key);
     (void)hipFree(d_val);
@@ -961,6 +979,266 @@ int kh_bsgs_build(kh_ctx *ctx) {
     ctx->h_bl[l].resize(256 * ctx->bd[l].stride);
     HIPCHK(ctx, hipMemcpy(ctx->h_bl[l].data(), ctx->d_bl[l], ctx->h_bl[l].size(), hipMemcpyDeviceToHost));
   }
+  ctx->bsgs_built = true;
+  return KH_OK;
+}
+
+// ==============================================================================================
+// BSGS table files (-S, keyhunt.cpp:1983-2230 read, 2504-2652 write): per layer 256 records of
+// {struct bloom (112 B), bit array, checksumsha256 {sha256(bits), same again}} in
+// keyhunt_bsgs_4_<M>.blm / _6_<M2>.blm / _7_<M3>.blm, and the sorted bP rows + sha256 in
+// keyhunt_bsgs_2_<M3>.tbl.
+// ==============================================================================================
+namespace {
+
+// SHA-256 of a byte string (the reference's sha256(), hash/sha256.cpp), on kh_math.h's compression
+void sha256_bytes(const uint8_t *p, size_t n, uint8_t out[32]) {
+  uint32_t st[8], w[16];
+  sha256_init(st);
+  uint8_t blk[64];
+  size_t off = 0;
+  auto compress = [&](const uint8_t *b) {
+    for (int i = 0; i < 16; i++)
+      w[i] = ((uint32_t)b[4 * i] << 24) | ((uint32_t)b[4 * i + 1] << 16) | ((uint32_t)b[4 * i + 2] << 8) | b[4 * i + 3];
+    sha256_transform(st, w);
+  };
+  for (; off + 64 <= n; off += 64) compress(p + off);
+  size_t rem = n - off;
+  memset(blk, 0, 64);
+  memcpy(blk, p + off, rem);
+  blk[rem] = 0x80;
+  if (rem >= 56) {
+    compress(blk);
+    memset(blk, 0, 64);
+  }
+  const uint64_t bits = (uint64_t)n * 8;
+  for (int i = 0; i < 8; i++) blk[56 + i] = (uint8_t)(bits >> (56 - 8 * i));
+  compress(blk);
+  for (int i = 0; i < 8; i++) {
+    out[4 * i] = (uint8_t)(st[i] >> 24);
+    out[4 * i + 1] = (uint8_t)(st[i] >> 16);
+    out[4 * i + 2] = (uint8_t)(st[i] >> 8);
+    out[4 * i + 3] = (uint8_t)st[i];
+  }
+}
+
+constexpr size_t KH_BLOOM_STRUCT = 112;  // sizeof(struct bloom) on x86-64 (bloom/bloom.h:26-49)
+
+// struct bloom as bloom_init2 leaves it (bloom/bloom.cpp:154-187): entries, bits, bytes, hashes,
+// error (x87 long double), ready = 1, version 2.201, bpe; the pointers and chunk fields are 0 here
+// (the reference writes its own heap pointer into `bf` and replaces it on reading)
+void bloom_header(uint8_t h[KH_BLOOM_STRUCT], uint64_t entries, const bloom_desc &d) {
+  memset(h, 0, KH_BLOOM_STRUCT);
+  memcpy(h + 0, &entries, 8);
+  memcpy(h + 8, &d.bits, 8);
+  memcpy(h + 16, &d.bytes, 8);
+  h[24] = (uint8_t)d.hashes;
+  const long double err = 0.000001;
+  memcpy(h + 32, &err, 10);
+  h[48] = 1;
+  h[49] = 2;
+  h[50] = 201;
+  const long double num = -logl(err), denom = 0.480453013918201;
+  const double bpe = (double)(num / denom);
+  memcpy(h + 56, &bpe, 8);
+}
+
+struct table_path {
+  std::string s;
+  table_path(const char *dir, int kind, uint64_t m, const char *ext) {
+    char name[96];
+    snprintf(name, sizeof name, "keyhunt_bsgs_%d_%llu.%s", kind, (unsigned long long)m, ext);
+    s = std::string((dir && *dir) ? dir : ".") + "/" + name;
+  }
+};
+
+// one layer (256 shards at d.stride in `bits`) -> .blm
+int write_blm(kh_ctx *c, const std::string &path, const uint8_t *bits, const bloom_desc &d, uint64_t entries) {
+  FILE *f = fopen(path.c_str(), "wb");
+  if (!f) {
+    c->err = "can't create the file " + path;
+    return KH_E_IO;
+  }
+  uint8_t h[KH_BLOOM_STRUCT], ck[64];
+  bloom_header(h, entries, d);
+  bool ok = true;
+  for (int i = 0; i < 256 && ok; i++) {
+    const uint8_t *bf = bits + (size_t)i * d.stride;
+    sha256_bytes(bf, d.bytes, ck);
+    memcpy(ck + 32, ck, 32);
+    ok = fwrite(h, KH_BLOOM_STRUCT, 1, f) == 1 && fwrite(bf, d.bytes, 1, f) == 1 && fwrite(ck, 64, 1, f) == 1;
+  }
+  ok = (fclose(f) == 0) && ok;
+  if (!ok) {
+    c->err = "error writing the file " + path;
+    return KH_E_IO;
+  }
+  return KH_OK;
+}
+
+// .blm -> one layer (256 shards at d.stride in `bits`); headers must carry this geometry
+int read_blm(kh_ctx *c, const std::string &path, uint8_t *bits, const bloom_desc &d, uint64_t entries, bool verify) {
+  FILE *f = fopen(path.c_str(), "rb");
+  if (!f) {
+    c->err = "missing file " + path;
+    return KH_E_IO;
+  }
+  uint8_t h[KH_BLOOM_STRUCT], ck[64], sum[32];
+  int rc = KH_OK;
+  for (int i = 0; i < 256 && rc == KH_OK; i++) {
+    uint8_t *bf = bits + (size_t)i * d.stride;
+    if (fread(h, KH_BLOOM_STRUCT, 1, f) != 1) {
+      rc = KH_E_IO;
+      break;
+    }
+    uint64_t fe_, fb, fy;
+    memcpy(&fe_, h, 8);
+    memcpy(&fb, h + 8, 8);
+    memcpy(&fy, h + 16, 8);
+    if (fe_ != entries || fb != d.bits || fy != d.bytes || h[24] != (uint8_t)d.hashes || h[48] != 1) {
+      c->err = "bloom geometry in " + path + " does not match this N/k";
+      rc = KH_E_FORMAT;
+      break;
+    }
+    if (fread(bf, d.bytes, 1, f) != 1 || fread(ck, 64, 1, f) != 1) {
+      rc = KH_E_IO;
+      break;
+    }
+    if (verify) {
+      sha256_bytes(bf, d.bytes, sum);
+      if (memcmp(ck, sum, 32) != 0 || memcmp(ck + 32, sum, 32) != 0) {
+        c->err = "checksum file mismatch! " + path;
+        rc = KH_E_FORMAT;
+      }
+    }
+  }
+  if (rc == KH_E_IO) c->err = "error reading the file " + path;
+  fclose(f);
+  return rc;
+}
+
+// layer 1 in the reference layout on the host: the device layer itself, or (blocked layout) a
+// reference-layout baby walk into a temporary buffer
+int ref_layer1(kh_ctx *c, std::vector<uint8_t> &out) {
+  const bloom_desc &d = c->bd_ref1;
+  out.assign(256 * d.stride, 0);
+  if (c->l1_layout == KH_LAYER1_REFERENCE) {
+    HIPCHK(c, hipMemcpy(out.data(), c->d_bl[0], out.size(), hipMemcpyDeviceToHost));
+    return KH_OK;
+  }
+  uint8_t *tmp = nullptr;
+  uint64_t *d_key = nullptr;
+  uint32_t *d_val = nullptr;
+  int r = KH_OK;
+  if (hipMalloc(&tmp, out.size() + 4) != hipSuccess || hipMalloc(&d_key, c->info.m3 * 8) != hipSuccess ||
+      hipMalloc(&d_val, c->info.m3 * 4) != hipSuccess || hipMemset(tmp, 0, out.size() + 4) != hipSuccess) {
+    c->err = "no device memory for the reference-layout layer 1";
+    r = KH_E_NOMEM;
+  }
+  if (r == KH_OK) r = build_walk(c, KM_BUILD, tmp, d, d_key, d_val);
+  if (r == KH_OK && hipMemcpy(out.data(), tmp, out.size(), hipMemcpyDeviceToHost) != hipSuccess) r = KH_E_HIP;
+  (void)hipFree(tmp);
+  (void)hipFree(d_key);
+  (void)hipFree(d_val);
+  return r;
+}
+
+}  // namespace
+
+int kh_bsgs_save(kh_ctx *ctx, const char *dir) {
+  if (!ctx) return KH_E_ARG;
+  if (!ctx->bsgs_built) return KH_E_STATE;
+  (void)hipSetDevice(ctx->device);
+  const kh_bsgs_info &I = ctx->info;
+  std::vector<uint8_t> l1;
+  int r = ref_layer1(ctx, l1);
+  if (r) return r;
+  r = write_blm(ctx, table_path(dir, 4, I.m, "blm").s, l1.data(), ctx->bd_ref1, ctx->entries[0]);
+  if (r) return r;
+  l1.clear();
+  l1.shrink_to_fit();
+  r = write_blm(ctx, table_path(dir, 6, I.m2, "blm").s, ctx->h_bl[1].data(), ctx->bd[1], ctx->entries[1]);
+  if (r) return r;
+  r = write_blm(ctx, table_path(dir, 7, I.m3, "blm").s, ctx->h_bl[2].data(), ctx->bd[2], ctx->entries[2]);
+  if (r) return r;
+  const std::string tp = table_path(dir, 2, I.m3, "tbl").s;
+  FILE *f = fopen(tp.c_str(), "wb");
+  if (!f) {
+    ctx->err = "can't create the file " + tp;
+    return KH_E_IO;
+  }
+  uint8_t ck[32];
+  sha256_bytes(ctx->h_rows.data(), ctx->h_rows.size(), ck);
+  bool ok = fwrite(ctx->h_rows.data(), ctx->h_rows.size(), 1, f) == 1 && fwrite(ck, 32, 1, f) == 1;
+  ok = (fclose(f) == 0) && ok;
+  if (!ok) {
+    ctx->err = "error writing the file " + tp;
+    return KH_E_IO;
+  }
+  return KH_OK;
+}
+
+int kh_bsgs_load(kh_ctx *ctx, const char *dir, uint32_t flags) {
+  if (!ctx) return KH_E_ARG;
+  if (!ctx->bsgs_ready) return KH_E_STATE;
+  (void)hipSetDevice(ctx->device);
+  const kh_bsgs_info &I = ctx->info;
+  const bool verify = !(flags & KH_LOAD_SKIP_CHECKSUM);
+  ctx->bsgs_built = false;
+  // bP table
+  const std::string tp = table_path(dir, 2, I.m3, "tbl").s;
+  std::vector<uint8_t> rows(I.m3 * 16);
+  {
+    FILE *f = fopen(tp.c_str(), "rb");
+    if (!f) {
+      ctx->err = "missing file " + tp;
+      return KH_E_IO;
+    }
+    uint8_t ck[32], sum[32];
+    bool ok = fread(rows.data(), rows.size(), 1, f) == 1 && fread(ck, 32, 1, f) == 1;
+    fclose(f);
+    if (!ok) {
+      ctx->err = "error reading the file " + tp;
+      return KH_E_IO;
+    }
+    if (verify) {
+      sha256_bytes(rows.data(), rows.size(), sum);
+      if (memcmp(ck, sum, 32) != 0) {
+        ctx->err = "checksum file mismatch! " + tp;
+        return KH_E_FORMAT;
+      }
+    }
+  }
+  // layers 2 and 3 (host copies serve the refinement)
+  for (int l = 1; l < 3; l++) {
+    std::vector<uint8_t> &h = ctx->h_bl[l];
+    h.assign(256 * ctx->bd[l].stride, 0);
+    int r = read_blm(ctx, table_path(dir, l == 1 ? 6 : 7, l == 1 ? I.m2 : I.m3, "blm").s, h.data(), ctx->bd[l],
+                     ctx->entries[l], verify);
+    if (r) return r;
+    HIPCHK(ctx, hipMemcpy(ctx->d_bl[l], h.data(), h.size(), hipMemcpyHostToDevice));
+  }
+  // layer 1: the file's bits for the reference layout; the blocked layout is rebuilt on the GPU
+  // (its bits are not in any reference file), after checking the file all the same
+  {
+    std::vector<uint8_t> l1(256 * ctx->bd_ref1.stride, 0);
+    int r = read_blm(ctx, table_path(dir, 4, I.m, "blm").s, l1.data(), ctx->bd_ref1, ctx->entries[0], verify);
+    if (r) return r;
+    if (ctx->l1_layout == KH_LAYER1_REFERENCE) {
+      HIPCHK(ctx, hipMemcpy(ctx->d_bl[0], l1.data(), l1.size(), hipMemcpyHostToDevice));
+    } else {
+      uint64_t *d_key = nullptr;
+      uint32_t *d_val = nullptr;
+      HIPCHK(ctx, hipMalloc(&d_key, I.m3 * 8));
+      HIPCHK(ctx, hipMalloc(&d_val, I.m3 * 4));
+      HIPCHK(ctx, hipMemset(ctx->d_bl[0], 0, 256 * ctx->bd[0].stride + 4));
+      r = build_walk(ctx, KM_BUILDB, ctx->d_bl[0], ctx->bd[0], d_key, d_val);
+      (void)hipFree(d_key);
+      (void)hipFree(d_val);
+      if (r) return r;
+    }
+  }
+  ctx->h_rows.swap(rows);
   ctx->bsgs_built = true;
   return KH_OK;
 }

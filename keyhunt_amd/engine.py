@@ -84,6 +84,8 @@ def lib() -> ctypes.CDLL:
     L.kh_bsgs_setup.argtypes = [P, ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(KhBsgsInfo)]
     L.kh_bsgs_set_layer1.argtypes = [P, ctypes.c_uint32]
     L.kh_bsgs_build.argtypes = [P]
+    L.kh_bsgs_save.argtypes = [P, ctypes.c_char_p]
+    L.kh_bsgs_load.argtypes = [P, ctypes.c_char_p, ctypes.c_uint32]
     L.kh_bsgs_set_targets.argtypes = [P, u8p, ctypes.c_uint32]
     L.kh_bsgs_scan.argtypes = [P, u8p, ctypes.c_uint64, ctypes.POINTER(KhBsgsFound), ctypes.c_uint32,
                                ctypes.POINTER(ctypes.c_uint32)]
@@ -194,6 +196,14 @@ class Engine:
 
     def bsgs_build(self) -> None:
         self._chk(lib().kh_bsgs_build(self._ctx), "kh_bsgs_build")
+
+    def bsgs_save(self, directory: str) -> None:
+        """Write the -S table files (keyhunt_bsgs_{4,6,7}_*.blm, keyhunt_bsgs_2_*.tbl) into directory."""
+        self._chk(lib().kh_bsgs_save(self._ctx, directory.encode()), "kh_bsgs_save")
+
+    def bsgs_load(self, directory: str, skip_checksum: bool = False) -> None:
+        """Load the -S table files instead of bsgs_build (after bsgs_setup)."""
+        self._chk(lib().kh_bsgs_load(self._ctx, directory.encode(), 1 if skip_checksum else 0), "kh_bsgs_load")
 
     def bsgs_set_targets(self, points: list[tuple[int, int]]) -> None:
         buf = b"".join(be32(x) + be32(y) for x, y in points)

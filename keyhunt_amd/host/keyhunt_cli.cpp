@@ -7,8 +7,8 @@
 // Sequential scans consume the range in whole N_SEQUENTIAL_MAX chunks (keyhunt.cpp:3314-3330) and
 // BSGS in whole 2N bases (keyhunt.cpp:4600-4617), exactly as the reference's cursors do.
 // BSGS base schedules -B sequential|backward|both|random|dance|angrygiant and random chunks (-R)
-// follow the reference's cursors (see take_bases).  Endomorphism (-e), -B ggsb, vanity, minikeys,
-// ETH and the table persistence flags are outside this engine's scope and are rejected.
+// follow the reference's cursors (see take_bases).  -e (address/rmd160/xpoint) and -S / -6 (BSGS table
+// files in the reference's formats) are provided; -B ggsb, vanity, minikeys and ETH are rejected.
 #include <getopt.h>
 #include <pthread.h>
 #include <stdint.h>
@@ -334,6 +334,8 @@ struct options {
   bool endo = false;    // -e
   bool stride_set = false;
   int bsgs_mode = 0;    // -B, index into BSGS_MODES
+  bool save_read = false;      // -S: read the table files if present, else build and write them
+  bool skip_checksum = false;  // -6
 } opt;
 // keyhunt.cpp:419; ggsb (re-blocked baby tables) is not provided, angrygiant walks like sequential
 const char *BSGS_MODES[7] = {"sequential", "backward", "both", "random", "dance", "ggsb", "angrygiant"};
@@ -604,6 +606,7 @@ struct bsgs_job {
   const std::vector<bool> *comp;
   uint64_t n, k;
   uint64_t bases_per_call;
+  bool first = false;  // the first GPU's worker (writes the -S files)
   int rc = 0;
 };
 std::vector<uint8_t> g_found;  // bsgs_found[]
@@ -659,6 +662,53 @@ bool take_bases(const U &twoN, uint64_t want, std::vector<U> &out) {
   return !out.empty();
 }
 
+// -S (keyhunt.cpp:1983-2230, 2504-2652): the files of this N/k in the working directory are read
+// when they are all there, else the tables are built and (by the first GPU's worker) written.
+int bsgs_tables(kh_ctx *ctx, const kh_bsgs_info &info, bool first) {
+  if (!opt.save_read) return kh_bsgs_build(ctx);
+  char f4[96], f6[96], f7[96], f2[96];
+  snprintf(f4, sizeof f4, "keyhunt_bsgs_4_%llu.blm", (unsigned long long)info.m);
+  snprintf(f6, sizeof f6, "keyhunt_bsgs_6_%llu.blm", (unsigned long long)info.m2);
+  snprintf(f7, sizeof f7, "keyhunt_bsgs_7_%llu.blm", (unsigned long long)info.m3);
+  snprintf(f2, sizeof f2, "keyhunt_bsgs_2_%llu.tbl", (unsigned long long)info.m3);
+  static std::mutex mtx;
+  static int decided = 0;  // 1: every worker reads the files, 2: every worker builds, the first writes
+  {
+    std::lock_guard<std::mutex> lk(mtx);
+    if (!decided) {
+      bool all = true;
+      for (const char *f : {f4, f6, f7, f2}) all = all && access(f, R_OK) == 0;
+      decided = all ? 1 : 2;
+    }
+  }
+  if (decided == 1) {
+    int r = kh_bsgs_load(ctx, ".", opt.skip_checksum ? KH_LOAD_SKIP_CHECKSUM : 0);
+    if (r) {
+      fprintf(stderr, "[E] %s\n", kh_last_error(ctx));
+      return r;
+    }
+    if (first) {
+      printf("[+] Reading bloom filter from file %s .... Done!\n", f4);
+      printf("[+] Reading bloom filter from file %s .... Done!\n", f6);
+      printf("[+] Reading bP Table from file %s .... Done!\n", f2);
+      printf("[+] Reading bloom filter from file %s .... Done!\n", f7);
+    }
+    return KH_OK;
+  }
+  int r = kh_bsgs_build(ctx);
+  if (r || !first) return r;
+  r = kh_bsgs_save(ctx, ".");
+  if (r) {
+    fprintf(stderr, "[E] %s\n", kh_last_error(ctx));
+    return r;
+  }
+  printf("[+] Writing bloom filter to file %s .... Done!\n", f4);
+  printf("[+] Writing bloom filter to file %s .... Done!\n", f6);
+  printf("[+] Writing bP Table to file %s .. Done!\n", f2);
+  printf("[+] Writing bloom filter to file %s .... Done!\n", f7);
+  return KH_OK;
+}
+
 void bsgs_worker(bsgs_job *j) {
   kh_ctx *ctx = nullptr;
   int r = kh_open(j->device, &ctx);
@@ -670,7 +720,7 @@ void bsgs_worker(bsgs_job *j) {
   kh_bsgs_info info;
   r = kh_bsgs_set_layer1(ctx, opt.layer1);
   if (!r) r = kh_bsgs_setup(ctx, j->n, j->k, &info);
-  if (!r) r = kh_bsgs_build(ctx);
+  if (!r) r = bsgs_tables(ctx, info, j->first);
   size_t nt = j->tx->size();
   std::vector<uint8_t> xy(64 * nt);
   for (size_t i = 0; i < nt; i++) {
@@ -757,7 +807,7 @@ int main(int argc, char **argv) {
   int c;
   U order;
   u_from_hex(ORDER_HEX, order);
-  while ((c = getopt(argc, argv, "m:f:l:r:b:k:n:t:g:qs:I:L:MRec:B:S")) != -1) {
+  while ((c = getopt(argc, argv, "m:f:l:r:b:k:n:t:g:qs:I:L:MRec:B:S6")) != -1) {
     switch (c) {
       case 'm': {
         int m = -1;
@@ -840,7 +890,12 @@ int main(int argc, char **argv) {
         opt.endo = true;
         printf("[+] Endomorphism enabled\n");
         break;
-      case 'c': case 'S':
+      case 'S': opt.save_read = true; break;  // keyhunt.cpp:1073-1075
+      case '6':  // keyhunt.cpp:837-840
+        opt.skip_checksum = true;
+        fprintf(stderr, "[W] Skipping checksums on files\n");
+        break;
+      case 'c':
         fprintf(stderr, "[E] -%c is outside the scope of this engine\n", c);
         return EXIT_FAILURE;
       default: usage(argv[0]); return EXIT_FAILURE;
@@ -966,6 +1021,7 @@ int main(int argc, char **argv) {
     g_running = gpus;
     for (int d = 0; d < gpus; d++) {
       bj[d].device = d;
+      bj[d].first = d == 0;
       bj[d].tx = &tx;
       bj[d].ty = &ty;
       bj[d].comp = &comp;

@@ -9,8 +9,10 @@ TEST INFRASTRUCTURE.  Runs in the development container only (needs /root/refere
   tests/golden/ref_e2e.json      end-to-end hit sets of oracle/_ref/keyhunt (the reference CLI) on
                                  known-answer windows, parsed from the
                                  KEYFOUNDKEYFOUND.txt it writes.
+  tests/golden/ref_tables.json   digests of the -S table files the reference CLI writes at small
+                                 (n, k) (heap pointers masked).
 
-Usage:  python oracle/make_golden.py [--vectors] [--e2e]
+Usage:  python oracle/make_golden.py [--vectors] [--e2e] [--tables]
 """
 from __future__ import annotations
 
@@ -60,6 +62,43 @@ E2E_RUNS = [
 ]
 
 
+# -S table files (keyhunt.cpp:2504-2652) written by the reference for small (n, k): their sha256
+# with each struct bloom's `bf` heap pointer (bytes 64..72 of every 112-byte header) zeroed
+TABLE_RUNS = [
+    ("n1000000_k2", ["-m", "bsgs", "-f", "63.pub", "-n", "0x1000000", "-k", "2", "-r", "7cce5efdac000000:7cce5efdad000000", "-S", "-t", "4"]),
+    ("n4000000_k3", ["-m", "bsgs", "-f", "63.pub", "-n", "0x4000000", "-k", "3", "-r", "7cce5efdac000000:7cce5efdb0000000", "-S", "-t", "4"]),
+    # layer 1 past the 10000-entry floor (M/256 = 16384 entries per shard)
+    ("n100000000_k64", ["-m", "bsgs", "-f", "63.pub", "-n", "0x100000000", "-k", "64", "-r", "7cce5efd00000000:7cce5efe00000000", "-S", "-t", "8"]),
+]
+
+
+def masked_table_digest(path: str) -> str:
+    import hashlib
+    data = bytearray(open(path, "rb").read())
+    if path.endswith(".blm"):
+        rec = len(data) // 256
+        for i in range(256):
+            data[i * rec + 64: i * rec + 72] = bytes(8)
+    return hashlib.sha256(bytes(data)).hexdigest()
+
+
+def gen_tables() -> None:
+    subprocess.run(["make", "-s", "-C", HERE, "-f", "Makefile.ref", "-j8"], check=True)
+    out = {}
+    for name, argv in TABLE_RUNS:
+        with tempfile.TemporaryDirectory() as td:
+            shutil.copy(os.path.join(DATA, "63.pub"), td)
+            p = subprocess.run(["timeout", "300", REF_BIN] + argv + ["-q"], cwd=td, capture_output=True, text=True)
+            files = sorted(f for f in os.listdir(td) if f.startswith("keyhunt_bsgs_"))
+            out[name] = {"argv": argv, "exit": p.returncode,
+                         "files": {f: masked_table_digest(os.path.join(td, f)) for f in files},
+                         "sizes": {f: os.path.getsize(os.path.join(td, f)) for f in files}}
+            print(name, p.returncode, files, flush=True)
+    out["_generator"] = "oracle/make_golden.py --tables: oracle/_ref/keyhunt -S (reference CLI built from its sources)"
+    with open(os.path.join(REPO, "tests", "golden", "ref_tables.json"), "w") as f:
+        json.dump(out, f, indent=1, sort_keys=True)
+
+
 def gen_vectors() -> None:
     subprocess.run(["make", "-s", "-C", HERE, "-f", "Makefile.ref", "-j8"], check=True)
     out = subprocess.run([REF_GOLDEN], check=True, capture_output=True, text=True).stdout
@@ -104,11 +143,14 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--vectors", action="store_true")
     ap.add_argument("--e2e", action="store_true")
+    ap.add_argument("--tables", action="store_true")
     ap.add_argument("--only", nargs="*")
     a = ap.parse_args()
-    if not a.vectors and not a.e2e:
-        a.vectors = a.e2e = True
+    if not a.vectors and not a.e2e and not a.tables:
+        a.vectors = a.e2e = a.tables = True
     if a.vectors:
         gen_vectors()
     if a.e2e:
         gen_e2e(a.only)
+    if a.tables:
+        gen_tables()
