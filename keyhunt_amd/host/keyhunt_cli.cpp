@@ -28,167 +28,14 @@
 
 #include "kh_gpu.h"
 #include "../csrc/kh_math.h"
+#include "kh_host_util.h"
 
 using namespace kh;
+using namespace khh;
 
 namespace {
 
 const char *VERSION = "keyhunt-amd 0.1 (MI355X engine for keyhunt 0.2.230519 hot paths)";
-
-// ---------------------------------------------------------------------------------------------
-// big integers (256-bit, plus a little headroom for range arithmetic)
-// ---------------------------------------------------------------------------------------------
-typedef unsigned __int128 u128;
-struct U {
-  uint64_t v[5] = {0, 0, 0, 0, 0};
-};
-U u_from_u64(uint64_t x) {
-  U r;
-  r.v[0] = x;
-  return r;
-}
-int u_cmp(const U &a, const U &b) {
-  for (int i = 4; i >= 0; i--) {
-    if (a.v[i] < b.v[i]) return -1;
-    if (a.v[i] > b.v[i]) return 1;
-  }
-  return 0;
-}
-U u_add(const U &a, const U &b) {
-  U r;
-  u128 c = 0;
-  for (int i = 0; i < 5; i++) {
-    c += (u128)a.v[i] + b.v[i];
-    r.v[i] = (uint64_t)c;
-    c >>= 64;
-  }
-  return r;
-}
-U u_sub(const U &a, const U &b) {
-  U r;
-  uint64_t br = 0;
-  for (int i = 0; i < 5; i++) {
-    u128 t = (u128)a.v[i] - b.v[i] - br;
-    r.v[i] = (uint64_t)t;
-    br = (uint64_t)(t >> 64) & 1;
-  }
-  return r;
-}
-U u_mul_u64(const U &a, uint64_t m) {
-  U r;
-  u128 c = 0;
-  for (int i = 0; i < 5; i++) {
-    c += (u128)a.v[i] * m;
-    r.v[i] = (uint64_t)c;
-    c >>= 64;
-  }
-  return r;
-}
-bool u_is_zero(const U &a) { return !(a.v[0] | a.v[1] | a.v[2] | a.v[3] | a.v[4]); }
-U u_shl1(int bits) {  // 1 << bits
-  U r;
-  r.v[bits / 64] = 1ULL << (bits % 64);
-  return r;
-}
-// a / b for b < 2^64, and remainder
-U u_divmod_u64(const U &a, uint64_t b, uint64_t *rem) {
-  U q;
-  u128 r = 0;
-  for (int i = 4; i >= 0; i--) {
-    r = (r << 64) | a.v[i];
-    q.v[i] = (uint64_t)(r / b);
-    r %= b;
-  }
-  if (rem) *rem = (uint64_t)r;
-  return q;
-}
-int u_bitlen(const U &a) {
-  for (int i = 4; i >= 0; i--)
-    if (a.v[i]) return 64 * i + 64 - __builtin_clzll(a.v[i]);
-  return 0;
-}
-// uniform in [a, b) by rejection over bitlen(b - a) bits (the reference's Int::Rand(a, b) draws
-// from MT19937 seeded by getrandom, keyhunt.cpp:697-715; not reproducible there either)
-std::mt19937_64 g_rng{std::random_device{}()};
-std::mutex g_rng_mtx;
-U u_rand_range(const U &a, const U &b) {
-  if (u_cmp(b, a) <= 0) return a;
-  U span = u_sub(b, a), r;
-  int bits = u_bitlen(span);
-  std::lock_guard<std::mutex> lk(g_rng_mtx);
-  do {
-    for (int i = 0; i < 5; i++) {
-      int lo = 64 * i;
-      r.v[i] = lo >= bits ? 0 : g_rng();
-      if (lo < bits && bits - lo < 64) r.v[i] &= (1ULL << (bits - lo)) - 1;
-    }
-  } while (u_cmp(r, span) >= 0);
-  return u_add(a, r);
-}
-bool u_from_hex(const char *s, U &r) {
-  r = U();
-  if (s[0] == '0' && (s[1] == 'x' || s[1] == 'X')) s += 2;
-  size_t n = strlen(s);
-  if (n == 0 || n > 64) return false;
-  for (size_t i = 0; i < n; i++) {
-    char c = s[i];
-    int d = (c >= '0' && c <= '9') ? c - '0' : (c >= 'a' && c <= 'f') ? c - 'a' + 10 : (c >= 'A' && c <= 'F') ? c - 'A' + 10 : -1;
-    if (d < 0) return false;
-    // r = r*16 + d
-    for (int k = 4; k > 0; k--) r.v[k] = (r.v[k] << 4) | (r.v[k - 1] >> 60);
-    r.v[0] = (r.v[0] << 4) | (uint64_t)d;
-  }
-  return true;
-}
-bool u_from_dec(const char *s, U &r) {
-  r = U();
-  if (!*s) return false;
-  for (; *s; s++) {
-    if (*s < '0' || *s > '9') return false;
-    r = u_add(u_mul_u64(r, 10), u_from_u64((uint64_t)(*s - '0')));
-  }
-  return true;
-}
-// lowercase hex without leading zeros (Int::GetBase16, secp256k1/Int.cpp:1019-1055)
-std::string u_hex(const U &a) {
-  static const char *H = "0123456789abcdef";
-  std::string s;
-  bool lead = true;
-  for (int i = 4; i >= 0; i--)
-    for (int j = 60; j >= 0; j -= 4) {
-      int d = (int)((a.v[i] >> j) & 15);
-      if (lead && d == 0) continue;
-      lead = false;
-      s += H[d];
-    }
-  return s.empty() ? "0" : s;
-}
-std::string u_dec(const U &a) {
-  if (u_is_zero(a)) return "0";
-  std::string s;
-  U x = a;
-  while (!u_is_zero(x)) {
-    uint64_t r;
-    x = u_divmod_u64(x, 10, &r);
-    s += (char)('0' + r);
-  }
-  std::reverse(s.begin(), s.end());
-  return s;
-}
-void u_to_be32(const U &a, uint8_t b[32]) {
-  for (int i = 0; i < 4; i++)
-    for (int j = 0; j < 8; j++) b[(3 - i) * 8 + j] = (uint8_t)(a.v[i] >> (56 - 8 * j));
-}
-U u_from_be32(const uint8_t b[32]) {
-  U r;
-  for (int i = 0; i < 4; i++) {
-    uint64_t w = 0;
-    for (int j = 0; j < 8; j++) w = (w << 8) | b[(3 - i) * 8 + j];
-    r.v[i] = w;
-  }
-  return r;
-}
-const char *ORDER_HEX = "FFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141";
 
 // ---------------------------------------------------------------------------------------------
 // hashing / encoding for hit output
@@ -270,29 +117,6 @@ bool b58dec25(const char *s, uint8_t out[25]) {
   for (size_t i = 0; i < buf.size(); i++) out[zeros + i] = buf[buf.size() - 1 - i];
   return true;
 }
-std::string hex(const uint8_t *b, int n) {
-  static const char *H = "0123456789abcdef";
-  std::string s;
-  for (int i = 0; i < n; i++) {
-    s += H[b[i] >> 4];
-    s += H[b[i] & 15];
-  }
-  return s;
-}
-bool is_hex(const char *s) {
-  for (; *s; s++)
-    if (!strchr("0123456789abcdefABCDEF", *s)) return false;
-  return true;
-}
-bool hex2bin(const char *s, uint8_t *out, size_t n) {
-  if (strlen(s) < 2 * n) return false;
-  for (size_t i = 0; i < n; i++) {
-    unsigned v;
-    if (sscanf(s + 2 * i, "%2x", &v) != 1) return false;
-    out[i] = (uint8_t)v;
-  }
-  return true;
-}
 std::string rmd_to_address(const uint8_t h[20]) {
   uint8_t d[25], c1[32], c2[32];
   d[0] = 0;
@@ -302,14 +126,6 @@ std::string rmd_to_address(const uint8_t h[20]) {
   memcpy(d + 21, c2, 4);
   return b58enc(d, 25);
 }
-void trim(char *s) {
-  size_t n = strlen(s);
-  while (n && strchr(" \t\r\n", s[n - 1])) s[--n] = 0;
-  size_t i = 0;
-  while (s[i] && strchr(" \t\r\n", s[i])) i++;
-  if (i) memmove(s, s + i, n - i + 1);
-}
-
 // ---------------------------------------------------------------------------------------------
 // options and shared state
 // ---------------------------------------------------------------------------------------------
@@ -448,59 +264,6 @@ bool read_targets(const char *fn, int mode, std::vector<uint8_t> &rows, uint64_t
   return true;
 }
 
-bool parse_pubkey(const char *s, fe &x, fe &y, bool &compressed) {
-  size_t n = strlen(s);
-  uint8_t raw[65];
-  if (n == 66 && (s[0] == '0' && (s[1] == '2' || s[1] == '3'))) {
-    if (!hex2bin(s + 2, raw, 32)) return false;
-    fe_from_be(x, raw);
-    fe t, s3, seven;
-    fe_sqr(t, x);
-    fe_mul(t, t, x);
-    fe_set_u32(seven, 7);
-    fe_add(s3, t, seven);
-    if (!fe_sqrt(y, s3)) return false;
-    uint32_t odd = s[1] == '3';
-    if ((y.d[0] & 1) != odd) fe_neg(y, y);
-    compressed = true;
-    return true;
-  }
-  if (n == 130 && s[0] == '0' && s[1] == '4') {
-    if (!hex2bin(s + 2, raw, 64)) return false;
-    fe_from_be(x, raw);
-    fe_from_be(y, raw + 32);
-    compressed = false;
-    return true;
-  }
-  return false;
-}
-
-// validate_nk (util.c:358-389)
-bool validate_nk(uint64_t n, uint64_t k) {
-  if (n < (1ULL << 20)) {
-    fprintf(stderr, "[E] n must be at least 2^20 (0x100000)\n");
-    return false;
-  }
-  if (n & (n - 1)) {
-    fprintf(stderr, "[E] n must be a power of two\n");
-    return false;
-  }
-  int bits = 0;
-  for (uint64_t t = n; t > 1; t >>= 1) bits++;
-  if (bits % 2 || bits < 20 || bits > 64) {
-    fprintf(stderr, "[E] invalid n 0x%llx\n", (unsigned long long)n);
-    return false;
-  }
-  uint64_t kmax = 1ULL << ((bits - 20) / 2 * 1);
-  // table: {20,1},{22,2},{24,4},... k_max doubles every 2 bits
-  kmax = 1ULL << ((bits - 20) / 2);
-  if (k > kmax) {
-    fprintf(stderr, "[E] k value %llu is too large for n 0x%llx (max %llu)\n", (unsigned long long)k,
-            (unsigned long long)n, (unsigned long long)kmax);
-    return false;
-  }
-  return true;
-}
 
 // ---------------------------------------------------------------------------------------------
 // stats (keyhunt.cpp:2850-2962)

@@ -49,7 +49,7 @@ def test_cli_rejects_out_of_scope_and_bad_nk(tmp_path):
     r = subprocess.run([cli, "-m", "bsgs", "-f", "x", "-k", "5000", "-b", "66"], capture_output=True, text=True)
     assert r.returncode == 1 and "too large" in r.stderr
     r = subprocess.run([cli, "-m", "address", "-f", "x", "-S"], capture_output=True, text=True)
-    assert r.returncode == 1
+    assert r.returncode == 1   # -S is accepted, the missing target file is not
     r = subprocess.run([cli, "-m", "bsgs", "-f", "x", "-B", "ggsb"], capture_output=True, text=True)
     assert r.returncode == 1 and "ggsb" in r.stderr
     # keyhunt.cpp:1185-1193 test the -B index against MODE_BSGS: -B both + -e / -I fail in any mode
@@ -57,3 +57,17 @@ def test_cli_rejects_out_of_scope_and_bad_nk(tmp_path):
     assert r.returncode == 1 and "Endomorphism doesn't work with BSGS" in r.stderr
     r = subprocess.run([cli, "-m", "address", "-f", "x", "-B", "both", "-I", "3"], capture_output=True, text=True)
     assert r.returncode == 1 and "Stride doesn't work with BSGS" in r.stderr
+
+
+def test_bsgsd_rejects_bad_arguments_before_any_gpu_call():
+    d = os.path.join(E.PKG, "bin", "bsgsd-amd")
+    if not os.path.exists(d):
+        pytest.skip("bsgsd-amd not built")
+    r = subprocess.run([d, "-n", "0x10000"], capture_output=True, text=True)
+    assert r.returncode == 1 and "n must be at least 2^20" in r.stderr
+    r = subprocess.run([d, "-n", "0x1000000", "-k", "5"], capture_output=True, text=True)
+    assert r.returncode == 1 and "too large" in r.stderr
+    r = subprocess.run([d, "-B", "random"], capture_output=True, text=True)
+    assert r.returncode == 1 and "sequentially" in r.stderr
+    r = subprocess.run([d, "-h"], capture_output=True, text=True)
+    assert r.returncode == 0 and "usage" in r.stdout
