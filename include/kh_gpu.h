@@ -46,6 +46,8 @@ extern "C" {
 /* scan modes (-m) and search kinds (-l) */
 #define KH_MODE_ADDRESS 0  /* -m address / -m rmd160: hash160 probes */
 #define KH_MODE_XPOINT 1   /* -m xpoint: X[0..20) probes */
+#define KH_MODE_ETH 2      /* -m address|rmd160 -c eth: Keccak-256(X||Y)[12..32) probes (the search kind is
+                              ignored; keyhunt.cpp:3524-3548, 3703-3760, 5663-5669); not with KH_MODE_ENDO */
 #define KH_MODE_ENDO 0x10  /* OR into the mode: -e, also probe (beta*X, Y) and (beta^2*X, Y), i.e. keys
                               lambda*k and lambda^2*k (keyhunt.cpp:3408-3440, 3476-3830) */
 #define KH_SEARCH_COMPRESS 0
@@ -64,6 +66,7 @@ extern "C" {
 #define KH_KIND_03 1       /* hash160(03||X) matched */
 #define KH_KIND_04 2       /* hash160(04||X||Y) matched */
 #define KH_KIND_XPOINT 3   /* X[0..20) matched */
+#define KH_KIND_ETH 5      /* Ethereum address matched (key printed by writekeyeth) */
 /* with KH_MODE_ENDO, kind also carries the image and (for 04 hashes) the Y sign: */
 #define KH_KIND_ENDO1 0x10 /* matched on (beta*X, Y): key = lambda*k (+- as reported) */
 #define KH_KIND_ENDO2 0x20 /* matched on (beta^2*X, Y): key = lambda^2*k */

@@ -670,7 +670,7 @@ int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride_be[32], u
   if (!ctx || !start || !n_hits || (n_keys % (2 * KH_WALK_H)) || n_keys == 0) return KH_E_ARG;
   const bool endo = (mode & KH_MODE_ENDO) != 0;
   mode &= ~(uint32_t)KH_MODE_ENDO;
-  if (mode > KH_MODE_XPOINT || search > KH_SEARCH_BOTH) return KH_E_ARG;
+  if (mode > KH_MODE_ETH || search > KH_SEARCH_BOTH || (mode == KH_MODE_ETH && endo)) return KH_E_ARG;
   if (!ctx->d_tbloom) return KH_E_STATE;
   (void)hipSetDevice(ctx->device);
   const int H = KH_WALK_H;
@@ -706,6 +706,7 @@ int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride_be[32], u
   if (r) return r;
 
   int km = mode == KH_MODE_XPOINT ? KM_XPOINT
+         : mode == KH_MODE_ETH ? KM_ETH
          : search == KH_SEARCH_COMPRESS ? KM_H160C
          : search == KH_SEARCH_UNCOMPRESS ? KM_H160U
                                           : KM_H160B;
@@ -779,6 +780,8 @@ int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride_be[32], u
       compressed = true;
     } else if (base == KH_KIND_04) {
       hash160_uncomp(xe, ye, w);
+    } else if (base == KH_KIND_ETH) {
+      eth_address(P.x, P.y, w);
     } else {
       for (int j = 0; j < 5; j++) w[j] = bswap32(xe.d[7 - j]);
     }

@@ -48,11 +48,12 @@ enum kh_walk_mode {
   KM_DUMP = 6,    // X/Y dump (parity tests)
   KM_BSGSB = 7,   // giant steps against the blocked layer-1 bloom (one 16-B block per probe)
   KM_BUILDB = 8,  // baby-step build with the blocked layer-1 bloom
+  KM_ETH = 9,     // Keccak-256(X||Y)[12..32): Ethereum address -> target bloom (-c eth)
   // flag on KM_H160C/U/B and KM_XPOINT: also probe the endomorphism images (beta*x, y) and
   // (beta^2*x, y), i.e. keys lambda*k and lambda^2*k (-e, keyhunt.cpp:3408-3440, 3476-3830)
   KM_ENDO = 16,
 };
-// device hit kinds: base kind (0: 02||X, 1: 03||X, 2: 04||X||Y, 3: xpoint, 4: bsgs) plus, with
+// device hit kinds: base kind (0: 02||X, 1: 03||X, 2: 04||X||Y, 3: xpoint, 4: bsgs, 5: eth) plus, with
 // KM_ENDO, the image e (0: X, 1: beta*X, 2: beta^2*X) << 4 and, for 04 hashes, the Y sign << 6
 #define KH_DKIND_ENDO_SHIFT 4
 #define KH_DKIND_NEG 0x40u

@@ -21,6 +21,7 @@
 //   KM_H160C / KM_H160U / KM_H160B  hash160 of 02/03||X, 04||X||Y or both -> 20-byte target bloom
 //                                    (thread_process, keyhunt.cpp:3475-3830)
 //   KM_XPOINT                        X[0..20) -> target bloom (keyhunt.cpp:3801-3824)
+//   KM_ETH                           Keccak-256(X||Y)[12..32) -> target bloom (-c eth, 3524-3760)
 //   KM_BSGS                          32-byte X -> bloom_bP[X[0]] (keyhunt.cpp:4819-4822)
 //   KM_BUILD                         baby X -> bloom layers 1/2/3 + bP rows (keyhunt.cpp:5394-5443)
 //   KM_BSGSB / KM_BUILDB             same with the BLOCKED layer-1 layout (kh_kernels.h): an item's
@@ -203,9 +204,21 @@ __device__ __forceinline__ void endo_beta(fe &b, int e) {
   for (int i = 0; i < 8; i++) b.d[i] = e == 1 ? B1[i] : B2[i];
 }
 
+// Ethereum address (Keccak-256 of X||Y, bytes 12..31); kind 5 (keyhunt.cpp:3524-3548, 3703-3760)
+__device__ __forceinline__ void probe_eth(const walk_args &A, const fe &x, const fe &y, uint64_t idx) {
+  uint32_t w[5];
+  eth_address(x, y, w);
+  uint64_t a = xxh64_20(w, KH_BLOOM_SEED);
+  if (bloom_probe_lazy(A.bloom, A.bd, a, [&](uint64_t s) { return xxh64_20(w, s); })) record_hit(A, idx, 5);
+}
+
 template <int MODE>
 __device__ __forceinline__ void probe_point(const walk_args &A, const fe &x, const fe &y, uint64_t idx) {
   if (idx >= A.n_points) return;
+  if constexpr (MODE == KM_ETH) {
+    probe_eth(A, x, y, idx);
+    return;
+  }
   constexpr int BASE = MODE & 15;
   constexpr bool ENDO = (MODE & KM_ENDO) != 0;
   if constexpr (BASE == KM_H160C || BASE == KM_H160B || BASE == KM_H160U || BASE == KM_XPOINT) {
@@ -369,7 +382,7 @@ __device__ __forceinline__ void probe_pair_bsgs(const walk_args &A, const fe &x1
 
 template <int MODE>
 constexpr bool needs_y() {
-  return (MODE & 15) == KM_H160U || (MODE & 15) == KM_H160B || MODE == KM_DUMP;
+  return (MODE & 15) == KM_H160U || (MODE & 15) == KM_H160B || MODE == KM_DUMP || MODE == KM_ETH;
 }
 
 }  // namespace
@@ -381,7 +394,8 @@ constexpr bool needs_y() {
 // 4 waves/SIMD even with a few spills; the hash160 modes prefer 3).
 template <int MODE>
 constexpr int walk_lb() {
-  return ((MODE & 15) == KM_H160C || (MODE & 15) == KM_H160U || (MODE & 15) == KM_H160B) ? KH_WALK_LB_HASH
+  return ((MODE & 15) == KM_H160C || (MODE & 15) == KM_H160U || (MODE & 15) == KM_H160B || MODE == KM_ETH)
+             ? KH_WALK_LB_HASH
          : MODE == KM_DUMP                                          ? 2
                                                                     : KH_WALK_LB;
 }
@@ -788,6 +802,7 @@ hipError_t launch_walk(int mode, const walk_args &A, hipStream_t st) {
     case KM_DUMP: hipLaunchKernelGGL(k_walk<KM_DUMP>, grid, block, 0, st, A); break;
     case KM_BSGSB: hipLaunchKernelGGL(k_walk<KM_BSGSB>, grid, block, 0, st, A); break;
     case KM_BUILDB: hipLaunchKernelGGL(k_walk<KM_BUILDB>, grid, block, 0, st, A); break;
+    case KM_ETH: hipLaunchKernelGGL(k_walk<KM_ETH>, grid, block, 0, st, A); break;
     case KM_H160C | KM_ENDO: hipLaunchKernelGGL(k_walk<KM_H160C | KM_ENDO>, grid, block, 0, st, A); break;
     case KM_H160U | KM_ENDO: hipLaunchKernelGGL(k_walk<KM_H160U | KM_ENDO>, grid, block, 0, st, A); break;
     case KM_H160B | KM_ENDO: hipLaunchKernelGGL(k_walk<KM_H160B | KM_ENDO>, grid, block, 0, st, A); break;

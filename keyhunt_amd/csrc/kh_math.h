@@ -15,6 +15,7 @@
 //   sha256 / ripemd160 ..... hash/sha256_sse.cpp:95-554, hash/ripemd160_sse.cpp:323-361
 //   hash160 packing ........ secp256k1/SECP256K1.cpp:974-1024 (04||X||Y), 1187-1250 (02/03||X)
 //   xxh64 .................. xxhash/xxhash.h:2290-2529 (v0.8.0)
+//   keccak-256 / eth ....... sha3/sha3.c (KECCAK_256_Final), keyhunt.cpp:5647-5669
 //   bloom probe/add ........ bloom/bloom.cpp:122-146, 189-212
 #pragma once
 #include <stdint.h>
@@ -770,6 +771,70 @@ KH_HD uint64_t xxh64_20(const uint32_t w[5], uint64_t seed) {
   h ^= (uint64_t)w[4] * KH_XP1;
   h = rotl64(h, 23) * KH_XP2 + KH_XP3;
   return xxh_avalanche(h);
+}
+
+// ------------------------------------------------------------------------------------------
+// Keccak-256 with the original 0x01 padding (sha3/sha3.c:229, KECCAK_256_Final) of the 64-byte
+// X||Y: the Ethereum address is digest bytes 12..31 (generate_binaddress_eth, keyhunt.cpp:5663-5669).
+// ------------------------------------------------------------------------------------------
+KH_HD void keccak_f1600(uint64_t a[25]) {
+  const uint64_t RC[24] = {0x0000000000000001ULL, 0x0000000000008082ULL, 0x800000000000808aULL, 0x8000000080008000ULL,
+                           0x000000000000808bULL, 0x0000000080000001ULL, 0x8000000080008081ULL, 0x8000000000008009ULL,
+                           0x000000000000008aULL, 0x0000000000000088ULL, 0x0000000080008009ULL, 0x000000008000000aULL,
+                           0x000000008000808bULL, 0x800000000000008bULL, 0x8000000000008089ULL, 0x8000000000008003ULL,
+                           0x8000000000008002ULL, 0x8000000000000080ULL, 0x000000000000800aULL, 0x800000008000000aULL,
+                           0x8000000080008081ULL, 0x8000000000008080ULL, 0x0000000080000001ULL, 0x8000000080008008ULL};
+  // rho rotation and pi destination of lane 1, 10, 7, ... (the standard walk of the 24 lanes)
+  const int ROT[24] = {1, 3, 6, 10, 15, 21, 28, 36, 45, 55, 2, 14, 27, 41, 56, 8, 25, 43, 62, 18, 39, 61, 20, 44};
+  const int PI[24] = {10, 7, 11, 17, 18, 3, 5, 16, 8, 21, 24, 4, 15, 23, 19, 13, 12, 2, 20, 14, 22, 9, 6, 1};
+#pragma unroll 1
+  for (int r = 0; r < 24; r++) {
+    uint64_t c[5];
+#pragma unroll
+    for (int x = 0; x < 5; x++) c[x] = a[x] ^ a[x + 5] ^ a[x + 10] ^ a[x + 15] ^ a[x + 20];
+#pragma unroll
+    for (int x = 0; x < 5; x++) {
+      const uint64_t d = c[(x + 4) % 5] ^ ((c[(x + 1) % 5] << 1) | (c[(x + 1) % 5] >> 63));
+#pragma unroll
+      for (int y = 0; y < 25; y += 5) a[y + x] ^= d;
+    }
+    uint64_t t = a[1];
+#pragma unroll
+    for (int i = 0; i < 24; i++) {
+      const uint64_t u = a[PI[i]];
+      a[PI[i]] = (t << ROT[i]) | (t >> (64 - ROT[i]));
+      t = u;
+    }
+#pragma unroll
+    for (int y = 0; y < 25; y += 5) {
+      const uint64_t b0 = a[y], b1 = a[y + 1], b2 = a[y + 2], b3 = a[y + 3], b4 = a[y + 4];
+      a[y] = b0 ^ (~b1 & b2);
+      a[y + 1] = b1 ^ (~b2 & b3);
+      a[y + 2] = b2 ^ (~b3 & b4);
+      a[y + 3] = b3 ^ (~b4 & b0);
+      a[y + 4] = b4 ^ (~b0 & b1);
+    }
+    a[0] ^= RC[r];
+  }
+}
+// Ethereum address of (x, y) as 5 LE u32 words = its 20 bytes in order
+KH_HD void eth_address(const fe &x, const fe &y, uint32_t out[5]) {
+  uint64_t a[25];
+#pragma unroll
+  for (int i = 0; i < 25; i++) a[i] = 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {  // the 32 big-endian bytes of X, then of Y, as LE u64 lanes
+    a[k] = (uint64_t)bswap32(x.d[7 - 2 * k]) | ((uint64_t)bswap32(x.d[6 - 2 * k]) << 32);
+    a[4 + k] = (uint64_t)bswap32(y.d[7 - 2 * k]) | ((uint64_t)bswap32(y.d[6 - 2 * k]) << 32);
+  }
+  a[8] = 0x01ULL;                  // padding: 0x01 after the 64 message bytes ...
+  a[16] = 0x8000000000000000ULL;   // ... and 0x80 in the last byte of the 136-byte rate
+  keccak_f1600(a);
+  out[0] = (uint32_t)(a[1] >> 32);
+  out[1] = (uint32_t)a[2];
+  out[2] = (uint32_t)(a[2] >> 32);
+  out[3] = (uint32_t)a[3];
+  out[4] = (uint32_t)(a[3] >> 32);
 }
 
 // ------------------------------------------------------------------------------------------

@@ -17,10 +17,10 @@ REPO = os.path.dirname(PKG)
 LIB_PATH = os.environ.get("KH_LIB") or os.path.join(PKG, "lib", "libkh_gpu.so")
 HEADER = os.path.join(REPO, "include", "kh_gpu.h")
 
-KH_MODE_ADDRESS, KH_MODE_XPOINT = 0, 1
+KH_MODE_ADDRESS, KH_MODE_XPOINT, KH_MODE_ETH = 0, 1, 2
 KH_MODE_ENDO = 0x10  # OR into mode: -e
 KH_SEARCH_COMPRESS, KH_SEARCH_UNCOMPRESS, KH_SEARCH_BOTH = 0, 1, 2
-KH_KIND_02, KH_KIND_03, KH_KIND_04, KH_KIND_XPOINT = 0, 1, 2, 3
+KH_KIND_02, KH_KIND_03, KH_KIND_04, KH_KIND_XPOINT, KH_KIND_ETH = 0, 1, 2, 3, 5
 KH_KIND_ENDO1, KH_KIND_ENDO2, KH_KIND_NEGY = 0x10, 0x20, 0x40
 TIME_ADDRESS, TIME_XPOINT, TIME_BSGS, TIME_BUILD, TIME_SETUP = 0, 1, 2, 3, 4
 KH_LAYER1_REFERENCE, KH_LAYER1_BLOCKED = 0, 1

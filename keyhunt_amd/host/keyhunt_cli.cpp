@@ -7,8 +7,9 @@
 // Sequential scans consume the range in whole N_SEQUENTIAL_MAX chunks (keyhunt.cpp:3314-3330) and
 // BSGS in whole 2N bases (keyhunt.cpp:4600-4617), exactly as the reference's cursors do.
 // BSGS base schedules -B sequential|backward|both|random|dance|angrygiant and random chunks (-R)
-// follow the reference's cursors (see take_bases).  -e (address/rmd160/xpoint) and -S / -6 (BSGS table
-// files in the reference's formats) are provided; -B ggsb, vanity, minikeys and ETH are rejected.
+// follow the reference's cursors (see take_bases).  -e (address/rmd160/xpoint), -c eth (address/rmd160)
+// and -S / -6 (BSGS table files in the reference's formats) are provided; -B ggsb, vanity and minikeys
+// are rejected.
 #include <getopt.h>
 #include <pthread.h>
 #include <stdint.h>
@@ -150,6 +151,7 @@ struct options {
   bool endo = false;    // -e
   bool stride_set = false;
   int bsgs_mode = 0;    // -B, index into BSGS_MODES
+  bool eth = false;            // -c eth (keyhunt.cpp:874-891)
   bool save_read = false;      // -S: read the table files if present, else build and write them
   bool skip_checksum = false;  // -6
 } opt;
@@ -201,9 +203,64 @@ void writekey(kh_ctx *ctx, bool compressed, const uint8_t key[32]) {
   fflush(stdout);
 }
 
+// keyhunt.cpp:6925-6950: Ethereum hits
+void writekeyeth(kh_ctx *ctx, const uint8_t key[32]) {
+  uint8_t xy[64];
+  kh_pubkeys(ctx, key, 1, xy);
+  fe x, y;
+  fe_from_be(x, xy);
+  fe_from_be(y, xy + 32);
+  uint32_t w[5];
+  eth_address(x, y, w);
+  uint8_t a[20];
+  memcpy(a, w, 20);
+  const std::string k = u_hex(u_from_be32(key)), addr = "0x" + hex(a, 20);
+  std::lock_guard<std::mutex> lk(g_keys_mtx);
+  FILE *f = fopen("KEYFOUNDKEYFOUND.txt", "a+");
+  if (f) {
+    fprintf(f, "Private Key: %s\naddress: %s\n", k.c_str(), addr.c_str());
+    fclose(f);
+  }
+  printf("\n Hit!!!! Private Key: %s\naddress: %s\n", k.c_str(), addr.c_str());
+  fflush(stdout);
+}
+
 // ---------------------------------------------------------------------------------------------
 // target files
 // ---------------------------------------------------------------------------------------------
+// forceReadFileAddressEth (keyhunt.cpp:7312-7384): 40 hex digits, or 0x and 40 hex digits
+bool read_targets_eth(const char *fn, std::vector<uint8_t> &rows, uint64_t &bloom_items) {
+  FILE *f = fopen(fn, "r");
+  if (!f) {
+    fprintf(stderr, "[E] Error opening the file %s\n", fn);
+    return false;
+  }
+  char line[1024];
+  std::vector<std::string> lines;
+  uint64_t counted = 0;
+  while (fgets(line, sizeof line, f)) {
+    trim(line);
+    if (strlen(line) >= 40) counted++;
+    lines.push_back(line);
+  }
+  fclose(f);
+  bloom_items = counted;
+  printf("[+] Allocating memory for %llu elements: %.2f MB\n", (unsigned long long)counted,
+         (double)(counted * 20) / 1048576.0);
+  for (auto &ln : lines) {
+    uint8_t raw[20];
+    const size_t r = ln.size();
+    if (r == 40 && is_hex(ln.c_str()) && hex2bin(ln.c_str(), raw, 20)) {
+      rows.insert(rows.end(), raw, raw + 20);
+    } else if (r == 42 && is_hex(ln.c_str() + 2) && hex2bin(ln.c_str() + 2, raw, 20)) {
+      rows.insert(rows.end(), raw, raw + 20);
+    } else if (r >= 40) {
+      fprintf(stderr, "[I] Ommiting invalid line %s\n", ln.c_str());
+    }
+  }
+  return true;
+}
+
 // forceReadFileAddress (keyhunt.cpp:7239-7310) / forceReadFileXPoint (7392-7490)
 bool read_targets(const char *fn, int mode, std::vector<uint8_t> &rows, uint64_t &bloom_items) {
   FILE *f = fopen(fn, "r");
@@ -349,13 +406,20 @@ void addr_worker(addr_job *j) {
     u_to_be32(base, st_be);
     uint32_t nh = 0;
     r = kh_scan(ctx, st_be, stride_be, j->nseq,
-                (opt.mode == MODE_XPOINT ? KH_MODE_XPOINT : KH_MODE_ADDRESS) | (opt.endo ? KH_MODE_ENDO : 0),
+                opt.mode == MODE_XPOINT ? (KH_MODE_XPOINT | (opt.endo ? KH_MODE_ENDO : 0))
+                : (opt.eth && (opt.mode == MODE_ADDRESS || opt.mode == MODE_RMD160)) ? KH_MODE_ETH
+                      : (KH_MODE_ADDRESS | (opt.endo ? KH_MODE_ENDO : 0)),
                 (uint32_t)opt.search, hits.data(), (uint32_t)hits.size(), &nh);
     if (r) {
       fprintf(stderr, "[E] kh_scan: %s (%s)\n", kh_strerror(r), kh_last_error(ctx));
       break;
     }
-    for (uint32_t i = 0; i < nh; i++) writekey(ctx, hits[i].compressed != 0, hits[i].key);
+    for (uint32_t i = 0; i < nh; i++) {
+      if (hits[i].kind == KH_KIND_ETH)
+        writekeyeth(ctx, hits[i].key);
+      else
+        writekey(ctx, hits[i].compressed != 0, hits[i].key);
+    }
     g_groups_done += j->nseq / 1024;
   }
   j->rc = r;
@@ -658,9 +722,17 @@ int main(int argc, char **argv) {
         opt.skip_checksum = true;
         fprintf(stderr, "[W] Skipping checksums on files\n");
         break;
-      case 'c':
-        fprintf(stderr, "[E] -%c is outside the scope of this engine\n", c);
-        return EXIT_FAILURE;
+      case 'c':  // keyhunt.cpp:874-891
+        if (!strcmp(optarg, "btc")) {
+          opt.eth = false;
+        } else if (!strcmp(optarg, "eth")) {
+          opt.eth = true;
+          printf("[+] Setting search for ETH adddress.\n");
+        } else {
+          fprintf(stderr, "[E] Unknow crypto value %s\n", optarg);
+          return EXIT_FAILURE;
+        }
+        break;
       default: usage(argv[0]); return EXIT_FAILURE;
     }
   }
@@ -675,6 +747,10 @@ int main(int argc, char **argv) {
   if (!validate_nk(nk_n, opt.kfactor)) return EXIT_FAILURE;
   // keyhunt.cpp:1185-1193 compares the -B index with MODE_BSGS (2), i.e. these two guards fire
   // for -B both whatever -m is (SURVEY 8a parity note 7); BSGS itself ignores -e and -I
+  if (opt.eth && opt.endo && (opt.mode == MODE_ADDRESS || opt.mode == MODE_RMD160)) {
+    fprintf(stderr, "[E] -e with -c eth is not provided by this engine\n");
+    return EXIT_FAILURE;
+  }
   if (opt.bsgs_mode == BM_BOTH && opt.endo) {
     fprintf(stderr, "[E] Endomorphism doesn't work with BSGS\n");
     return EXIT_FAILURE;
@@ -729,7 +805,11 @@ int main(int argc, char **argv) {
     }
     printf("[+] N = %p\n", (void *)nseq);
     uint64_t items = 0;
-    if (!read_targets(opt.file, opt.mode, rows, items)) return EXIT_FAILURE;
+    if (opt.eth && opt.mode == MODE_ADDRESS) {
+      if (!read_targets_eth(opt.file, rows, items)) return EXIT_FAILURE;
+    } else if (!read_targets(opt.file, opt.mode, rows, items)) {
+      return EXIT_FAILURE;
+    }
     printf("[+] Sorting data ... done! %llu values were loaded and sorted\n", (unsigned long long)(rows.size() / 20));
     g_running = gpus;
     for (int d = 0; d < gpus; d++) {

@@ -455,6 +455,61 @@ uint64_t or_xxh64(const uint8_t *p, uint64_t len, uint64_t seed) {
 /* as double, bloom.h:43).                                                                     */
 /* ------------------------------------------------------------------------------------------ */
 #define BLOOM_SEED 0x59f2815b16f81798ULL
+/* Keccak-256, original 0x01 padding (sha3/sha3.c:229 KECCAK_256_Final; keyhunt.cpp:5647-5653) */
+static const uint64_t KEC_RC[24] = {
+    0x0000000000000001ULL, 0x0000000000008082ULL, 0x800000000000808aULL, 0x8000000080008000ULL,
+    0x000000000000808bULL, 0x0000000080000001ULL, 0x8000000080008081ULL, 0x8000000000008009ULL,
+    0x000000000000008aULL, 0x0000000000000088ULL, 0x0000000080008009ULL, 0x000000008000000aULL,
+    0x000000008000808bULL, 0x800000000000008bULL, 0x8000000000008089ULL, 0x8000000000008003ULL,
+    0x8000000000008002ULL, 0x8000000000000080ULL, 0x000000000000800aULL, 0x800000008000000aULL,
+    0x8000000080008081ULL, 0x8000000000008080ULL, 0x0000000080000001ULL, 0x8000000080008008ULL};
+/* the state as a 5x5 array a[x + 5y]; rho offsets r[x][y] and pi (x, y) -> (y, 2x + 3y) written out */
+static void keccak_f(uint64_t a[25]) {
+  static const int R[25] = {0, 1, 62, 28, 27, 36, 44, 6, 55, 20, 3, 10, 43, 25, 39, 41, 45, 15, 21, 8, 18, 2, 61, 56, 14};
+  for (int r = 0; r < 24; r++) {
+    uint64_t c[5], b[25];
+    for (int x = 0; x < 5; x++) c[x] = a[x] ^ a[x + 5] ^ a[x + 10] ^ a[x + 15] ^ a[x + 20];
+    for (int x = 0; x < 5; x++)
+      for (int y = 0; y < 5; y++) a[x + 5 * y] ^= c[(x + 4) % 5] ^ rotl64(c[(x + 1) % 5], 1);
+    for (int x = 0; x < 5; x++)
+      for (int y = 0; y < 5; y++) {
+        uint64_t v = a[x + 5 * y];
+        int rr = R[x + 5 * y];
+        b[y + 5 * ((2 * x + 3 * y) % 5)] = rr ? rotl64(v, rr) : v;
+      }
+    for (int x = 0; x < 5; x++)
+      for (int y = 0; y < 5; y++) a[x + 5 * y] = b[x + 5 * y] ^ (~b[(x + 1) % 5 + 5 * y] & b[(x + 2) % 5 + 5 * y]);
+    a[0] ^= KEC_RC[r];
+  }
+}
+void or_keccak256(const uint8_t *msg, uint64_t len, uint8_t out[32]) {
+  uint64_t a[25] = {0};
+  uint8_t blk[136];
+  uint64_t off = 0;
+  for (;;) {
+    uint64_t n = len - off < 136 ? len - off : 136;
+    memset(blk, 0, 136);
+    memcpy(blk, msg + off, n);
+    if (n < 136) {  /* last block: pad 0x01 ... 0x80 */
+      blk[n] ^= 0x01;
+      blk[135] ^= 0x80;
+    }
+    for (int i = 0; i < 17; i++) a[i] ^= rd64(blk + 8 * i);
+    keccak_f(a);
+    off += n;
+    if (n < 136) break;
+  }
+  for (int i = 0; i < 32; i++) out[i] = (uint8_t)(a[i / 8] >> (8 * (i % 8)));
+}
+/* generate_binaddress_eth (keyhunt.cpp:5663-5669): Keccak-256(X||Y) bytes 12..31 */
+void or_eth_address(const uint8_t x[32], const uint8_t y[32], uint8_t out[20]) {
+  uint8_t m[64], d[32];
+  memcpy(m, x, 32);
+  memcpy(m + 32, y, 32);
+  or_keccak256(m, 64, d);
+  memcpy(out, d + 12, 20);
+}
+
 int or_bloom_params(uint64_t entries, double error, uint64_t *bits, uint64_t *bytes, uint32_t *hashes) {
   if (entries < 1000 || error <= 0 || error >= 1) return 1;
   long double err = (long double)error;
@@ -711,7 +766,7 @@ static void *scan_groups(void *arg) {
   or_hit *hits = J->hits;
   const int cap = J->cap;
   int nh = 0;
-  int need_y = (search == 1 || search == 2);
+  int need_y = (search == 1 || search == 2 || mode == 2);
   int ne = endo ? 3 : 1;
   fe key, one = {{1, 0, 0, 0}};
   u256_add_u64(&key, &J->start, J->g0 * GRP);
@@ -725,6 +780,14 @@ static void *scan_groups(void *arg) {
       fe x0; fe_from_be(&x0, xs + t * 32);
       uint8_t xe[3][32];
       for (int e = 0; e < ne; e++) { fe v; fe_mul(&v, &x0, &END_BETA[e]); fe_to_be(xe[e], &v); }
+      if (mode == 2) {  /* -c eth (keyhunt.cpp:3524-3548, 3703-3760): the uncompressed point */
+        uint8_t ya[32], h[20];
+        memcpy(ya, ys + t * 32, 32);
+        or_eth_address(xs + t * 32, ya, h);
+        if (or_bloom_check(bf, bits, hashes, h, 20) && or_searchbinary(rows, n_rows, h, 20, 0))
+          push_hit(hits, cap, &nh, &kf, 0, 5);
+        continue;
+      }
       if (mode == 1) {  /* xpoint (keyhunt.cpp:3801-3824) */
         for (int e = 0; e < ne; e++)
           if (or_bloom_check(bf, bits, hashes, xe[e], 20) && or_searchbinary(rows, n_rows, xe[e], 20, 0)) {

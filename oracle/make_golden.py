@@ -47,6 +47,9 @@ E2E_RUNS = [
     ("address_endo_targets", ["-m", "address", "-f", "endo_addr.txt", "-r", "1:100000", "-n", "0x100000", "-e", "-t", "8"], 300),
     ("address_endo_targets_no_e", ["-m", "address", "-f", "endo_addr.txt", "-r", "1:100000", "-n", "0x100000", "-t", "8"], 300),
     ("xpoint_endo_targets", ["-m", "xpoint", "-f", "endo_x.txt", "-r", "1:100000", "-n", "0x100000", "-e", "-t", "8"], 300),
+    # -c eth: Keccak-256(X||Y)[12:32] targets (tests/golden/make_eth_targets.py)
+    ("address_eth_2p20", ["-m", "address", "-c", "eth", "-f", "eth_targets.txt", "-r", "1:100000", "-n", "0x100000", "-t", "8"], 300),
+    ("rmd160_eth_2p20", ["-m", "rmd160", "-c", "eth", "-f", "eth_targets.rmd", "-r", "1:100000", "-n", "0x100000", "-t", "8"], 300),
     ("bsgs_120_window", ["-m", "bsgs", "-f", "120.txt", "-r", "b10f22572c497a836e9d0000000000:b10f22572c497a836edd0000000000", "-t", "8"], 300),
     ("bsgs_125_window", ["-m", "bsgs", "-f", "125.txt", "-r", "1c533b6bb7f0804e0995fe0000000000:1c533b6bb7f0804e09963e0000000000", "-t", "8"], 300),
     ("bsgs_130_window", ["-m", "bsgs", "-f", "130.txt", "-r", "33e7665705359f04f28b8880000000000:33e7665705359f04f28b8c80000000000", "-t", "8"], 300),
@@ -114,6 +117,8 @@ def parse_keyfound(text: str) -> list[dict]:
         hits.append({"key": m.group(1), "pubkey": m.group(2), "address": m.group(3), "rmd160": m.group(4)})
     for m in re.finditer(r"Key found privkey ([0-9a-f]+)\nPublickey ([0-9a-f]+)", text):
         hits.append({"key": m.group(1), "pubkey": m.group(2)})
+    for m in re.finditer(r"Private Key: ([0-9a-f]+)\naddress: (0x[0-9a-f]+)\n", text):  # writekeyeth
+        hits.append({"key": m.group(1), "address": m.group(2)})
     return hits
 
 

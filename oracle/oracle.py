@@ -107,6 +107,19 @@ def hash160_uncomp(x: int, y: int) -> bytes:
     return out.raw
 
 
+def keccak256(msg: bytes) -> bytes:
+    out = ctypes.create_string_buffer(32)
+    lib().or_keccak256(msg, ctypes.c_uint64(len(msg)), out)
+    return out.raw
+
+
+def eth_address(x: int, y: int) -> bytes:
+    """generate_binaddress_eth (keyhunt.cpp:5663-5669): Keccak-256(X||Y)[12:32]."""
+    out = ctypes.create_string_buffer(20)
+    lib().or_eth_address(be32(x), be32(y), out)
+    return out.raw
+
+
 def h160_to_address(h: bytes) -> str:
     out = ctypes.create_string_buffer(64)
     lib().or_h160_to_address(h, out, 64)
@@ -180,6 +193,7 @@ class OrHit(ctypes.Structure):
 
 MODE_ADDRESS = 0   # address / rmd160 share the hash160 probe
 MODE_XPOINT = 1
+MODE_ETH = 2       # -c eth: Keccak-256(X||Y)[12:32] probes
 SEARCH_COMPRESS, SEARCH_UNCOMPRESS, SEARCH_BOTH = 0, 1, 2
 
 

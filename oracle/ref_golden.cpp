@@ -20,6 +20,7 @@
 #include "hash/sha256.h"
 #include "bloom/bloom.h"
 #include "xxhash/xxhash.h"
+#include "sha3/sha3.h"
 
 static uint64_t rng_state = 0x6b657968756e7421ULL;
 static uint64_t g_rnd() {  // splitmix64
@@ -248,6 +249,25 @@ int main() {
              sh[2].c_str(), sha_hex(tb.data(), tb.size()).c_str(), c == 2 ? "" : ",");
       for (int l = 0; l < 3; l++) for (int s = 0; s < 256; s++) bloom_free(&L[l][s]);
     }
+  }
+  printf("],\n");
+  // Ethereum addresses (generate_binaddress_eth, keyhunt.cpp:5663-5669): the reference's
+  // SHA3_256_Init / Update / KECCAK_256_Final (keyhunt.cpp:5647-5653) of the 64-byte X||Y
+  printf("\"eth\": [\n");
+  for (int i = 0; i < 40; i++) {
+    Int k;
+    if (i < 8) k.SetInt32((uint32_t)(i * 7919 + 1));
+    else rand_int(k);
+    Point P = secp->ComputePublicKey(&k);
+    uint8_t xy[64], d[32];
+    P.x.Get32Bytes(xy);
+    P.y.Get32Bytes(xy + 32);
+    SHA3_256_CTX ctx;
+    SHA3_256_Init(&ctx);
+    SHA3_256_Update(&ctx, xy, 64);
+    KECCAK_256_Final(d, &ctx);
+    printf("  {\"k\":\"%s\",\"xy\":\"%s\",\"keccak\":\"%s\",\"address\":\"%s\"}%s\n", ihex(k).c_str(),
+           hexs(xy, 64).c_str(), hexs(d, 32).c_str(), hexs(d + 12, 20).c_str(), i == 39 ? "" : ",");
   }
   printf("]\n}\n");
   return 0;

@@ -16,6 +16,8 @@ def parse_keyfound(text: str) -> list[dict]:
         hits.append({"key": m.group(1), "pubkey": m.group(2), "address": m.group(3), "rmd160": m.group(4)})
     for m in re.finditer(r"Key found privkey ([0-9a-f]+)\nPublickey ([0-9a-f]+)", text):
         hits.append({"key": m.group(1), "pubkey": m.group(2)})
+    for m in re.finditer(r"Private Key: ([0-9a-f]+)\naddress: (0x[0-9a-f]+)\n", text):  # writekeyeth
+        hits.append({"key": m.group(1), "address": m.group(2)})
     return sorted(hits, key=lambda h: int(h["key"], 16))
 
 

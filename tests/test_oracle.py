@@ -152,3 +152,12 @@ def test_searchbinary_is_membership(oracle):
         for _ in range(50):
             q = rng.getrandbits(160).to_bytes(20, "big")
             assert oracle.searchbinary(table, len(rows), q) == (q in set(rows))
+
+
+def test_oracle_keccak_and_eth_against_reference_vectors(oracle):
+    """The oracle's Keccak-256 / generate_binaddress_eth against the reference's (ref_golden "eth")."""
+    for v in VEC["eth"]:
+        x, y = oracle.pubkey(int(v["k"], 16))
+        assert (x.to_bytes(32, "big") + y.to_bytes(32, "big")).hex() == v["xy"]
+        assert oracle.keccak256(bytes.fromhex(v["xy"])).hex() == v["keccak"]
+        assert oracle.eth_address(x, y).hex() == v["address"]
