@@ -116,6 +116,13 @@ int kh_synchronize(kh_ctx *ctx);
  * count the reference sizes its bloom with (numberItems), 0 -> n.  Sorts the table, builds the
  * reference-layout bloom (bloom_init2(max(10000, items), 1e-6)) and uploads both. */
 int kh_set_targets(kh_ctx *ctx, const uint8_t *rows, uint64_t n, uint64_t bloom_items);
+/* -m vanity targets instead (addvanity / processOneVanity, keyhunt.cpp:6739-6866, 6970-7035):
+ * ranges = n x {A[20], B[20]} hash160 bounds (inclusive), probe_len = the prefix length the bloom
+ * keys on (vanity_rmd_minimun_bytes_check_length, 1..20), bloom_items = the reference's item count
+ * (vanity_rmd_total).  Following kh_scan calls in the hash160 modes report every point whose
+ * hash lies in a range (vanityrmdmatch, 6677-6703), with the same key resolution as -m address.
+ * kh_set_targets switches back to exact targets. */
+int kh_set_vanity(kh_ctx *ctx, const uint8_t *ranges, uint64_t n, uint32_t probe_len, uint64_t bloom_items);
 /* Scan keys start + i*stride, i in [0, n_keys) (n_keys a multiple of 1024; stride NULL -> 1).
  * Returns the confirmed hits in the order one reference thread prints them. */
 int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride[32], uint64_t n_keys, uint32_t mode,

@@ -159,13 +159,20 @@ void host_bloom_hash(const uint8_t *buf, int len, uint64_t &a, uint64_t &b) {
     }
     a = xxh64_32(in, KH_BLOOM_SEED);
     b = xxh64_32(in, a);
-  } else {
+  } else {  // 20 bytes, or a shorter hash160 prefix (vanity)
+    uint8_t p[20] = {0};
+    memcpy(p, buf, (size_t)std::min(len, 20));
     uint32_t w[5];
     for (int k = 0; k < 5; k++)
-      w[k] = (uint32_t)buf[4 * k] | ((uint32_t)buf[4 * k + 1] << 8) | ((uint32_t)buf[4 * k + 2] << 16) |
-             ((uint32_t)buf[4 * k + 3] << 24);
-    a = xxh64_20(w, KH_BLOOM_SEED);
-    b = xxh64_20(w, a);
+      w[k] = (uint32_t)p[4 * k] | ((uint32_t)p[4 * k + 1] << 8) | ((uint32_t)p[4 * k + 2] << 16) |
+             ((uint32_t)p[4 * k + 3] << 24);
+    if (len == 20) {
+      a = xxh64_20(w, KH_BLOOM_SEED);
+      b = xxh64_20(w, a);
+    } else {
+      a = xxh64_prefix(w, (uint32_t)len, KH_BLOOM_SEED);
+      b = xxh64_prefix(w, (uint32_t)len, a);
+    }
   }
 }
 void host_bloom_add(uint8_t *bf, const bloom_desc &d, const uint8_t *buf, int len) {
@@ -315,6 +322,10 @@ struct kh_ctx {
   // address targets
   std::vector<uint8_t> rows;  // sorted, 20 B each
   uint64_t n_rows = 0;
+  // vanity targets (kh_set_vanity): hash160 ranges [A, B] (40 B each), bloom keyed on A's prefix
+  bool vanity = false;
+  std::vector<uint8_t> v_ranges;
+  uint32_t probe_len = 20;
   bloom_desc tbd{};
   std::vector<uint8_t> h_tbloom;
   uint8_t *d_tbloom = nullptr;
@@ -655,9 +666,31 @@ int kh_set_targets(kh_ctx *ctx, const uint8_t *rows, uint64_t n, uint64_t bloom_
   ctx->rows.resize(n * 20);
   for (uint64_t i = 0; i < n; i++) memcpy(&ctx->rows[i * 20], v[i].data(), 20);
   ctx->n_rows = n;
+  ctx->vanity = false;
+  ctx->probe_len = 20;
+  ctx->v_ranges.clear();
   ctx->tbd = bloom_size(bloom_entries(bloom_items ? bloom_items : n));
   ctx->h_tbloom.assign(ctx->tbd.bytes, 0);
   for (uint64_t i = 0; i < n; i++) host_bloom_add(ctx->h_tbloom.data(), ctx->tbd, &ctx->rows[i * 20], 20);
+  (void)hipFree(ctx->d_tbloom);
+  ctx->d_tbloom = nullptr;
+  HIPCHK(ctx, hipMalloc(&ctx->d_tbloom, ctx->tbd.bytes + 4));
+  HIPCHK(ctx, hipMemcpy(ctx->d_tbloom, ctx->h_tbloom.data(), ctx->tbd.bytes, hipMemcpyHostToDevice));
+  return KH_OK;
+}
+
+int kh_set_vanity(kh_ctx *ctx, const uint8_t *ranges, uint64_t n, uint32_t probe_len, uint64_t bloom_items) {
+  if (!ctx || (!ranges && n) || probe_len == 0 || probe_len > 20) return KH_E_ARG;
+  (void)hipSetDevice(ctx->device);
+  ctx->v_ranges.assign(ranges, ranges + n * 40);
+  ctx->rows.clear();
+  ctx->n_rows = 0;
+  ctx->vanity = true;
+  ctx->probe_len = probe_len;
+  // processOneVanity / readFileVanity (keyhunt.cpp:6970-7035): bloom over A's first probe_len bytes
+  ctx->tbd = bloom_size(bloom_entries(bloom_items ? bloom_items : n));
+  ctx->h_tbloom.assign(ctx->tbd.bytes, 0);
+  for (uint64_t i = 0; i < n; i++) host_bloom_add(ctx->h_tbloom.data(), ctx->tbd, &ctx->v_ranges[i * 40], (int)probe_len);
   (void)hipFree(ctx->d_tbloom);
   ctx->d_tbloom = nullptr;
   HIPCHK(ctx, hipMalloc(&ctx->d_tbloom, ctx->tbd.bytes + 4));
@@ -725,11 +758,29 @@ int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride_be[32], u
   A.hit_count = ctx->d_hit_count;
   A.hits = ctx->d_hits;
   A.hit_cap = ctx->hit_cap;
-  HIPCHK(ctx, hipMemsetAsync(ctx->d_hit_count, 0, 4, ctx->stream));
-  r = run_walk(ctx, km, mode == KH_MODE_XPOINT ? 1 : 0, A, jg.gpl, 2);
-  if (r) return r;
+  A.probe_len = mode == KH_MODE_XPOINT || mode == KH_MODE_ETH ? 20 : ctx->probe_len;
   uint32_t nd = 0;
-  r = fetch_hits(ctx, nd);
+  for (;;) {
+    HIPCHK(ctx, hipMemsetAsync(ctx->d_hit_count, 0, 4, ctx->stream));
+    r = run_walk(ctx, km, mode == KH_MODE_XPOINT ? 1 : 0, A, jg.gpl, 2);
+    if (r) return r;
+    r = fetch_hits(ctx, nd);
+    if (r != KH_E_OVERFLOW) break;
+    // more bloom hits than the buffer holds (short vanity prefixes): grow it, redo the chunk
+    uint32_t need = 0;
+    HIPCHK(ctx, hipMemcpy(&need, ctx->d_hit_count, 4, hipMemcpyDeviceToHost));
+    uint64_t cap2 = ctx->hit_cap;
+    while (cap2 < need) cap2 *= 2;
+    if (cap2 > (1u << 26)) return KH_E_OVERFLOW;
+    (void)hipFree(ctx->d_hits);
+    ctx->d_hits = nullptr;
+    HIPCHK(ctx, hipMalloc(&ctx->d_hits, cap2 * sizeof(kh_dev_hit)));
+    ctx->hit_cap = (uint32_t)cap2;
+    A.hits = ctx->d_hits;
+    A.hit_cap = ctx->hit_cap;
+    r = run_setup(ctx, s, nullptr);  // the walk moved the lane centres on: start them again
+    if (r) return r;
+  }
   if (r) return r;
 
   // Confirm each bloom hit against the sorted table and resolve the key: parity fix-up
@@ -786,7 +837,15 @@ int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride_be[32], u
       for (int j = 0; j < 5; j++) w[j] = bswap32(xe.d[7 - j]);
     }
     memcpy(probe, w, 20);
-    if (!searchbinary(ctx->rows.data(), (int64_t)ctx->n_rows, probe, 20, 0)) continue;
+    if (ctx->vanity && base != KH_KIND_XPOINT && base != KH_KIND_ETH) {
+      // vanityrmdmatch (keyhunt.cpp:6677-6703): inside any [A, B] range
+      bool in = false;
+      for (size_t j = 0; j < ctx->v_ranges.size() && !in; j += 40)
+        in = memcmp(&ctx->v_ranges[j], probe, 20) <= 0 && memcmp(&ctx->v_ranges[j + 20], probe, 20) >= 0;
+      if (!in) continue;
+    } else if (!searchbinary(ctx->rows.data(), (int64_t)ctx->n_rows, probe, 20, 0)) {
+      continue;
+    }
     kh_hit o;
     memset(&o, 0, sizeof o);
     u256 kr = e ? sc_mul(k, LAMBDA[e]) : k;  // (beta^e x, y) = lambda^e * (x, y)

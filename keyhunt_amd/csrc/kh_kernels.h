@@ -79,7 +79,7 @@ struct walk_args {
   uint32_t *hit_count;
   kh_dev_hit *hits;
   uint32_t hit_cap;
-  uint32_t pad0;
+  uint32_t probe_len;  // hash160 modes: bytes of the hash the bloom keys on (20; vanity: the prefix length)
   // BSGS build
   uint8_t *bl1, *bl2, *bl3;
   kh::bloom_desc bd2, bd3;

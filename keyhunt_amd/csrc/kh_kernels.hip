@@ -155,6 +155,17 @@ __device__ __forceinline__ void x_bytes_u64(const fe &x, uint64_t in[4]) {
     in[k] = (uint64_t)bswap32(x.d[7 - 2 * k]) | ((uint64_t)bswap32(x.d[6 - 2 * k]) << 32);
 }
 
+// one 20-byte hash into the target bloom: the whole hash (address/rmd160), or its first
+// A.probe_len bytes (vanity prefixes, vanityrmdmatch keyhunt.cpp:6677-6703)
+__device__ __forceinline__ bool probe_h160(const walk_args &A, const uint32_t h[5]) {
+  if (A.probe_len == 20) {
+    const uint64_t a = xxh64_20(h, KH_BLOOM_SEED);
+    return bloom_probe_lazy(A.bloom, A.bd, a, [&](uint64_t s) { return xxh64_20(h, s); });
+  }
+  const uint64_t a = xxh64_prefix(h, A.probe_len, KH_BLOOM_SEED);
+  return bloom_probe_lazy(A.bloom, A.bd, a, [&](uint64_t s) { return xxh64_prefix(h, A.probe_len, s); });
+}
+
 // hash160(02||X) and hash160(03||X) of one x-coordinate into the target bloom; kinds 0/1 | tag
 __device__ __forceinline__ void probe_comp(const walk_args &A, const fe &x, uint64_t idx, uint32_t tag) {
 #if KH_HASH_PAIR
@@ -165,17 +176,14 @@ __device__ __forceinline__ void probe_comp(const walk_args &A, const fe &x, uint
     uint32_t h[5];
 #pragma unroll
     for (int q = 0; q < 5; q++) h[q] = k ? hh[1][q] : hh[0][q];
-    uint64_t a = xxh64_20(h, KH_BLOOM_SEED);
-    if (bloom_probe_lazy(A.bloom, A.bd, a, [&](uint64_t s) { return xxh64_20(h, s); })) record_hit(A, idx, k | tag);
+    if (probe_h160(A, h)) record_hit(A, idx, k | tag);
   }
 #else
 #pragma unroll 1
   for (uint32_t pfx = 2; pfx <= 3; pfx++) {
     uint32_t h[5];
     hash160_comp(x, pfx, h);
-    uint64_t a = xxh64_20(h, KH_BLOOM_SEED);
-    if (bloom_probe_lazy(A.bloom, A.bd, a, [&](uint64_t s) { return xxh64_20(h, s); }))
-      record_hit(A, idx, (pfx - 2) | tag);
+    if (probe_h160(A, h)) record_hit(A, idx, (pfx - 2) | tag);
   }
 #endif
 }
@@ -183,8 +191,7 @@ __device__ __forceinline__ void probe_comp(const walk_args &A, const fe &x, uint
 __device__ __forceinline__ void probe_uncomp(const walk_args &A, const fe &x, const fe &y, uint64_t idx, uint32_t tag) {
   uint32_t h[5];
   hash160_uncomp(x, y, h);
-  uint64_t a = xxh64_20(h, KH_BLOOM_SEED);
-  if (bloom_probe_lazy(A.bloom, A.bd, a, [&](uint64_t s) { return xxh64_20(h, s); })) record_hit(A, idx, 2 | tag);
+  if (probe_h160(A, h)) record_hit(A, idx, 2 | tag);
 }
 // X[0..20); kind 3 | tag
 __device__ __forceinline__ void probe_xpoint(const walk_args &A, const fe &x, uint64_t idx, uint32_t tag) {

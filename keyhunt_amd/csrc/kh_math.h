@@ -773,6 +773,38 @@ KH_HD uint64_t xxh64_20(const uint32_t w[5], uint64_t seed) {
   return xxh_avalanche(h);
 }
 
+// word i of w[5] without dynamic register indexing
+KH_HD uint32_t w5_at(const uint32_t w[5], uint32_t i) {
+  uint32_t v = w[0];
+  v = i == 1 ? w[1] : v;
+  v = i == 2 ? w[2] : v;
+  v = i == 3 ? w[3] : v;
+  v = i == 4 ? w[4] : v;
+  return v;
+}
+// XXH64 of the first len <= 20 bytes of 5 LE u32 words (XXH64 short-input path,
+// xxhash/xxhash.h:2468-2529): the vanity bloom hashes a hash160 prefix (keyhunt.cpp:6680)
+KH_HD uint64_t xxh64_prefix(const uint32_t w[5], uint32_t len, uint64_t seed) {
+  uint64_t h = seed + KH_XP5 + len;
+  uint32_t p = 0;
+  for (; p + 8 <= len; p += 8) {
+    const uint64_t k = (uint64_t)w5_at(w, p / 4) | ((uint64_t)w5_at(w, p / 4 + 1) << 32);
+    h ^= xxh_round(0, k);
+    h = rotl64(h, 27) * KH_XP1 + KH_XP4;
+  }
+  if (p + 4 <= len) {
+    h ^= (uint64_t)w5_at(w, p / 4) * KH_XP1;
+    h = rotl64(h, 23) * KH_XP2 + KH_XP3;
+    p += 4;
+  }
+  for (; p < len; p++) {
+    const uint64_t b = (w5_at(w, p / 4) >> (8 * (p % 4))) & 0xFFu;
+    h ^= b * KH_XP5;
+    h = rotl64(h, 11) * KH_XP1;
+  }
+  return xxh_avalanche(h);
+}
+
 // ------------------------------------------------------------------------------------------
 // Keccak-256 with the original 0x01 padding (sha3/sha3.c:229, KECCAK_256_Final) of the 64-byte
 // X||Y: the Ethereum address is digest bytes 12..31 (generate_binaddress_eth, keyhunt.cpp:5663-5669).

@@ -130,7 +130,7 @@ std::string rmd_to_address(const uint8_t h[20]) {
 // ---------------------------------------------------------------------------------------------
 // options and shared state
 // ---------------------------------------------------------------------------------------------
-enum { MODE_ADDRESS, MODE_RMD160, MODE_XPOINT, MODE_BSGS };
+enum { MODE_ADDRESS, MODE_RMD160, MODE_XPOINT, MODE_BSGS, MODE_VANITY };
 struct options {
   int mode = MODE_ADDRESS;
   const char *file = nullptr;
@@ -152,6 +152,7 @@ struct options {
   bool stride_set = false;
   int bsgs_mode = 0;    // -B, index into BSGS_MODES
   bool eth = false;            // -c eth (keyhunt.cpp:874-891)
+  vanity_set vanity;           // -m vanity targets (-v, -f)
   bool save_read = false;      // -S: read the table files if present, else build and write them
   bool skip_checksum = false;  // -6
 } opt;
@@ -225,9 +226,66 @@ void writekeyeth(kh_ctx *ctx, const uint8_t key[32]) {
   fflush(stdout);
 }
 
+// keyhunt.cpp:6705-6737: vanity hits
+void writevanitykey(kh_ctx *ctx, bool compressed, const uint8_t key[32]) {
+  uint8_t xy[64];
+  kh_pubkeys(ctx, key, 1, xy);
+  fe x, y;
+  fe_from_be(x, xy);
+  fe_from_be(y, xy + 32);
+  uint32_t hw[5];
+  std::string pub;
+  if (compressed) {
+    uint8_t pfx = (y.d[0] & 1) ? 3 : 2;
+    hash160_comp(x, pfx, hw);
+    pub = hex(&pfx, 1) + hex(xy, 32);
+  } else {
+    uint8_t pfx = 4;
+    hash160_uncomp(x, y, hw);
+    pub = hex(&pfx, 1) + hex(xy, 64);
+  }
+  uint8_t rmd[20];
+  memcpy(rmd, hw, 20);
+  const std::string addr = rmd_to_address(rmd), k = u_hex(u_from_be32(key));
+  std::lock_guard<std::mutex> lk(g_keys_mtx);
+  FILE *f = fopen("VANITYKEYFOUND.txt", "a+");
+  if (f) {
+    fprintf(f, "Vanity Private Key: %s\npubkey: %s\nAddress %s\nrmd160 %s\n", k.c_str(), pub.c_str(), addr.c_str(),
+            hex(rmd, 20).c_str());
+    fclose(f);
+  }
+  printf("\nVanity Private Key: %s\npubkey: %s\nAddress %s\nrmd160 %s\n", k.c_str(), pub.c_str(), addr.c_str(),
+         hex(rmd, 20).c_str());
+  fflush(stdout);
+}
+
 // ---------------------------------------------------------------------------------------------
 // target files
 // ---------------------------------------------------------------------------------------------
+// readFileVanity (keyhunt.cpp:6990-7035): base58 prefixes, one per line, added to the -v ones
+bool read_vanity(const char *fn) {
+  FILE *f = fn ? fopen(fn, "r") : nullptr;
+  if (f) {
+    char line[1024];
+    while (fgets(line, sizeof line, f)) {
+      trim(line);
+      const size_t len = strlen(line);
+      if (len > 0 && len < 36) {
+        if (is_base58(line))
+          addvanity(line, opt.vanity);
+        else
+          fprintf(stderr, "[E] the string \"%s\" is not valid Base58, omiting it\n", line);
+      }
+    }
+    fclose(f);
+  }
+  if (opt.vanity.targets == 0) {
+    fprintf(stderr, "[E] There aren't any vanity targets\n");
+    return false;
+  }
+  return true;
+}
+
 // forceReadFileAddressEth (keyhunt.cpp:7312-7384): 40 hex digits, or 0x and 40 hex digits
 bool read_targets_eth(const char *fn, std::vector<uint8_t> &rows, uint64_t &bloom_items) {
   FILE *f = fopen(fn, "r");
@@ -385,8 +443,12 @@ void addr_worker(addr_job *j) {
     g_running--;
     return;
   }
-  r = kh_set_targets(ctx, j->rows->data(), j->rows->size() / 20, j->bloom_items);
-  std::vector<kh_hit> hits(1 << 12);
+  if (opt.mode == MODE_VANITY)
+    r = kh_set_vanity(ctx, opt.vanity.ranges.data(), opt.vanity.ranges.size() / 40, (uint32_t)opt.vanity.min_bytes,
+                      opt.vanity.total);
+  else
+    r = kh_set_targets(ctx, j->rows->data(), j->rows->size() / 20, j->bloom_items);
+  std::vector<kh_hit> hits(1 << 16);
   uint8_t st_be[32], stride_be[32];
   u_to_be32(opt.stride, stride_be);
   const U span = u_mul_u64(opt.stride, j->nseq);
@@ -410,6 +472,11 @@ void addr_worker(addr_job *j) {
                 : (opt.eth && (opt.mode == MODE_ADDRESS || opt.mode == MODE_RMD160)) ? KH_MODE_ETH
                       : (KH_MODE_ADDRESS | (opt.endo ? KH_MODE_ENDO : 0)),
                 (uint32_t)opt.search, hits.data(), (uint32_t)hits.size(), &nh);
+    if (r == KH_E_OVERFLOW && nh > hits.size()) {  // a short vanity prefix: take them all
+      hits.resize(nh);
+      r = kh_scan(ctx, st_be, stride_be, j->nseq, KH_MODE_ADDRESS | (opt.endo ? KH_MODE_ENDO : 0),
+                  (uint32_t)opt.search, hits.data(), (uint32_t)hits.size(), &nh);
+    }
     if (r) {
       fprintf(stderr, "[E] kh_scan: %s (%s)\n", kh_strerror(r), kh_last_error(ctx));
       break;
@@ -417,6 +484,8 @@ void addr_worker(addr_job *j) {
     for (uint32_t i = 0; i < nh; i++) {
       if (hits[i].kind == KH_KIND_ETH)
         writekeyeth(ctx, hits[i].key);
+      else if (opt.mode == MODE_VANITY)
+        writevanitykey(ctx, hits[i].compressed != 0, hits[i].key);
       else
         writekey(ctx, hits[i].compressed != 0, hits[i].key);
     }
@@ -630,18 +699,18 @@ void usage(const char *p) {
 
 int main(int argc, char **argv) {
   printf("[+] Version %s\n", VERSION);
-  const char *mode_names[] = {"address", "rmd160", "xpoint", "bsgs"};
+  const char *mode_names[] = {"address", "rmd160", "xpoint", "bsgs", "vanity"};
   int c;
   U order;
   u_from_hex(ORDER_HEX, order);
-  while ((c = getopt(argc, argv, "m:f:l:r:b:k:n:t:g:qs:I:L:MRec:B:S6")) != -1) {
+  while ((c = getopt(argc, argv, "m:f:l:r:b:k:n:t:g:qs:I:L:MRec:B:S6v:")) != -1) {
     switch (c) {
       case 'm': {
         int m = -1;
-        for (int i = 0; i < 4; i++)
+        for (int i = 0; i < 5; i++)
           if (!strcmp(optarg, mode_names[i])) m = i;
         if (m < 0) {
-          fprintf(stderr, "[E] Unsupported mode %s (engine covers address, rmd160, xpoint, bsgs)\n", optarg);
+          fprintf(stderr, "[E] Unsupported mode %s (engine covers address, rmd160, xpoint, bsgs, vanity)\n", optarg);
           return EXIT_FAILURE;
         }
         opt.mode = m;
@@ -649,6 +718,16 @@ int main(int argc, char **argv) {
         break;
       }
       case 'f': opt.file = optarg; break;
+      case 'v':  // keyhunt.cpp:1083-1100
+        if (is_base58(optarg)) {
+          if (addvanity(optarg, opt.vanity) > 0)
+            printf("[+] Added Vanity search : %s\n", optarg);
+          else
+            printf("[+] Vanity search \"%s\" was NOT Added\n", optarg);
+        } else {
+          fprintf(stderr, "[+] The string \"%s\" is not Valid Base58\n", optarg);
+        }
+        break;
       case 'l':
         if (!strcmp(optarg, "compress")) opt.search = KH_SEARCH_COMPRESS;
         else if (!strcmp(optarg, "uncompress")) opt.search = KH_SEARCH_UNCOMPRESS;
@@ -737,7 +816,7 @@ int main(int argc, char **argv) {
     }
   }
   if (opt.mode == MODE_BSGS) printf("[+] Mode BSGS %s\n", BSGS_MODES[opt.bsgs_mode]);  // keyhunt.cpp:1209-1211
-  if (!opt.file) {
+  if (!opt.file && !(opt.mode == MODE_VANITY && opt.vanity.targets)) {
     fprintf(stderr, "[E] -f FILE is required\n");
     return EXIT_FAILURE;
   }
@@ -805,7 +884,9 @@ int main(int argc, char **argv) {
     }
     printf("[+] N = %p\n", (void *)nseq);
     uint64_t items = 0;
-    if (opt.eth && opt.mode == MODE_ADDRESS) {
+    if (opt.mode == MODE_VANITY) {
+      if (!read_vanity(opt.file)) return EXIT_FAILURE;
+    } else if (opt.eth && opt.mode == MODE_ADDRESS) {
       if (!read_targets_eth(opt.file, rows, items)) return EXIT_FAILURE;
     } else if (!read_targets(opt.file, opt.mode, rows, items)) {
       return EXIT_FAILURE;

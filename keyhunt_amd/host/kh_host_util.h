@@ -11,6 +11,7 @@
 #include <mutex>
 #include <random>
 #include <string>
+#include <vector>
 
 #include "../csrc/kh_math.h"
 
@@ -230,6 +231,101 @@ inline bool parse_pubkey(const char *s, fe &x, fe &y, bool &compressed) {
     return true;
   }
   return false;
+}
+
+// ---------------------------------------------------------------------------------------------
+// vanity targets
+// ---------------------------------------------------------------------------------------------
+// b58tobin (base58/base58.c, libbase58): big-endian into *binszp bytes with 32-bit limbs, false on
+// an invalid digit or overflow (then *binszp is unchanged); else *binszp = the canonical length
+// (binsz - leading zero bytes + leading '1's)
+inline bool b58tobin_ref(uint8_t *bin, size_t *binszp, const char *b58, size_t b58sz) {
+  static const char *D = "123456789ABCDEFGHJKLMNPQRSTUVWXYZabcdefghijkmnopqrstuvwxyz";
+  const size_t binsz = *binszp;
+  const size_t outisz = (binsz + 3) / 4;
+  std::vector<uint32_t> outi(outisz ? outisz : 1, 0);
+  const unsigned bytesleft = binsz % 4;
+  const uint32_t zeromask = bytesleft ? (uint32_t)(0xFFFFFFFFull << (bytesleft * 8)) : 0;
+  unsigned zerocount = 0;
+  size_t i = 0;
+  for (; i < b58sz && b58[i] == '1'; ++i) ++zerocount;
+  for (; i < b58sz; ++i) {
+    const char *pos = ((unsigned char)b58[i] & 0x80) ? nullptr : strchr(D, b58[i]);
+    if (!pos || !b58[i]) return false;
+    uint32_t c = (uint32_t)(pos - D);
+    for (size_t j = outisz; j--;) {
+      const uint64_t t = (uint64_t)outi[j] * 58 + c;
+      c = (uint32_t)(t >> 32);
+      outi[j] = (uint32_t)t;
+    }
+    if (c || (outi[0] & zeromask)) return false;
+  }
+  uint8_t *b = bin;
+  size_t j = 0;
+  if (bytesleft) {
+    for (unsigned q = bytesleft; q > 0; --q) *(b++) = (uint8_t)(outi[0] >> (8 * (q - 1)));
+    ++j;
+  }
+  for (; j < outisz; ++j)
+    for (int q = 4; q > 0; --q) *(b++) = (uint8_t)(outi[j] >> (8 * (q - 1)));
+  for (i = 0; i < binsz; ++i) {
+    if (bin[i]) break;
+    --*binszp;
+  }
+  *binszp += zerocount;
+  return true;
+}
+
+inline bool is_base58(const char *s) {
+  for (; *s; s++)
+    if (!strchr("123456789ABCDEFGHJKLMNPQRSTUVWXYZabcdefghijkmnopqrstuvwxyz", *s)) return false;
+  return true;
+}
+
+// addvanity (keyhunt.cpp:6739-6866): the hash160 ranges [A_j, B_j] of the addresses that start
+// with `target` (padded with '1' for A, 'z' for B up to each 25-byte decoding length), appended to
+// `ranges` (40 bytes each); min_bytes tracks the common-prefix length the vanity bloom keys on.
+struct vanity_set {
+  std::vector<uint8_t> ranges;
+  uint64_t total = 0;      // vanity_rmd_total
+  int min_bytes = 999999;  // vanity_rmd_minimun_bytes_check_length
+  int targets = 0;
+};
+inline int addvanity(const char *target, vanity_set &v) {
+  const int targetsize = (int)strlen(target);
+  if (targetsize >= 30) return 0;
+  std::vector<std::vector<uint8_t>> side[2];
+  for (int sd = 0; sd < 2; sd++) {
+    char copy[50];
+    memset(copy, 0, 50);
+    memcpy(copy, target, (size_t)targetsize);
+    int stringsize = targetsize;
+    uint8_t raw[50];
+    memset(raw, 0, 50);
+    size_t len;
+    do {
+      len = 50;
+      b58tobin_ref(raw, &len, copy, (size_t)stringsize);
+      if (len < 25) copy[stringsize++] = sd ? 'z' : '1';
+      if (len == 25) {
+        b58tobin_ref(raw, &len, copy, (size_t)stringsize);
+        side[sd].push_back(std::vector<uint8_t>(raw + 1, raw + 21));
+        copy[stringsize++] = sd ? 'z' : '1';
+      }
+    } while (len <= 25 && stringsize < 50);
+  }
+  if (side[0].empty() || side[1].empty()) return 0;
+  const int r = (int)std::min(side[0].size(), side[1].size());
+  for (int j = 0; j < r; j++) {
+    int same = 0;
+    while (same < 20 && side[0][j][same] == side[1][j][same]) same++;
+    v.min_bytes = std::min(v.min_bytes, same);
+    v.ranges.insert(v.ranges.end(), side[0][j].begin(), side[0][j].end());
+    v.ranges.insert(v.ranges.end(), side[1][j].begin(), side[1][j].end());
+  }
+  v.total += (uint64_t)r;
+  v.targets++;
+  return r;
 }
 
 // validate_nk (util.c:358-389)

@@ -50,6 +50,12 @@ E2E_RUNS = [
     # -c eth: Keccak-256(X||Y)[12:32] targets (tests/golden/make_eth_targets.py)
     ("address_eth_2p20", ["-m", "address", "-c", "eth", "-f", "eth_targets.txt", "-r", "1:100000", "-n", "0x100000", "-t", "8"], 300),
     ("rmd160_eth_2p20", ["-m", "rmd160", "-c", "eth", "-f", "eth_targets.rmd", "-r", "1:100000", "-n", "0x100000", "-t", "8"], 300),
+    # -m vanity: base58 prefixes -> hash160 ranges (keyhunt.cpp:6739-6866), VANITYKEYFOUND.txt
+    ("vanity_2p20_compress", ["-m", "vanity", "-v", "1Kha", "-v", "1PUB", "-l", "compress", "-r", "1:100000", "-n", "0x100000", "-t", "8"], 300),
+    ("vanity_2p20_both", ["-m", "vanity", "-v", "1Kha", "-v", "1PUB", "-r", "1:100000", "-n", "0x100000", "-t", "8"], 300),
+    ("vanity_2p20_uncompress_endo", ["-m", "vanity", "-v", "1Kha", "-v", "1PUB", "-l", "uncompress", "-e", "-r", "1:100000", "-n", "0x100000", "-t", "8"], 300),
+    ("vanity_2p20_compress_endo", ["-m", "vanity", "-v", "1Kha", "-v", "1PUB", "-l", "compress", "-e", "-r", "1:100000", "-n", "0x100000", "-t", "8"], 300),
+    ("vanity_file_2p20", ["-m", "vanity", "-f", "vanity.txt", "-l", "compress", "-r", "1:100000", "-n", "0x100000", "-t", "8"], 300),
     ("bsgs_120_window", ["-m", "bsgs", "-f", "120.txt", "-r", "b10f22572c497a836e9d0000000000:b10f22572c497a836edd0000000000", "-t", "8"], 300),
     ("bsgs_125_window", ["-m", "bsgs", "-f", "125.txt", "-r", "1c533b6bb7f0804e0995fe0000000000:1c533b6bb7f0804e09963e0000000000", "-t", "8"], 300),
     ("bsgs_130_window", ["-m", "bsgs", "-f", "130.txt", "-r", "33e7665705359f04f28b8880000000000:33e7665705359f04f28b8c80000000000", "-t", "8"], 300),
@@ -113,8 +119,11 @@ def gen_vectors() -> None:
 
 def parse_keyfound(text: str) -> list[dict]:
     hits = []
-    for m in re.finditer(r"Private Key: ([0-9a-f]+)\npubkey: ([0-9a-f]+)\nAddress (\S+)\nrmd160 ([0-9a-f]+)", text):
-        hits.append({"key": m.group(1), "pubkey": m.group(2), "address": m.group(3), "rmd160": m.group(4)})
+    for m in re.finditer(r"(Vanity )?Private Key: ([0-9a-f]+)\npubkey: ([0-9a-f]+)\nAddress (\S+)\nrmd160 ([0-9a-f]+)", text):
+        h = {"key": m.group(2), "pubkey": m.group(3), "address": m.group(4), "rmd160": m.group(5)}
+        if m.group(1):
+            h["vanity"] = True
+        hits.append(h)
     for m in re.finditer(r"Key found privkey ([0-9a-f]+)\nPublickey ([0-9a-f]+)", text):
         hits.append({"key": m.group(1), "pubkey": m.group(2)})
     for m in re.finditer(r"Private Key: ([0-9a-f]+)\naddress: (0x[0-9a-f]+)\n", text):  # writekeyeth
@@ -133,8 +142,10 @@ def gen_e2e(only: list[str] | None = None) -> None:
             for fn in os.listdir(DATA):
                 shutil.copy(os.path.join(DATA, fn), td)
             p = subprocess.run(["timeout", str(tmo), REF_BIN] + argv + ["-q"], cwd=td, capture_output=True, text=True)
-            kf = os.path.join(td, "KEYFOUNDKEYFOUND.txt")
-            text = open(kf).read() if os.path.exists(kf) else ""
+            text = ""
+            for fn in ("KEYFOUNDKEYFOUND.txt", "VANITYKEYFOUND.txt"):
+                kf = os.path.join(td, fn)
+                text += open(kf).read() if os.path.exists(kf) else ""
             hits = parse_keyfound(text)
             results[name] = {"argv": argv, "exit": p.returncode, "hits": sorted(hits, key=lambda h: int(h["key"], 16)),
                              "stdout_hit_lines": [ln.strip() for ln in p.stdout.split("\n") if "Hit!" in ln or "Key found" in ln]}

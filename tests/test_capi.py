@@ -41,7 +41,7 @@ def test_cli_rejects_out_of_scope_and_bad_nk(tmp_path):
     cli = os.path.join(E.PKG, "bin", "keyhunt-amd")
     if not os.path.exists(cli):
         pytest.skip("CLI not built")
-    r = subprocess.run([cli, "-m", "vanity", "-f", "x"], capture_output=True, text=True)
+    r = subprocess.run([cli, "-m", "minikeys", "-f", "x"], capture_output=True, text=True)
     assert r.returncode == 1 and "Unsupported mode" in r.stderr
     r = subprocess.run([cli, "-m", "address", "-f", "x", "-r", "1:100000", "-n", "0x10000"], capture_output=True,
                        text=True)
@@ -57,6 +57,19 @@ def test_cli_rejects_out_of_scope_and_bad_nk(tmp_path):
     assert r.returncode == 1 and "Endomorphism doesn't work with BSGS" in r.stderr
     r = subprocess.run([cli, "-m", "address", "-f", "x", "-B", "both", "-I", "3"], capture_output=True, text=True)
     assert r.returncode == 1 and "Stride doesn't work with BSGS" in r.stderr
+
+
+def test_cli_vanity_and_eth_argument_checks(tmp_path):
+    cli = os.path.join(E.PKG, "bin", "keyhunt-amd")
+    if not os.path.exists(cli):
+        pytest.skip("CLI not built")
+    r = subprocess.run([cli, "-m", "vanity", "-r", "1:100000", "-v", "1Bitc0in", "-f", str(tmp_path / "none.txt")],
+                       capture_output=True, text=True)
+    assert 'The string "1Bitc0in" is not Valid Base58' in r.stderr and r.returncode == 1
+    r = subprocess.run([cli, "-m", "address", "-c", "doge", "-f", "x"], capture_output=True, text=True)
+    assert r.returncode == 1 and "Unknow crypto value doge" in r.stderr
+    r = subprocess.run([cli, "-m", "address", "-c", "eth", "-e", "-f", "x"], capture_output=True, text=True)
+    assert r.returncode == 1 and "-e with -c eth" in r.stderr
 
 
 def test_bsgsd_rejects_bad_arguments_before_any_gpu_call():
