@@ -28,14 +28,12 @@ static_assert(KH_WALK_H >= 64 && KH_WALK_H <= 512 && (512 % KH_WALK_H) == 0,
 
 // Blocked layer-1 bloom (KH_LAYER1_BLOCKED), a split-block filter: per shard X[0], `blocks` 16-byte
 // blocks, blocks = ceil(KH_BLK_BITS_MUL x reference bits / 128).  An item X (an x-coordinate, so
-// already uniform) uses its own words instead of a hash: with u = big-endian u32 of X[8..12) and
-// s_0 = big-endian u32 of X[12..16), the block is (u * blocks) >> 32, and the LCG
-// s_{t+1} = s_t*MUL + ADD (u32) gives three 5-bit fields per step, (s >> 27), (s >> 22) & 31,
-// (s >> 17) & 31; fields 4w..4w+3 are the bits set in little-endian u32 word w of the block
-// (w < 4).  An item is present iff every word covers its mask.  3x the reference's bits: FP 5.6e-7
-// (Poisson block load) vs the reference's 1e-6; one 16-byte load per probe and no XXH64.
-#define KH_BLK_LCG_MUL 0x9E3779B1u
-#define KH_BLK_LCG_ADD 0x7F4A7C15u
+// already uniform) uses its own bits instead of a hash: with u = big-endian u32 of X[8..12), the
+// block is (u * blocks) >> 32.  The 16 bit positions are 5-bit fields of the next 96 bits, taken
+// as big-endian u32s s0 = X[12..16), s1 = X[16..20), s2 = X[20..24): field f (f < 16) is
+// (s_{f/6} >> 5*(f%6)) & 31; fields 4w..4w+3 are the bits set in little-endian u32 word w of the
+// block (w < 4).  An item is present iff every word covers its mask.  3x the reference's bits:
+// FP 5.6e-7 (Poisson block load) vs the reference's 1e-6; one 16-byte load per probe, no hashing.
 #define KH_BLK_BITS_MUL 3
 
 enum kh_walk_mode {

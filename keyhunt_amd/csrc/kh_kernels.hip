@@ -108,32 +108,32 @@ __device__ __forceinline__ void bloom_insert(uint8_t *__restrict__ bf_base, uint
 
 
 // Blocked layer-1 (split-block) geometry, kh_kernels.h: desc.bits = blocks per shard.  The item
-// is an x-coordinate, already uniform, so the block and the seed are taken from its words directly
-// (no XXH64): block = (X[8..12) * blocks) >> 32, seed = X[12..16) (big-endian u32s = limbs 5, 4).
+// is an x-coordinate, already uniform, so the block and the bit positions are taken from its words
+// directly (no XXH64): block = (X[8..12) * blocks) >> 32 (limb 5); positions = 5-bit fields of
+// X[12..24) (limbs 4, 3, 2).
 __device__ __forceinline__ uint32_t blk_index(uint32_t w5, const bloom_desc &bd) {
   return (uint32_t)(((uint64_t)w5 * bd.bits) >> 32);
 }
-__device__ __forceinline__ void blk_masks(uint32_t s, uint32_t m[4]) {
-  uint32_t f[18];
+// masks of the four block words from s0 = limb 4, s1 = limb 3, s2 = limb 2.  `1u << (s >> k)`
+// is one v_lshrrev + one v_lshlrev: the hardware shift uses the low 5 bits of the amount.
+__device__ __forceinline__ void blk_masks(uint32_t s0, uint32_t s1, uint32_t s2, uint32_t m[4]) {
+  uint32_t f[16];
 #pragma unroll
-  for (int t = 0; t < 6; t++) {
-    s = s * KH_BLK_LCG_MUL + KH_BLK_LCG_ADD;
-    f[3 * t] = s >> 27;
-    f[3 * t + 1] = (s >> 22) & 31u;
-    f[3 * t + 2] = (s >> 17) & 31u;
+  for (int t = 0; t < 16; t++) {
+    const uint32_t s = t < 6 ? s0 : t < 12 ? s1 : s2;
+    f[t] = 1u << ((s >> (5 * (t % 6))) & 31u);
   }
 #pragma unroll
-  for (int w = 0; w < 4; w++)
-    m[w] = (1u << f[4 * w]) | (1u << f[4 * w + 1]) | (1u << f[4 * w + 2]) | (1u << f[4 * w + 3]);
+  for (int w = 0; w < 4; w++) m[w] = f[4 * w] | f[4 * w + 1] | f[4 * w + 2] | f[4 * w + 3];
 }
-__device__ __forceinline__ bool blk_match(const uint4 &v, uint32_t seed) {
+__device__ __forceinline__ bool blk_match(const uint4 &v, uint32_t s0, uint32_t s1, uint32_t s2) {
   uint32_t m[4];
-  blk_masks(seed, m);
+  blk_masks(s0, s1, s2, m);
   return ((v.x & m[0]) == m[0]) & ((v.y & m[1]) == m[1]) & ((v.z & m[2]) == m[2]) & ((v.w & m[3]) == m[3]);
 }
 __device__ __forceinline__ void blk_insert(uint8_t *__restrict__ bf_shard, const bloom_desc &bd, const fe &x) {
   uint32_t m[4];
-  blk_masks(x.d[4], m);
+  blk_masks(x.d[4], x.d[3], x.d[2], m);
   uint32_t *w = reinterpret_cast<uint32_t *>(bf_shard + (size_t)blk_index(x.d[5], bd) * 16);
 #pragma unroll
   for (int k = 0; k < 4; k++) atomicOr(&w[k], m[k]);
@@ -321,12 +321,12 @@ __device__ __forceinline__ uint4 ld_nt16(const uint4 *p) {
   v4u32 v = __builtin_nontemporal_load(reinterpret_cast<const v4u32 *>(p));
   return make_uint4(v.x, v.y, v.z, v.w);
 }
-// {global block index (shard*stride + block*16)/16, seed} of one point
-__device__ __forceinline__ uint2 blk_record(const walk_args &A, const fe &x) {
+// {global block index (shard*stride + block*16)/16, limbs 4, 3, 2} of one point
+__device__ __forceinline__ uint4 blk_record(const walk_args &A, const fe &x) {
   const uint64_t off = (uint64_t)(x.d[7] >> 24) * A.bd.stride + (uint64_t)blk_index(x.d[5], A.bd) * 16;
-  return make_uint2((uint32_t)(off >> 4), x.d[4]);
+  return make_uint4((uint32_t)(off >> 4), x.d[4], x.d[3], x.d[2]);
 }
-__device__ __forceinline__ uint4 blk_load(const walk_args &A, const uint2 &r) {
+__device__ __forceinline__ uint4 blk_load(const walk_args &A, const uint4 &r) {
 #ifdef KH_TIMING_NO_PROBE_LOADS
   // timing-only build: no HBM reads (outputs are wrong); isolates the probe's compute
   return make_uint4(r.x, r.x * 3u, r.x * 5u, r.x * 7u);
@@ -334,10 +334,11 @@ __device__ __forceinline__ uint4 blk_load(const walk_args &A, const uint2 &r) {
   return ld_nt16(reinterpret_cast<const uint4 *>(A.bloom) + r.x);
 #endif
 }
+__device__ __forceinline__ bool blk_match_rec(const uint4 &v, const uint4 &r) { return blk_match(v, r.y, r.z, r.w); }
 // one blocked probe, in place (the group centre)
 __device__ __forceinline__ void blk_probe(const walk_args &A, const fe &x, uint64_t idx) {
-  const uint2 r = blk_record(A, x);
-  if (idx < A.n_points && blk_match(blk_load(A, r), r.y)) record_hit(A, idx, 4);
+  const uint4 r = blk_record(A, x);
+  if (idx < A.n_points && blk_match_rec(blk_load(A, r), r)) record_hit(A, idx, 4);
 }
 
 // Reference-layout layer-1 probes of two giant-step points in lockstep (keyhunt.cpp:4819-4822
@@ -453,7 +454,7 @@ __global__ void __launch_bounds__(256, walk_lb<MODE>()) k_walk(walk_args A) {
     // backward: recover 1/dx_i and emit C - T[i] (offset -(i+1)) and C + T[i] (offset i+1).
     // Both points use the second operand (T.x, +-T.y): x3 = s^2 - C.x - T.x, y3 = s(T.x - x3) -+ T.y.
     // prefix[i-1] is fetched one iteration ahead so its HBM latency overlaps the previous pair
-    uint2 pm = make_uint2(0u, 0u), pp = make_uint2(0u, 0u);  // KM_BSGSB: previous pair's probe records
+    uint4 pm = make_uint4(0u, 0u, 0u, 0u), pp = make_uint4(0u, 0u, 0u, 0u);  // KM_BSGSB: previous pair's probe records
     uint64_t poff = 0;
     uint32_t plive = 0;
     fe pre;
@@ -491,8 +492,8 @@ __global__ void __launch_bounds__(256, walk_lb<MODE>()) k_walk(walk_args A) {
         fe_sqr(xp, s);
         fe_sub(xp, xp, cx);
         fe_sub(xp, xp, tx);
-        if ((plive & 1u) && blk_match(vm, pm.y)) record_hit(A, cidx - poff, 4);
-        if ((plive & 2u) && blk_match(vp, pp.y)) record_hit(A, cidx + poff, 4);
+        if ((plive & 1u) && blk_match_rec(vm, pm)) record_hit(A, cidx - poff, 4);
+        if ((plive & 2u) && blk_match_rec(vp, pp)) record_hit(A, cidx + poff, 4);
         const uint64_t off = (uint64_t)(i + 1);
         pm = blk_record(A, xm);
         pp = blk_record(A, xp);
@@ -539,8 +540,8 @@ __global__ void __launch_bounds__(256, walk_lb<MODE>()) k_walk(walk_args A) {
       }
     }
     if constexpr (MODE == KM_BSGSB) {  // the last pair of the group
-      if ((plive & 1u) && blk_match(blk_load(A, pm), pm.y)) record_hit(A, cidx - poff, 4);
-      if ((plive & 2u) && blk_match(blk_load(A, pp), pp.y)) record_hit(A, cidx + poff, 4);
+      if ((plive & 1u) && blk_match_rec(blk_load(A, pm), pm)) record_hit(A, cidx - poff, 4);
+      if ((plive & 2u) && blk_match_rec(blk_load(A, pp), pp)) record_hit(A, cidx + poff, 4);
     }
     // next centre C += T[H]  (keyhunt.cpp:3840-3855)
     {
@@ -778,10 +779,12 @@ __global__ void k_test_bloom(const uint8_t *items, uint32_t n, uint32_t len, con
   }
   const uint8_t *bf = bloom + (sharded ? (size_t)p[0] * bd.stride : 0);
   if (blocked) {
-    // X[8..12) and X[12..16) as big-endian u32s (limbs 5 and 4)
-    const uint32_t w5 = ((uint32_t)p[8] << 24) | ((uint32_t)p[9] << 16) | ((uint32_t)p[10] << 8) | p[11];
-    const uint32_t w4 = ((uint32_t)p[12] << 24) | ((uint32_t)p[13] << 16) | ((uint32_t)p[14] << 8) | p[15];
-    out[i] = blk_match(reinterpret_cast<const uint4 *>(bf)[blk_index(w5, bd)], w4) ? 1u : 0u;
+    // X[8..12), X[12..16), X[16..20), X[20..24) as big-endian u32s (limbs 5, 4, 3, 2)
+    uint32_t w[4];
+    for (int k = 0; k < 4; k++)
+      w[k] = ((uint32_t)p[8 + 4 * k] << 24) | ((uint32_t)p[9 + 4 * k] << 16) | ((uint32_t)p[10 + 4 * k] << 8) |
+             p[11 + 4 * k];
+    out[i] = blk_match(reinterpret_cast<const uint4 *>(bf)[blk_index(w[0], bd)], w[1], w[2], w[3]) ? 1u : 0u;
     return;
   }
   out[i] = bloom_probe(bf, bd, a, b) ? 1u : 0u;

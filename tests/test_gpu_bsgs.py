@@ -137,8 +137,8 @@ def test_blocked_and_reference_find_same_keys(engine, oracle):
 def test_blocked_layer1_bytes_match_layout_spec(engine, oracle):
     """The blocked (split-block) layer-1 bloom is bit-exact with its specification (kh_kernels.h):
     shard X[0]; 16-byte block (u * blocks) >> 32 with u = X[8..12); four little-endian u32 words,
-    each with the 4 bits given by 5-bit fields of a 32-bit LCG seeded with X[12..16)."""
-    MUL, ADD = 0x9E3779B1, 0x7F4A7C15
+    each with the 4 bits given by 5-bit fields of X[12..24) (big-endian u32s s0, s1, s2; field f is
+    (s_{f/6} >> 5*(f%6)) & 31)."""
     info = engine.bsgs_setup(1 << 20, 1, layer1=1)       # M = 1024 babies
     engine.bsgs_build()
     blocks = info.bloom_bits[0] // 128
@@ -146,12 +146,10 @@ def test_blocked_layer1_bytes_match_layout_spec(engine, oracle):
     model = bytearray(256 * blocks * 16)
     for i in range(1, info.m + 1):
         xb = oracle.pubkey(i)[0].to_bytes(32, "big")
-        u, s = int.from_bytes(xb[8:12], "big"), int.from_bytes(xb[12:16], "big")
+        u = int.from_bytes(xb[8:12], "big")
+        s = [int.from_bytes(xb[12 + 4 * q:16 + 4 * q], "big") for q in range(3)]
         base = xb[0] * blocks * 16 + ((u * blocks) >> 32) * 16
-        fields = []
-        for _ in range(6):
-            s = (s * MUL + ADD) & 0xFFFFFFFF
-            fields += [s >> 27, (s >> 22) & 31, (s >> 17) & 31]
+        fields = [(s[f // 6] >> (5 * (f % 6))) & 31 for f in range(16)]
         for w in range(4):
             for f in fields[4 * w:4 * w + 4]:
                 model[base + 4 * w + (f >> 3)] |= 1 << (f & 7)
