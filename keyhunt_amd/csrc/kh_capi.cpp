@@ -306,6 +306,7 @@ struct kh_ctx {
   uint32_t lanes_max = 1u << 18;
   uint32_t groups_per_launch = 0;
   uint32_t lanes_alloc = 0;
+  int scratch_h = 0;  // inversion-pad entries per lane in d_scratch
   uint32_t *d_cx = nullptr, *d_cy = nullptr, *d_scalars = nullptr;
   uint4 *d_scratch = nullptr;
   std::vector<uint32_t> h_scalars;
@@ -415,8 +416,11 @@ kh_ctx::~kh_ctx() {
 
 namespace {
 
-int ensure_lanes(kh_ctx *c, uint32_t L) {
-  if (L <= c->lanes_alloc) return KH_OK;
+// lane centres for L lanes and an inversion pad of H entries per lane
+int ensure_lanes(kh_ctx *c, uint32_t L, int H = KH_WALK_H) {
+  if (L <= c->lanes_alloc && H <= c->scratch_h) return KH_OK;
+  L = std::max(L, c->lanes_alloc);
+  H = std::max(H, c->scratch_h);
   (void)hipFree(c->d_cx);
   (void)hipFree(c->d_cy);
   (void)hipFree(c->d_scalars);
@@ -424,25 +428,27 @@ int ensure_lanes(kh_ctx *c, uint32_t L) {
   c->d_cx = c->d_cy = c->d_scalars = nullptr;
   c->d_scratch = nullptr;
   c->lanes_alloc = 0;
+  c->scratch_h = 0;
   HIPCHK(c, hipMalloc(&c->d_cx, (size_t)L * 32));
   HIPCHK(c, hipMalloc(&c->d_cy, (size_t)L * 32));
   HIPCHK(c, hipMalloc(&c->d_scalars, (size_t)L * 32));
-  HIPCHK(c, hipMalloc(&c->d_scratch, (size_t)L * KH_WALK_H * 32));
+  HIPCHK(c, hipMalloc(&c->d_scratch, (size_t)L * H * 32));
   c->lanes_alloc = L;
+  c->scratch_h = H;
   return KH_OK;
 }
 
 // delta table T[i] = (i+1)*D, i < H, and T[H] = 2H*D, for D = d*G (d a scalar, may be "negative")
-int get_table(kh_ctx *c, const u256 &d, const uint32_t **out) {
+int get_table(kh_ctx *c, const u256 &d, const uint32_t **out, const int H = KH_WALK_H) {
   uint8_t be[32];
   u256_to_be(be, d);
   std::string key((const char *)be, 32);
+  key += std::to_string(H);
   for (auto &t : c->tables)
     if (t.first == key) {
       *out = t.second;
       return KH_OK;
     }
-  const int H = KH_WALK_H;
   std::vector<uint32_t> h((size_t)(H + 1) * 16);
   ge D;
   if (!c->comb.mult(D, d)) {
@@ -1444,7 +1450,7 @@ bool second_finish(const kh_ctx *c, const u256 &base_key, uint32_t mask, const g
 
 namespace {
 
-int ensure_pipeline(kh_ctx *c, uint32_t L) {
+int ensure_pipeline(kh_ctx *c, uint32_t L, int H) {
   for (int i = 0; i < 2; i++) {
     if (!c->d_cnt2[i]) {
       HIPCHK(c, hipMalloc(&c->d_cnt2[i], 4));
@@ -1462,7 +1468,7 @@ int ensure_pipeline(kh_ctx *c, uint32_t L) {
     }
     c->h_scal_cap = L;
   }
-  return ensure_lanes(c, L);
+  return ensure_lanes(c, L, H);
 }
 
 // grow the per-round candidate buffers to hold `need` entries (stream must be idle)
@@ -1513,15 +1519,22 @@ static int bsgs_scan_impl(kh_ctx *ctx, const u256 &st, const std::vector<u256> *
   (void)hipSetDevice(ctx->device);
   *n_found = 0;
   if (n_bases == 0) return KH_OK;
-  const int H = KH_WALK_H;
   const kh_bsgs_info &I = ctx->info;
   const uint64_t A_pts = I.cycles * 1024;  // giant points walked per base (cycles x 1024)
+  // Continuous mode: when a base's walk ends exactly where the next base's starts (cycles*1024 ==
+  // aux, every power-of-two k), P_t = Q - (start + M + 2M t)G is ONE progression over the whole
+  // call.  Lanes then own long runs of t, start once, and every round just continues them.
+  // Otherwise (bases overlap, SURVEY parity note 13) rounds restart lanes per base run.
+  const bool cont = !list && A_pts == I.aux;
+  // group half-size: continuous runs use the large groups (one inversion per 2*KH_WALK_HB points)
+  // when a base holds whole groups; per-base runs keep the reference's 1024-point group
+  const int H = (cont && A_pts % (2 * KH_WALK_HB) == 0 && !getenv("KH_NO_BIG_GROUPS")) ? KH_WALK_HB : KH_WALK_H;
   auto base_of = [&](uint64_t b) {
     return list ? (*list)[b] : sc_add(st, sc_reduce(u256_from_u128((u128)b * 2 * I.n)));
   };
   // GSn[i] = -(i+1)*2M*G  (keyhunt.cpp:1797-1816)
   const uint32_t *tab = nullptr;
-  int r = get_table(ctx, sc_neg(u256_u64(2 * I.m)), &tab);
+  int r = get_table(ctx, sc_neg(u256_u64(2 * I.m)), &tab, H);
   if (r) return r;
   if (!ctx->refine_threads) {
     unsigned hw = std::thread::hardware_concurrency();
@@ -1533,11 +1546,6 @@ static int bsgs_scan_impl(kh_ctx *ctx, const u256 &st, const std::vector<u256> *
   // of a group whose first point is t sits at key base_b + M + 2M*(a + H).
   const uint64_t gpb = A_pts / (2 * H);  // walk groups per base
   const uint64_t total_groups = n_bases * gpb;
-  // Continuous mode: when a base's walk ends exactly where the next base's starts (cycles*1024 ==
-  // aux, every power-of-two k), P_t = Q - (start + M + 2M t)G is ONE progression over the whole
-  // call.  Lanes then own long runs of t, start once, and every round just continues them.
-  // Otherwise (bases overlap, SURVEY parity note 13) rounds restart lanes per base run.
-  const bool cont = !list && A_pts == I.aux;
   job_geom jc{};
   uint64_t gpr = 0;  // continuous mode: groups per lane per round
   if (cont) {
@@ -1605,7 +1613,7 @@ static int bsgs_scan_impl(kh_ctx *ctx, const u256 &st, const std::vector<u256> *
       R.rg = rg;
       R.L = jg.L;
       R.gpl = jg.gpl;
-      int rr = ensure_pipeline(ctx, jg.L);
+      int rr = ensure_pipeline(ctx, jg.L, H);
       if (rr) return rr;
       if (!cont || need_setup) {
         uint32_t *hs = ctx->h_scal2[slot];
@@ -1653,7 +1661,7 @@ static int bsgs_scan_impl(kh_ctx *ctx, const u256 &st, const std::vector<u256> *
       for (uint64_t gb = gb0; gb < gb1; gb += per_launch) {
         Aw.group_base = gb;
         Aw.groups = (uint32_t)std::min<uint64_t>(per_launch, gb1 - gb);
-        HIPCHK(ctx, launch_walk(ctx->info.layer1_layout == KH_LAYER1_BLOCKED ? KM_BSGSB : KM_BSGS, Aw, ctx->stream));
+        HIPCHK(ctx, launch_walk(ctx->info.layer1_layout == KH_LAYER1_BLOCKED ? KM_BSGSB : KM_BSGS, Aw, ctx->stream, H));
         R.launches++;
         R.points += (uint64_t)jg.L * Aw.groups * 2 * H;
       }

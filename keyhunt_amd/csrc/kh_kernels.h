@@ -13,6 +13,13 @@
 static_assert(KH_WALK_H >= 64 && KH_WALK_H <= 512 && (512 % KH_WALK_H) == 0,
               "2H must divide the reference's 1024-point group so lanes never straddle a BSGS base");
 
+// Large group half-size for the continuous BSGS giant walk (KM_BSGS / KM_BSGSB): lanes there own
+// long runs, so a group may span 4096 points and its one Fermat inversion is shared 4x wider.
+// Scratch per lane = KH_WALK_HB * 32 bytes; the delta table holds KH_WALK_HB + 1 points.
+#ifndef KH_WALK_HB
+#define KH_WALK_HB 2048
+#endif
+
 // minimum waves per SIMD requested for the walk kernel: XPOINT/BSGS/BUILD modes (KH_WALK_LB) and
 // the hash160 modes (KH_WALK_LB_HASH).  256 / LB VGPRs per lane at most; see DESIGN.md.
 #ifndef KH_WALK_LB
@@ -120,7 +127,7 @@ struct refine_args {
 };
 
 namespace kh {
-hipError_t launch_walk(int mode, const walk_args &A, hipStream_t st);
+hipError_t launch_walk(int mode, const walk_args &A, hipStream_t st, int H = KH_WALK_H);
 hipError_t launch_refine(const refine_args &A, hipStream_t st);
 hipError_t launch_setup(const setup_args &A, hipStream_t st);
 hipError_t launch_test_hash160(const uint32_t *xs, const uint32_t *ys, uint32_t n, uint32_t *out, hipStream_t st);

@@ -408,9 +408,8 @@ constexpr int walk_lb() {
                                                                     : KH_WALK_LB;
 }
 
-template <int MODE>
+template <int MODE, int H = KH_WALK_H>
 __global__ void __launch_bounds__(256, walk_lb<MODE>()) k_walk(walk_args A) {
-  constexpr int H = KH_WALK_H;
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= A.L) return;
   kconst_ptr T = (kconst_ptr)A.tab;  // (H+1) x {x[8], y[8]}, wave-uniform reads
@@ -795,8 +794,17 @@ __global__ void k_test_bloom(const uint8_t *items, uint32_t n, uint32_t len, con
 // ------------------------------------------------------------------------------------------
 namespace kh {
 
-hipError_t launch_walk(int mode, const walk_args &A, hipStream_t st) {
+hipError_t launch_walk(int mode, const walk_args &A, hipStream_t st, int H) {
   dim3 block(256), grid((A.L + 255) / 256);
+  if (H == KH_WALK_HB) {
+    switch (mode) {
+      case KM_BSGS: hipLaunchKernelGGL((k_walk<KM_BSGS, KH_WALK_HB>), grid, block, 0, st, A); break;
+      case KM_BSGSB: hipLaunchKernelGGL((k_walk<KM_BSGSB, KH_WALK_HB>), grid, block, 0, st, A); break;
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
+  if (H != KH_WALK_H) return hipErrorInvalidValue;
 #ifdef KH_ONLY_MODE
   if (mode != KH_ONLY_MODE) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_walk<KH_ONLY_MODE>, grid, block, 0, st, A);
