@@ -480,17 +480,16 @@ __global__ void __launch_bounds__(256, walk_lb<MODE>()) k_walk(walk_args A) {
         // math: the loads fly during it.  Only their addresses cross the loop edge (ALU values),
         // never an in-flight load destination.
         const uint4 vm = blk_load(A, pm), vp = blk_load(A, pp);
-        fe xm, xp, s, dy;
+        fe xm, xp, s, dy, sx;
+        fe_add(sx, cx, tx);  // x3 = s^2 - (C.x + T.x) for both points
         fe_add(dy, ty, cy);  // -(dy of C - T[i]); only s^2 is needed, so the sign drops out
         fe_mul(s, dy, di);
         fe_sqr(xm, s);
-        fe_sub(xm, xm, cx);
-        fe_sub(xm, xm, tx);
+        fe_sub(xm, xm, sx);
         fe_sub(dy, ty, cy);
         fe_mul(s, dy, di);
         fe_sqr(xp, s);
-        fe_sub(xp, xp, cx);
-        fe_sub(xp, xp, tx);
+        fe_sub(xp, xp, sx);
         if ((plive & 1u) && blk_match_rec(vm, pm)) record_hit(A, cidx - poff, 4);
         if ((plive & 2u) && blk_match_rec(vp, pp)) record_hit(A, cidx + poff, 4);
         const uint64_t off = (uint64_t)(i + 1);
@@ -502,21 +501,22 @@ __global__ void __launch_bounds__(256, walk_lb<MODE>()) k_walk(walk_args A) {
       }
       if constexpr (MODE == KM_BSGS) {
         // both points first, then one lockstep probe of the pair (two loads in flight per lane)
-        fe xm, xp, s, dy;
+        fe xm, xp, s, dy, sx;
+        fe_add(sx, cx, tx);
         fe_sub(dy, nty, cy);
         fe_mul(s, dy, di);
         fe_sqr(xm, s);
-        fe_sub(xm, xm, cx);
-        fe_sub(xm, xm, tx);
+        fe_sub(xm, xm, sx);
         fe_sub(dy, ty, cy);
         fe_mul(s, dy, di);
         fe_sqr(xp, s);
-        fe_sub(xp, xp, cx);
-        fe_sub(xp, xp, tx);
+        fe_sub(xp, xp, sx);
         const uint64_t off = (uint64_t)(i + 1);
         probe_pair_bsgs(A, xm, cidx - off, xp, cidx + off, i < H - 1);
         continue;
       }
+      fe sx;
+      fe_add(sx, cx, tx);  // x3 = s^2 - (C.x + T.x) on both sides
 #pragma unroll 1
       for (int side = 0; side < 2; side++) {
         if (side == 1 && i == H - 1) break;
@@ -526,8 +526,7 @@ __global__ void __launch_bounds__(256, walk_lb<MODE>()) k_walk(walk_args A) {
         fe_sub(dy, tys, cy);
         fe_mul(s, dy, di);
         fe_sqr(x, s);
-        fe_sub(x, x, cx);
-        fe_sub(x, x, tx);
+        fe_sub(x, x, sx);
         if constexpr (needs_y<MODE>()) {
           fe t;
           fe_sub(t, tx, x);

@@ -103,7 +103,30 @@ KH_HD void fe_canon(fe &r) {
   if (fe_geq_p(r)) fe_sub_p(r);
 }
 
+#if defined(__HIP_DEVICE_COMPILE__)
+// true iff `v` holds on any lane of the wave: a wave-uniform branch around a rarely needed fix-up
+// (a carry rippling past limb 1, a value in [p, 2^256)).  When no lane needs it the wave jumps
+// over it with one scalar branch; when taken, lanes that do not need it run it as a no-op.
+__device__ __forceinline__ bool kh_any(bool v) { return __builtin_amdgcn_ballot_w64(v) != 0; }
+#endif
+
 KH_HD void fe_add(fe &r, const fe &a, const fe &b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  // a, b < p.  r = a + b; on a carry out of 2^256 (a + b - 2^256 < p) add 2^256 - p = 0x1000003D1:
+  // the carry past limb 1 is rare.  Without a carry r < 2^256 is >= p only if its top limb is
+  // all ones (rare).
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.d[i] = addc(a.d[i], b.d[i], c, c);
+  uint32_t c1;
+  r.d[0] = addc(r.d[0], c ? 0x3D1u : 0u, 0, c1);
+  r.d[1] = addc(r.d[1], c, c1, c1);
+  if (kh_any(c1 != 0 || r.d[7] == 0xFFFFFFFFu)) {
+#pragma unroll
+    for (int i = 2; i < 8; i++) r.d[i] = addc(r.d[i], 0, c1, c1);
+    fe_canon(r);
+  }
+#else
   uint32_t c = 0;
 #pragma unroll
   for (int i = 0; i < 8; i++) r.d[i] = addc(a.d[i], b.d[i], c, c);
@@ -117,11 +140,25 @@ KH_HD void fe_add(fe &r, const fe &a, const fe &b) {
   bool sel = (c | c2) != 0;
 #pragma unroll
   for (int i = 0; i < 8; i++) r.d[i] = sel ? t.d[i] : r.d[i];
+#endif
 }
 KH_HD void fe_sub(fe &r, const fe &a, const fe &b) {
   uint32_t br = 0;
 #pragma unroll
   for (int i = 0; i < 8; i++) r.d[i] = subb(a.d[i], b.d[i], br, br);
+#if defined(__HIP_DEVICE_COMPILE__)
+  // borrow: r += p == r -= 0x1000003D1 (mod 2^256); the borrow past limb 1 is rare
+  {
+    uint32_t b2;
+    r.d[0] = subb(r.d[0], br ? 0x3D1u : 0u, 0, b2);
+    r.d[1] = subb(r.d[1], br, b2, b2);
+    if (kh_any(b2 != 0)) {
+#pragma unroll
+      for (int i = 2; i < 8; i++) r.d[i] = subb(r.d[i], 0, b2, b2);
+    }
+    return;
+  }
+#endif
   // borrow: r += p  == r -= 0x1000003D1 (mod 2^256)
   uint32_t k0 = br ? 0x3D1u : 0u, k1 = br ? 1u : 0u, b2;
   r.d[0] = subb(r.d[0], k0, 0, b2);
@@ -160,10 +197,22 @@ KH_HD void fe_reduce512(fe &r, const uint32_t t[16]) {
   v = (uint64_t)u[2] + u[9] + c;
   r.d[2] = (uint32_t)v;
   uint32_t cc = (uint32_t)(v >> 32);
+#if defined(__HIP_DEVICE_COMPILE__)
+  // the carry past limb 2 and a result in [p, 2^256) are both rare
+#pragma unroll
+  for (int i = 3; i < 8; i++) r.d[i] = u[i];
+  if (kh_any(cc != 0 || r.d[7] == 0xFFFFFFFFu)) {
+#pragma unroll
+    for (int i = 3; i < 8; i++) r.d[i] = addc(r.d[i], 0, cc, cc);
+    if (cc) fe_sub_p(r);
+    if (r.d[7] == 0xFFFFFFFFu) fe_canon(r);
+  }
+#else
 #pragma unroll
   for (int i = 3; i < 8; i++) r.d[i] = addc(u[i], 0, cc, cc);
   if (cc) fe_sub_p(r);  // wrapped past 2^256: add 0x1000003D1 (cannot wrap again)
   if (r.d[7] == 0xFFFFFFFFu) fe_canon(r);
+#endif
 }
 
 #if defined(__HIP_DEVICE_COMPILE__)
