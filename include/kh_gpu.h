@@ -143,6 +143,16 @@ int kh_bsgs_build(kh_ctx *ctx);                  /* baby-step blooms + sorted bP
 #define KH_LOAD_SKIP_CHECKSUM 1   /* the reference's -6 */
 int kh_bsgs_save(kh_ctx *ctx, const char *dir);
 int kh_bsgs_load(kh_ctx *ctx, const char *dir, uint32_t flags);
+
+/* -S for -m address|rmd160|xpoint (and -c eth): the target file cache data_<hex>.dat, named by the
+ * CLI from the first 4 bytes of the target file's sha256 (keyhunt.cpp:7043-7049).  Layout:
+ * sha256(bloom bits) | struct bloom (112 B) | bloom bits | sha256(rows) | u64 row bytes | sorted
+ * 20-byte rows.  kh_targets_save writes the context's targets (after kh_set_targets), replacing
+ * writeFileIfNeeded (keyhunt.cpp:7756-7855); kh_targets_load stands in for kh_set_targets and takes
+ * the bloom geometry and bits from the file, as readFileAddress does (keyhunt.cpp:7033-7210), so a
+ * file the reference wrote probes identically.  flags: KH_LOAD_SKIP_CHECKSUM. */
+int kh_targets_save(kh_ctx *ctx, const char *path);
+int kh_targets_load(kh_ctx *ctx, const char *path, uint32_t flags);
 /* targets: n x {x[32], y[32]} affine points (big-endian) */
 int kh_bsgs_set_targets(kh_ctx *ctx, const uint8_t *xy, uint32_t n);
 /* Walk n_bases bases start, start + 2N, ... for every target not yet found.  Keys already found

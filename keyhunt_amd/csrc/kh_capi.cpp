@@ -328,6 +328,7 @@ struct kh_ctx {
   std::vector<uint8_t> v_ranges;
   uint32_t probe_len = 20;
   bloom_desc tbd{};
+  uint64_t t_entries = 0;  // the target bloom's struct bloom `entries`
   std::vector<uint8_t> h_tbloom;
   uint8_t *d_tbloom = nullptr;
 
@@ -675,7 +676,8 @@ int kh_set_targets(kh_ctx *ctx, const uint8_t *rows, uint64_t n, uint64_t bloom_
   ctx->vanity = false;
   ctx->probe_len = 20;
   ctx->v_ranges.clear();
-  ctx->tbd = bloom_size(bloom_entries(bloom_items ? bloom_items : n));
+  ctx->t_entries = bloom_entries(bloom_items ? bloom_items : n);
+  ctx->tbd = bloom_size(ctx->t_entries);
   ctx->h_tbloom.assign(ctx->tbd.bytes, 0);
   for (uint64_t i = 0; i < n; i++) host_bloom_add(ctx->h_tbloom.data(), ctx->tbd, &ctx->rows[i * 20], 20);
   (void)hipFree(ctx->d_tbloom);
@@ -694,7 +696,8 @@ int kh_set_vanity(kh_ctx *ctx, const uint8_t *ranges, uint64_t n, uint32_t probe
   ctx->vanity = true;
   ctx->probe_len = probe_len;
   // processOneVanity / readFileVanity (keyhunt.cpp:6970-7035): bloom over A's first probe_len bytes
-  ctx->tbd = bloom_size(bloom_entries(bloom_items ? bloom_items : n));
+  ctx->t_entries = bloom_entries(bloom_items ? bloom_items : n);
+  ctx->tbd = bloom_size(ctx->t_entries);
   ctx->h_tbloom.assign(ctx->tbd.bytes, 0);
   for (uint64_t i = 0; i < n; i++) host_bloom_add(ctx->h_tbloom.data(), ctx->tbd, &ctx->v_ranges[i * 40], (int)probe_len);
   (void)hipFree(ctx->d_tbloom);
@@ -1308,6 +1311,99 @@ int kh_bsgs_load(kh_ctx *ctx, const char *dir, uint32_t flags) {
   }
   ctx->h_rows.swap(rows);
   ctx->bsgs_built = true;
+  return KH_OK;
+}
+
+// ==============================================================================================
+// Target files (-S for address/rmd160/xpoint): data_<hex>.dat as readFileAddress reads it
+// (keyhunt.cpp:7033-7210) and writeFileIfNeeded writes it (7756-7855):
+//   sha256(bloom bits) | struct bloom (112 B) | bloom bits | sha256(table) | u64 table bytes |
+//   the sorted 20-byte rows (struct address_value).
+// ==============================================================================================
+int kh_targets_save(kh_ctx *ctx, const char *path) {
+  if (!ctx || !path) return KH_E_ARG;
+  if (!ctx->d_tbloom || ctx->vanity) return KH_E_STATE;
+  FILE *f = fopen(path, "wb");
+  if (!f) {
+    ctx->err = std::string("can't create the file ") + path;
+    return KH_E_IO;
+  }
+  uint8_t ckb[32], ckd[32], h[KH_BLOOM_STRUCT];
+  sha256_bytes(ctx->h_tbloom.data(), ctx->tbd.bytes, ckb);
+  bloom_header(h, ctx->t_entries, ctx->tbd);
+  const uint64_t data_size = ctx->n_rows * 20;
+  sha256_bytes(ctx->rows.data(), data_size, ckd);
+  bool ok = fwrite(ckb, 1, 32, f) == 32 && fwrite(h, 1, KH_BLOOM_STRUCT, f) == KH_BLOOM_STRUCT &&
+            fwrite(ctx->h_tbloom.data(), 1, ctx->tbd.bytes, f) == ctx->tbd.bytes && fwrite(ckd, 1, 32, f) == 32 &&
+            fwrite(&data_size, 1, 8, f) == 8 && fwrite(ctx->rows.data(), 1, data_size, f) == data_size;
+  ok = (fclose(f) == 0) && ok;
+  if (!ok) {
+    ctx->err = std::string("error writing the file ") + path;
+    return KH_E_IO;
+  }
+  return KH_OK;
+}
+
+int kh_targets_load(kh_ctx *ctx, const char *path, uint32_t flags) {
+  if (!ctx || !path) return KH_E_ARG;
+  (void)hipSetDevice(ctx->device);
+  FILE *f = fopen(path, "rb");
+  if (!f) {
+    ctx->err = std::string("can't open the file ") + path;
+    return KH_E_IO;
+  }
+  uint8_t ckb[32], ckd[32], h[KH_BLOOM_STRUCT], ck[32];
+  std::vector<uint8_t> bits, rows;
+  uint64_t entries = 0, nbits = 0, nbytes = 0, data_size = 0;
+  int rc = KH_OK;
+  if (fread(ckb, 1, 32, f) != 32 || fread(h, 1, KH_BLOOM_STRUCT, f) != KH_BLOOM_STRUCT) rc = KH_E_IO;
+  if (!rc) {
+    memcpy(&entries, h + 0, 8);
+    memcpy(&nbits, h + 8, 8);
+    memcpy(&nbytes, h + 16, 8);
+    // the reader trusts bits/bytes/hashes of the stored struct (keyhunt.cpp:7076-7081)
+    if (nbits == 0 || h[24] == 0 || nbytes != nbits / 8 + ((nbits % 8) ? 1 : 0)) rc = KH_E_FORMAT;
+  }
+  if (!rc) {
+    bits.resize(nbytes);
+    if (fread(bits.data(), 1, nbytes, f) != nbytes || fread(ckd, 1, 32, f) != 32 || fread(&data_size, 1, 8, f) != 8)
+      rc = KH_E_IO;
+  }
+  if (!rc && data_size % 20) rc = KH_E_FORMAT;
+  if (!rc) {
+    rows.resize(data_size);
+    if (fread(rows.data(), 1, data_size, f) != data_size) rc = KH_E_IO;
+  }
+  fclose(f);
+  if (!rc && !(flags & KH_LOAD_SKIP_CHECKSUM)) {  // FLAGSKIPCHECKSUM (keyhunt.cpp:7129-7146, 7193-7200)
+    sha256_bytes(bits.data(), nbytes, ck);
+    if (memcmp(ck, ckb, 32)) rc = KH_E_FORMAT;
+    sha256_bytes(rows.data(), data_size, ck);
+    if (!rc && memcmp(ck, ckd, 32)) rc = KH_E_FORMAT;
+  }
+  if (rc) {
+    ctx->err = std::string(rc == KH_E_IO ? "error reading the file " : "checksum or format mismatch in ") + path;
+    return rc;
+  }
+  bloom_desc d;
+  memset(&d, 0, sizeof d);
+  d.bits = nbits;
+  d.bytes = nbytes;
+  d.hashes = h[24];
+  d.recip = ~0ULL / d.bits;
+  d.stride = d.bytes;
+  ctx->rows.swap(rows);
+  ctx->n_rows = data_size / 20;
+  ctx->vanity = false;
+  ctx->probe_len = 20;
+  ctx->v_ranges.clear();
+  ctx->t_entries = entries;
+  ctx->tbd = d;
+  ctx->h_tbloom.swap(bits);
+  (void)hipFree(ctx->d_tbloom);
+  ctx->d_tbloom = nullptr;
+  HIPCHK(ctx, hipMalloc(&ctx->d_tbloom, ctx->tbd.bytes + 4));
+  HIPCHK(ctx, hipMemcpy(ctx->d_tbloom, ctx->h_tbloom.data(), ctx->tbd.bytes, hipMemcpyHostToDevice));
   return KH_OK;
 }
 

@@ -86,6 +86,8 @@ def lib() -> ctypes.CDLL:
     L.kh_bsgs_build.argtypes = [P]
     L.kh_bsgs_save.argtypes = [P, ctypes.c_char_p]
     L.kh_bsgs_load.argtypes = [P, ctypes.c_char_p, ctypes.c_uint32]
+    L.kh_targets_save.argtypes = [P, ctypes.c_char_p]
+    L.kh_targets_load.argtypes = [P, ctypes.c_char_p, ctypes.c_uint32]
     L.kh_bsgs_set_targets.argtypes = [P, u8p, ctypes.c_uint32]
     L.kh_bsgs_scan.argtypes = [P, u8p, ctypes.c_uint64, ctypes.POINTER(KhBsgsFound), ctypes.c_uint32,
                                ctypes.POINTER(ctypes.c_uint32)]
@@ -173,6 +175,14 @@ class Engine:
         buf = b"".join(rows)
         assert all(len(r) == 20 for r in rows)
         self._chk(lib().kh_set_targets(self._ctx, buf, len(rows), bloom_items), "kh_set_targets")
+
+    def targets_save(self, path: str) -> None:
+        """Write the -S target file (data_<hex>.dat layout) of the current targets to path."""
+        self._chk(lib().kh_targets_save(self._ctx, path.encode()), "kh_targets_save")
+
+    def targets_load(self, path: str, skip_checksum: bool = False) -> None:
+        """Targets (rows and bloom, geometry included) from a data_<hex>.dat file, instead of set_targets."""
+        self._chk(lib().kh_targets_load(self._ctx, path.encode(), 1 if skip_checksum else 0), "kh_targets_load")
 
     def scan(self, start: int, n_keys: int, mode: int = KH_MODE_ADDRESS, search: int = KH_SEARCH_BOTH,
              stride: int = 1, cap: int = 4096, endo: bool = False) -> list[ScanHit]:

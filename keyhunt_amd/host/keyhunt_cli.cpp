@@ -8,8 +8,8 @@
 // BSGS in whole 2N bases (keyhunt.cpp:4600-4617), exactly as the reference's cursors do.
 // BSGS base schedules -B sequential|backward|both|random|dance|angrygiant and random chunks (-R)
 // follow the reference's cursors (see take_bases).  -e (address/rmd160/xpoint), -c eth (address/rmd160)
-// and -S / -6 (BSGS table files in the reference's formats) are provided; -B ggsb, vanity and minikeys
-// are rejected.
+// -m vanity, and -S / -6 (the BSGS table files and the address/rmd160/xpoint data_<hex>.dat target
+// cache, in the reference's formats) are provided; -B ggsb and minikeys are rejected.
 #include <getopt.h>
 #include <pthread.h>
 #include <stdint.h>
@@ -431,8 +431,28 @@ struct addr_job {
   const std::vector<uint8_t> *rows;
   uint64_t bloom_items;
   uint64_t nseq;
+  const char *data_file = nullptr;  // -S: data_<hex>.dat to read (or, with save_data, to write)
+  bool save_data = false;
   int rc = 0;
 };
+
+// -S target cache name (readFileAddress / writeFileIfNeeded, keyhunt.cpp:7043-7049, 7765-7770):
+// data_ + hex of the first 4 bytes of the target file's sha256
+bool data_file_name(const char *fn, std::string &name) {
+  FILE *f = fopen(fn, "rb");
+  if (!f) return false;
+  std::vector<uint8_t> buf;
+  uint8_t chunk[1 << 16];
+  size_t n;
+  while ((n = fread(chunk, 1, sizeof chunk, f)) > 0) buf.insert(buf.end(), chunk, chunk + n);
+  fclose(f);
+  uint8_t ck[32];
+  sha256(buf.data(), buf.size(), ck);
+  char hex[9];
+  snprintf(hex, sizeof hex, "%02x%02x%02x%02x", ck[0], ck[1], ck[2], ck[3]);
+  name = std::string("data_") + hex + ".dat";
+  return true;
+}
 
 void addr_worker(addr_job *j) {
   kh_ctx *ctx = nullptr;
@@ -446,8 +466,15 @@ void addr_worker(addr_job *j) {
   if (opt.mode == MODE_VANITY)
     r = kh_set_vanity(ctx, opt.vanity.ranges.data(), opt.vanity.ranges.size() / 40, (uint32_t)opt.vanity.min_bytes,
                       opt.vanity.total);
+  else if (j->data_file && !j->save_data)
+    r = kh_targets_load(ctx, j->data_file, opt.skip_checksum ? KH_LOAD_SKIP_CHECKSUM : 0);
   else
     r = kh_set_targets(ctx, j->rows->data(), j->rows->size() / 20, j->bloom_items);
+  if (!r && j->save_data) {
+    printf("[+] Writing file %s ........\n", j->data_file);
+    r = kh_targets_save(ctx, j->data_file);
+  }
+  if (r) fprintf(stderr, "[E] GPU %d: %s (%s)\n", j->device, kh_strerror(r), kh_last_error(ctx));
   std::vector<kh_hit> hits(1 << 16);
   uint8_t st_be[32], stride_be[32];
   u_to_be32(opt.stride, stride_be);
@@ -873,6 +900,7 @@ int main(int argc, char **argv) {
   std::vector<addr_job> aj(gpus);
   std::vector<bsgs_job> bj(gpus);
   std::vector<uint8_t> rows;
+  std::string data_file;  // -S target cache (outlives the GPU threads)
   std::vector<fe> tx, ty;
   std::vector<bool> comp;
 
@@ -884,20 +912,41 @@ int main(int argc, char **argv) {
     }
     printf("[+] N = %p\n", (void *)nseq);
     uint64_t items = 0;
-    if (opt.mode == MODE_VANITY) {
+    // -S: read the target cache if it exists (FLAGREADEDFILE1), else read the file and write it
+    bool have_data = false;
+    if (opt.save_read && opt.mode != MODE_VANITY) {
+      if (!data_file_name(opt.file, data_file)) {
+        fprintf(stderr, "[E] sha256_file error\n");
+        return EXIT_FAILURE;
+      }
+      FILE *df = fopen(data_file.c_str(), "rb");
+      if (df) {
+        fclose(df);
+        have_data = true;
+        printf("[+] Reading file %s\n", data_file.c_str());
+      }
+    }
+    if (have_data) {
+      // rows and bloom come from the file, in each GPU's kh_targets_load
+    } else if (opt.mode == MODE_VANITY) {
       if (!read_vanity(opt.file)) return EXIT_FAILURE;
     } else if (opt.eth && opt.mode == MODE_ADDRESS) {
       if (!read_targets_eth(opt.file, rows, items)) return EXIT_FAILURE;
     } else if (!read_targets(opt.file, opt.mode, rows, items)) {
       return EXIT_FAILURE;
     }
-    printf("[+] Sorting data ... done! %llu values were loaded and sorted\n", (unsigned long long)(rows.size() / 20));
+    if (!have_data)
+      printf("[+] Sorting data ... done! %llu values were loaded and sorted\n", (unsigned long long)(rows.size() / 20));
     g_running = gpus;
     for (int d = 0; d < gpus; d++) {
       aj[d].device = d;
       aj[d].rows = &rows;
       aj[d].bloom_items = items;
       aj[d].nseq = nseq;
+      if (!data_file.empty()) {
+        aj[d].data_file = data_file.c_str();
+        aj[d].save_data = !have_data && d == 0;  // one GPU writes the cache
+      }
       th.emplace_back(addr_worker, &aj[d]);
     }
   } else {

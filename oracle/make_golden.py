@@ -11,8 +11,11 @@ TEST INFRASTRUCTURE.  Runs in the development container only (needs /root/refere
                                  KEYFOUNDKEYFOUND.txt it writes.
   tests/golden/ref_tables.json   digests of the -S table files the reference CLI writes at small
                                  (n, k) (heap pointers masked).
+  tests/golden/ref_data/         the -S target caches (data_<hex>.dat) the reference CLI writes for
+                                 address / rmd160 / xpoint / eth target files, with
+                                 ref_data/index.json (name, size, masked sha256, hit set of the run).
 
-Usage:  python oracle/make_golden.py [--vectors] [--e2e] [--tables]
+Usage:  python oracle/make_golden.py [--vectors] [--e2e] [--tables] [--data]
 """
 from __future__ import annotations
 
@@ -108,6 +111,47 @@ def gen_tables() -> None:
         json.dump(out, f, indent=1, sort_keys=True)
 
 
+# -S target caches (keyhunt.cpp:7756-7855): data_<hex>.dat per target file
+DATA_RUNS = [
+    ("address_1to32", "1to32.txt", ["-m", "address", "-f", "1to32.txt", "-r", "1:FFFFF", "-n", "0x100000", "-S", "-t", "2"]),
+    ("rmd160_1to32", "1to32.rmd", ["-m", "rmd160", "-f", "1to32.rmd", "-l", "compress", "-r", "1:FFFFF", "-n", "0x100000", "-S", "-t", "2"]),
+    ("xpoint_1to63_65", "1to63_65.txt", ["-m", "xpoint", "-f", "1to63_65.txt", "-r", "1:FFFFF", "-n", "0x100000", "-S", "-t", "2"]),
+    ("eth_targets", "eth_targets.txt", ["-m", "address", "-c", "eth", "-f", "eth_targets.txt", "-r", "1:FFFFF", "-n", "0x100000", "-S", "-t", "2"]),
+]
+
+
+def masked_data_digest(path: str) -> str:
+    """sha256 of a data_<hex>.dat with the struct bloom's `bf` heap pointer (file bytes 96..104) zeroed."""
+    import hashlib
+    data = bytearray(open(path, "rb").read())
+    data[32 + 64: 32 + 72] = bytes(8)
+    return hashlib.sha256(bytes(data)).hexdigest()
+
+
+def gen_data() -> None:
+    subprocess.run(["make", "-s", "-C", HERE, "-f", "Makefile.ref", "-j8"], check=True)
+    dst = os.path.join(REPO, "tests", "golden", "ref_data")
+    os.makedirs(dst, exist_ok=True)
+    index = {}
+    for name, src, argv in DATA_RUNS:
+        with tempfile.TemporaryDirectory() as td:
+            shutil.copy(os.path.join(DATA, src), td)
+            p = subprocess.run(["timeout", "120", REF_BIN] + argv + ["-q"], cwd=td, capture_output=True, text=True)
+            files = [f for f in os.listdir(td) if f.startswith("data_")]
+            assert len(files) == 1, (name, files, p.stdout, p.stderr)
+            f = files[0]
+            shutil.copy(os.path.join(td, f), os.path.join(dst, f))
+            kf = os.path.join(td, "KEYFOUNDKEYFOUND.txt")
+            hits = parse_keyfound(open(kf).read()) if os.path.exists(kf) else []
+            index[name] = {"argv": argv, "source": src, "file": f, "size": os.path.getsize(os.path.join(td, f)),
+                           "masked_sha256": masked_data_digest(os.path.join(td, f)),
+                           "keys": sorted({h["key"] for h in hits})}
+            print(name, p.returncode, f, flush=True)
+    index["_generator"] = "oracle/make_golden.py --data: oracle/_ref/keyhunt -S (reference CLI built from its sources)"
+    with open(os.path.join(dst, "index.json"), "w") as fh:
+        json.dump(index, fh, indent=1, sort_keys=True)
+
+
 def gen_vectors() -> None:
     subprocess.run(["make", "-s", "-C", HERE, "-f", "Makefile.ref", "-j8"], check=True)
     out = subprocess.run([REF_GOLDEN], check=True, capture_output=True, text=True).stdout
@@ -160,13 +204,16 @@ if __name__ == "__main__":
     ap.add_argument("--vectors", action="store_true")
     ap.add_argument("--e2e", action="store_true")
     ap.add_argument("--tables", action="store_true")
+    ap.add_argument("--data", action="store_true")
     ap.add_argument("--only", nargs="*")
     a = ap.parse_args()
-    if not a.vectors and not a.e2e and not a.tables:
-        a.vectors = a.e2e = a.tables = True
+    if not a.vectors and not a.e2e and not a.tables and not a.data:
+        a.vectors = a.e2e = a.tables = a.data = True
     if a.vectors:
         gen_vectors()
     if a.e2e:
         gen_e2e(a.only)
     if a.tables:
         gen_tables()
+    if a.data:
+        gen_data()
