@@ -43,10 +43,18 @@ sys.path.insert(0, REPO)
 METRIC = "Mkeys/s at 1/2/4/8 GPU (BSGS b125; addr b66); HBM GB/s fraction"
 HBM_PEAK_GBS = 8000.0
 ALGO_BYTES_PER_GIANT_POINT = {0: 128, 1: 64}      # by layer-1 layout (reference, blocked)
-WALK_KERNEL = {0: "k_walk<4>", 1: "k_walk<7>"}    # KM_BSGS, KM_BSGSB
+WALK_KERNEL = {0: "k_walk<4, 2048>", 1: "k_walk<7, 2048>"}    # KM_BSGS, KM_BSGSB on 4096-point groups
 # 256 CU x 4 SIMD x 32 lanes/clk (a wave64 VALU op issues over 2 clk) x 2.4 GHz, MI355X_MICROARCH.md
 VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
 PUZZLE125 = "0233709eb11e0d4439a729f21c2c443dedb727528229713f0065721ba8fa46f00e"
+PUZZLE130 = "03633cbe3ec02b9401c5effa144c5b4d22f87940259634858fc7e59b1c09937852"
+# BSGS workloads: --config 4 (the metric's, default) and 5 (BASELINE configs[4], k = 512)
+BSGS_CONFIGS = {
+    4: {"pub": PUZZLE125, "bits": 125, "k": 128, "bases": 65536,
+        "workload": "-m bsgs -f tests/125.txt -b 125 -k 128", "data": "puzzle-125 public key (tests/125.txt)"},
+    5: {"pub": PUZZLE130, "bits": 130, "k": 512, "bases": 262144,
+        "workload": "-m bsgs -f tests/130.txt -b 130 -k 512", "data": "puzzle-130 public key (tests/130.txt)"},
+}
 PUZZLE66_RMD = "20d45a6a762535700ce9e0b216e31994335db8a5"
 P = 2**256 - 2**32 - 977
 
@@ -112,16 +120,17 @@ def timed(D: Dist, eng, warmup: int, steps: int, step_fn):
 
 def bsgs_leg(D: Dist, eng, args):
     import keyhunt_amd as K
-    info = eng.bsgs_setup(1 << 44, 128, layer1=args.layer1)
+    C = BSGS_CONFIGS[args.config]
+    info = eng.bsgs_setup(1 << 44, C["k"], layer1=args.layer1)
     t = time.perf_counter()
     eng.bsgs_build()
     eng.synchronize()
     build_s = time.perf_counter() - t
-    q = decompress(PUZZLE125)
+    q = decompress(C["pub"])
     eng.bsgs_set_targets([q])
     two_n = 2 * info.n
-    base0 = 1 << 124
-    B = args.bases
+    base0 = 1 << (C["bits"] - 1)
+    B = args.bases or C["bases"]
 
     def step(s):
         batch = s * D.world + D.rank
@@ -131,6 +140,7 @@ def bsgs_leg(D: Dist, eng, args):
     T = timed(D, eng, args.warmup, args.steps, step)
     la, ms, pts = eng.kernel_time(K.engine.TIME_BSGS)
     keys = D.world * args.steps * B * two_n
+    args.bases = B
     pts_launch = pts / la
     ms_launch = ms / la
     bpp = ALGO_BYTES_PER_GIANT_POINT[info.layer1_layout]
@@ -208,14 +218,14 @@ def cpu_threads() -> int:
         return max(1, min(16, os.cpu_count() or 1))
 
 
-def cpu_baseline_bsgs(eng, info, q, seconds: float):
+def cpu_baseline_bsgs(eng, info, q, seconds: float, k: int = 128):
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle
     # the CPU restatement probes the reference-layout layer 1: rebuild it in that layout
-    eng.bsgs_setup(1 << 44, 128, layer1=0)
+    eng.bsgs_setup(1 << 44, k, layer1=0)
     eng.bsgs_build()
     bf1 = eng.get_bloom(1)
-    p = oracle.bsgs_params(1 << 44, 128)
+    p = oracle.bsgs_params(1 << 44, k)
     thr = cpu_threads()
     t = time.perf_counter()
     oracle.bsgs_giant_probe(p, bf1, q, 4, thr)
@@ -227,7 +237,7 @@ def cpu_baseline_bsgs(eng, info, q, seconds: float):
     pts = thr * groups * 1024
     return {"value": pts * 2 * info.m / dt / 1e6, "unit": "Mkeys/s", "cores": thr, "kind": "port",
             "sample": f"{pts} giant-step points ({groups} 1024-point groups x {thr} threads) probed against the "
-                      f"GPU-built k=128 layer-1 bloom, {dt:.1f} s; keys = points x 2M",
+                      f"GPU-built k={k} layer-1 bloom, {dt:.1f} s; keys = points x 2M",
             "giant_points_per_s": pts / dt}
 
 
@@ -259,7 +269,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--bases", type=int, default=65536, help="BSGS bases (of 2N keys) per step per GPU")
+    ap.add_argument("--config", type=int, default=4, choices=sorted(BSGS_CONFIGS),
+                    help="BSGS workload: 4 = b125 k128 (the metric's), 5 = b130 k512")
+    ap.add_argument("--bases", type=int, default=0, help="BSGS bases (of 2N keys) per step per GPU (0: per config)")
     ap.add_argument("--steps-rmd", type=int, default=None)
     ap.add_argument("--warmup-rmd", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -279,7 +291,7 @@ def main():
     sec = None if args.no_secondary else rmd160_leg(D, eng, args)
     cpu_b = cpu_r = None
     if D.rank == 0 and D.world == 1 and not args.no_cpu_baseline:
-        cpu_b = cpu_baseline_bsgs(eng, prim["info"], prim["q"], args.cpu_seconds)
+        cpu_b = cpu_baseline_bsgs(eng, prim["info"], prim["q"], args.cpu_seconds, BSGS_CONFIGS[args.config]["k"])
         cpu_r = cpu_baseline_rmd160(int(args.cpu_seconds + 5))
     eng.close()
     D.barrier()
@@ -289,8 +301,8 @@ def main():
             "metric": METRIC, "value": prim["value"], "unit": "Mkeys/s", "n_gpus": D.world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": prim["ms_per_step"], "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "u32",
-            "data": "synthetic: puzzle-125 public key (tests/125.txt), sequential bases from 2^124",
-            "config": {"workload": "-m bsgs -f tests/125.txt -b 125 -k 128", "n": info.n, "k": 128, "m": info.m,
+            "data": f"synthetic: {BSGS_CONFIGS[args.config]['data']}, sequential bases from 2^{BSGS_CONFIGS[args.config]['bits'] - 1}",
+            "config": {"workload": BSGS_CONFIGS[args.config]["workload"], "n": info.n, "k": BSGS_CONFIGS[args.config]["k"], "m": info.m,
                        "layer1_layout": "blocked" if info.layer1_layout == 1 else "reference",
                        "bases_per_step": args.bases, "giant_points_per_step": args.bases * info.cycles * 1024,
                        "parallelism": f"keyspace split x{D.world} (no collective)"},

@@ -36,3 +36,7 @@ if has pmc; then
   done
   echo "pmc ok"
 fi
+if has config5; then
+  timeout -k 10 600 python $R/bench.py --config 5 > $O/bench_c5.json 2> $O/bench_c5.err || { echo "bench c5 rc=$?"; tail -20 $O/bench_c5.err; exit 1; }
+  cat $O/bench_c5.json
+fi

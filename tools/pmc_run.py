@@ -10,7 +10,7 @@ e = K.Engine(0)
 info = e.bsgs_setup(1 << 44, 128)
 e.bsgs_build()
 e.bsgs_set_targets([bench.decompress(bench.PUZZLE125)])
-e.bsgs_scan(1 << 124, 16384)          # one round: 2^18 lanes x 2 groups = 2^29 giant points
+e.bsgs_scan(1 << 124, 32768)          # one launch: 2^18 lanes x 1 group of 4096 = 2^30 giant points
 e.set_targets([bytes.fromhex(bench.PUZZLE66_RMD)], bloom_items=1)
 e.scan(1 << 65, 1 << 30, K.KH_MODE_ADDRESS, K.KH_SEARCH_COMPRESS)
 e.synchronize()
