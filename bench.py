@@ -9,6 +9,8 @@ Metric (BASELINE.json): "Mkeys/s at 1/2/4/8 GPU (BSGS b125; addr b66); HBM GB/s 
               (2N per base, keyhunt.cpp:4883-4884 / 2871-2874).
   secondary : -m rmd160 -f tests/66.rmd -b 66 -l compress (configs[1]).  A step = one 2^32-key
               N_SEQUENTIAL_MAX chunk; keys counted x2 for -l compress (keyhunt.cpp:2889-2891).
+  tertiary  : -m xpoint -f tests/63.pub -b 63 (configs[2]), same chunks, one key per point.
+  --config 5: the primary on -m bsgs -f tests/130.txt -b 130 -k 512 (configs[4]) instead.
 Ranks split the keyspace (weak scaling, no collective on the data path): rank r of N walks chunk /
 base-batch s*N + r.  The table build (baby steps) is replicated per GPU and not timed; its time is
 reported.  torch.distributed (gloo, CPU tensors) provides the barrier and the max over ranks; the
@@ -56,6 +58,7 @@ BSGS_CONFIGS = {
         "workload": "-m bsgs -f tests/130.txt -b 130 -k 512", "data": "puzzle-130 public key (tests/130.txt)"},
 }
 PUZZLE66_RMD = "20d45a6a762535700ce9e0b216e31994335db8a5"
+PUZZLE63_X = 0x65ec2994b8cc0a20d40dd69edfe55ca32a54bcbbaa6b0ddcff36049301a54579  # tests/63.pub
 P = 2**256 - 2**32 - 977
 
 
@@ -211,6 +214,26 @@ def rmd160_leg(D: Dist, eng, args):
                        "points_per_launch": pts / la, "points_per_s_in_kernel": pts / (ms / 1e3)}}
 
 
+def xpoint_leg(D: Dist, eng, args):
+    """-m xpoint -f tests/63.pub -b 63 (BASELINE configs[2]): X[0..20) probes, one key per point."""
+    import keyhunt_amd as K
+    eng.set_targets([PUZZLE63_X.to_bytes(32, "big")[:20]], bloom_items=1)
+    chunk = 1 << 32
+    base0 = 1 << 62
+
+    def step(s):
+        c = s * D.world + D.rank
+        hits = eng.scan(base0 + c * chunk, chunk, K.KH_MODE_XPOINT, K.KH_SEARCH_COMPRESS)
+        assert not hits
+
+    T = timed(D, eng, args.warmup_rmd, args.steps_rmd, step)
+    la, ms, pts = eng.kernel_time(K.engine.TIME_XPOINT)
+    keys = D.world * args.steps_rmd * chunk
+    return {"value": keys / T / 1e6, "ms_per_step": T / args.steps_rmd * 1e3,
+            "kernel": {"name": "k_walk<KM_XPOINT>", "launches": la, "mean_launch_ms": ms / la,
+                       "points_per_launch": pts / la, "points_per_s_in_kernel": pts / (ms / 1e3)}}
+
+
 def cpu_threads() -> int:
     try:
         return max(1, min(16, len(os.sched_getaffinity(0))))
@@ -289,6 +312,7 @@ def main():
     eng = K.Engine(D.local % max(1, ndev))
     prim = bsgs_leg(D, eng, args)
     sec = None if args.no_secondary else rmd160_leg(D, eng, args)
+    ter = None if args.no_secondary else xpoint_leg(D, eng, args)
     cpu_b = cpu_r = None
     if D.rank == 0 and D.world == 1 and not args.no_cpu_baseline:
         cpu_b = cpu_baseline_bsgs(eng, prim["info"], prim["q"], args.cpu_seconds, BSGS_CONFIGS[args.config]["k"])
@@ -317,6 +341,10 @@ def main():
             line["secondary"] = {"workload": "-m rmd160 -f tests/66.rmd -b 66 -l compress", "value": sec["value"],
                                  "unit": "Mkeys/s", "ms_per_step": sec["ms_per_step"], "steps": args.steps_rmd,
                                  "kernel": sec["kernel"], "cpu_baseline": cpu_r}
+        if ter:
+            line["tertiary"] = {"workload": "-m xpoint -f tests/63.pub -b 63", "value": ter["value"],
+                                "unit": "Mkeys/s", "ms_per_step": ter["ms_per_step"], "steps": args.steps_rmd,
+                                "kernel": ter["kernel"]}
         json_out.write(json.dumps(line) + "\n")
         json_out.flush()
     D.close()
