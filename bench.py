@@ -48,6 +48,7 @@ ALGO_BYTES_PER_GIANT_POINT = {0: 128, 1: 64}      # by layer-1 layout (reference
 WALK_KERNEL = {0: "k_walk<4, 2048>", 1: "k_walk<7, 2048>"}    # KM_BSGS, KM_BSGSB on 4096-point groups
 # 256 CU x 4 SIMD x 32 lanes/clk (a wave64 VALU op issues over 2 clk) x 2.4 GHz, MI355X_MICROARCH.md
 VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
+RANDOM16_CEILING_GPS = 51.36   # measured random 16-B nontemporal loads/s, 24 GB footprint (profiles/)
 PUZZLE125 = "0233709eb11e0d4439a729f21c2c443dedb727528229713f0065721ba8fa46f00e"
 PUZZLE130 = "03633cbe3ec02b9401c5effa144c5b4d22f87940259634858fc7e59b1c09937852"
 # BSGS workloads: --config 4 (the metric's, default) and 5 (BASELINE configs[4], k = 512)
@@ -156,8 +157,14 @@ def bsgs_leg(D: Dist, eng, args):
         a = ipp * pts_launch / (ms_launch / 1e3) / 1e12
         valu = {"achieved": a, "peak": VALU_PEAK_TOPS, "unit": "T lane-instr/s", "frac": a / VALU_PEAK_TOPS,
                 "lane_instructions_per_giant_point": ipp, "source": tsrc}
+    # the probe is one random 16-B load per giant point: its own ceiling is the chip's random-load
+    # rate at this footprint (tools/ubench_random2.hip, profiles/r01l_random16B.txt: 24 GB, nt loads)
+    rand = {"achieved": pts_launch / (ms_launch / 1e3) / 1e9, "ceiling": RANDOM16_CEILING_GPS, "unit": "G loads/s",
+            "frac": pts_launch / (ms_launch / 1e3) / 1e9 / RANDOM16_CEILING_GPS,
+            "source": "profiles/r01l_random16B.txt"} if info.layer1_layout == 1 else None
     res = {
         "value": keys / T / 1e6,
+        "random_access": rand,
         "ms_per_step": T / args.steps * 1e3,
         "giant_points_per_s": D.world * args.steps * B * info.cycles * 1024 / T,
         "build_seconds": build_s,
@@ -335,6 +342,7 @@ def main():
             "first_level_candidates": prim["candidates"],
             "roofline": prim["roofline"],
             "valu": prim["valu"],
+            "random_access": prim["random_access"],
             "cpu_baseline": cpu_b,
         }
         if sec:
