@@ -530,20 +530,21 @@ job_geom plan(kh_ctx *c, uint64_t total_groups, uint64_t gpl_divides) {
 }
 
 // walk all lanes through `gpl` groups in launches of groups_per_launch; kind = timing slot
-int run_walk(kh_ctx *c, int mode, int kind, walk_args A, uint64_t gpl, uint32_t default_gpl_launch) {
+int run_walk(kh_ctx *c, int mode, int kind, walk_args A, uint64_t gpl, uint32_t default_gpl_launch,
+             int H = KH_WALK_H) {
   uint32_t per = c->groups_per_launch ? c->groups_per_launch : default_gpl_launch;
   for (uint64_t gb = 0; gb < gpl; gb += per) {
     A.group_base = gb;
     A.groups = (uint32_t)std::min<uint64_t>(per, gpl - gb);
     HIPCHK(c, hipEventRecord(c->ev_a, c->stream));
-    HIPCHK(c, launch_walk(mode, A, c->stream));
+    HIPCHK(c, launch_walk(mode, A, c->stream, H));
     HIPCHK(c, hipEventRecord(c->ev_b, c->stream));
     HIPCHK(c, hipEventSynchronize(c->ev_b));
     float ms = 0;
     (void)hipEventElapsedTime(&ms, c->ev_a, c->ev_b);
     c->tm[kind].launches++;
     c->tm[kind].ms += ms;
-    c->tm[kind].points += (uint64_t)A.L * A.groups * 2 * KH_WALK_H;
+    c->tm[kind].points += (uint64_t)A.L * A.groups * 2 * H;
   }
   return KH_OK;
 }
@@ -715,12 +716,23 @@ int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride_be[32], u
   if (mode > KH_MODE_ETH || search > KH_SEARCH_BOTH || (mode == KH_MODE_ETH && endo)) return KH_E_ARG;
   if (!ctx->d_tbloom) return KH_E_STATE;
   (void)hipSetDevice(ctx->device);
-  const int H = KH_WALK_H;
+  int km = mode == KH_MODE_XPOINT ? KM_XPOINT
+         : mode == KH_MODE_ETH ? KM_ETH
+         : search == KH_SEARCH_COMPRESS ? KM_H160C
+         : search == KH_SEARCH_UNCOMPRESS ? KM_H160U
+                                          : KM_H160B;
+  if (endo) km |= KM_ENDO;
+  // xpoint and compressed rmd160/address (configs 2-3) walk 4096-point groups when the chunk holds
+  // whole ones (the default 2^32-key chunk does): one inversion per 4096 points
+  const int H = ((km == KM_XPOINT || km == KM_H160C) && n_keys % (2 * KH_WALK_HB) == 0 &&
+                 !getenv("KH_NO_BIG_GROUPS"))
+                    ? KH_WALK_HB
+                    : KH_WALK_H;
   u256 st = sc_reduce(u256_from_be(start));
   u256 stride = stride_be ? sc_reduce(u256_from_be(stride_be)) : u256_u64(1);
   if (u256_is_zero(stride)) return KH_E_ARG;
   const uint32_t *tab = nullptr;
-  int r = get_table(ctx, stride, &tab);
+  int r = get_table(ctx, stride, &tab, H);
   if (r) return r;
 
   uint64_t total_groups = n_keys / (2 * H);
@@ -744,15 +756,11 @@ int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride_be[32], u
       return KH_E_ARG;
     }
   }
+  r = ensure_lanes(ctx, jg.L, H);  // the pad for H entries per lane, before the centres are set
+  if (r) return r;
   r = run_setup(ctx, s, nullptr);
   if (r) return r;
 
-  int km = mode == KH_MODE_XPOINT ? KM_XPOINT
-         : mode == KH_MODE_ETH ? KM_ETH
-         : search == KH_SEARCH_COMPRESS ? KM_H160C
-         : search == KH_SEARCH_UNCOMPRESS ? KM_H160U
-                                          : KM_H160B;
-  if (endo) km |= KM_ENDO;
   walk_args A;
   memset(&A, 0, sizeof A);
   A.tab = tab;
@@ -771,7 +779,7 @@ int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride_be[32], u
   uint32_t nd = 0;
   for (;;) {
     HIPCHK(ctx, hipMemsetAsync(ctx->d_hit_count, 0, 4, ctx->stream));
-    r = run_walk(ctx, km, mode == KH_MODE_XPOINT ? 1 : 0, A, jg.gpl, 2);
+    r = run_walk(ctx, km, mode == KH_MODE_XPOINT ? 1 : 0, A, jg.gpl, 2, H);
     if (r) return r;
     r = fetch_hits(ctx, nd);
     if (r != KH_E_OVERFLOW) break;

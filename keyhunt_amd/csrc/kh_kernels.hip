@@ -799,6 +799,8 @@ hipError_t launch_walk(int mode, const walk_args &A, hipStream_t st, int H) {
     switch (mode) {
       case KM_BSGS: hipLaunchKernelGGL((k_walk<KM_BSGS, KH_WALK_HB>), grid, block, 0, st, A); break;
       case KM_BSGSB: hipLaunchKernelGGL((k_walk<KM_BSGSB, KH_WALK_HB>), grid, block, 0, st, A); break;
+      case KM_XPOINT: hipLaunchKernelGGL((k_walk<KM_XPOINT, KH_WALK_HB>), grid, block, 0, st, A); break;
+      case KM_H160C: hipLaunchKernelGGL((k_walk<KM_H160C, KH_WALK_HB>), grid, block, 0, st, A); break;
       default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
