@@ -155,6 +155,7 @@ struct options {
   vanity_set vanity;           // -m vanity targets (-v, -f)
   bool save_read = false;      // -S: read the table files if present, else build and write them
   bool skip_checksum = false;  // -6
+  int bloom_mult = 1;          // -z (FLAGBLOOMMULTIPLIER)
 } opt;
 // keyhunt.cpp:419; ggsb (re-blocked baby tables) is not provided, angrygiant walks like sequential
 const char *BSGS_MODES[7] = {"sequential", "backward", "both", "random", "dance", "ggsb", "angrygiant"};
@@ -719,7 +720,9 @@ void bsgs_worker(bsgs_job *j) {
 
 void usage(const char *p) {
   printf("Usage: %s -m address|rmd160|xpoint|bsgs -f FILE [-b BITS | -r START:END] [-l compress|uncompress|both]\n"
-         "       [-n N] [-k K] [-I STRIDE] [-g GPUS] [-q] [-s SECONDS] [-M] [-L blocked|reference]\n", p);
+         "       [-n N] [-k K] [-I STRIDE] [-g GPUS] [-q] [-s SECONDS] [-M] [-L blocked|reference]\n"
+         "       [-e] [-c btc|eth] [-R] [-B sequential|backward|both|random|dance|angrygiant] [-S] [-6]\n"
+         "       [-z MULT] [-m vanity -v PREFIX ...] [-d] [-h]\n", p);
 }
 
 }  // namespace
@@ -730,7 +733,7 @@ int main(int argc, char **argv) {
   int c;
   U order;
   u_from_hex(ORDER_HEX, order);
-  while ((c = getopt(argc, argv, "m:f:l:r:b:k:n:t:g:qs:I:L:MRec:B:S6v:")) != -1) {
+  while ((c = getopt(argc, argv, "m:f:l:r:b:k:n:t:g:qs:I:L:MRec:B:S6v:z:dh")) != -1) {
     switch (c) {
       case 'm': {
         int m = -1;
@@ -839,6 +842,17 @@ int main(int argc, char **argv) {
           return EXIT_FAILURE;
         }
         break;
+      case 'z':  // keyhunt.cpp:1112-1118: bloom entries = multiplier x items above 10000 (7608)
+        opt.bloom_mult = (int)strtol(optarg, NULL, 10);
+        if (opt.bloom_mult <= 0) opt.bloom_mult = 1;
+        printf("[+] Bloom Size Multiplier %i\n", opt.bloom_mult);
+        break;
+      case 'd':  // keyhunt.cpp:1019-1022
+        printf("[+] Flag DEBUG enabled\n");
+        break;
+      case 'h':
+        usage(argv[0]);
+        return EXIT_SUCCESS;
       default: usage(argv[0]); return EXIT_FAILURE;
     }
   }
@@ -941,7 +955,9 @@ int main(int argc, char **argv) {
     for (int d = 0; d < gpus; d++) {
       aj[d].device = d;
       aj[d].rows = &rows;
-      aj[d].bloom_items = items;
+      // initBloomFilter (keyhunt.cpp:7608): max(10000, items), times -z above the floor
+      const uint64_t nitems = items ? items : rows.size() / 20;
+      aj[d].bloom_items = nitems <= 10000 ? nitems : nitems * (uint64_t)opt.bloom_mult;
       aj[d].nseq = nseq;
       if (!data_file.empty()) {
         aj[d].data_file = data_file.c_str();

@@ -117,6 +117,9 @@ DATA_RUNS = [
     ("rmd160_1to32", "1to32.rmd", ["-m", "rmd160", "-f", "1to32.rmd", "-l", "compress", "-r", "1:FFFFF", "-n", "0x100000", "-S", "-t", "2"]),
     ("xpoint_1to63_65", "1to63_65.txt", ["-m", "xpoint", "-f", "1to63_65.txt", "-r", "1:FFFFF", "-n", "0x100000", "-S", "-t", "2"]),
     ("eth_targets", "eth_targets.txt", ["-m", "address", "-c", "eth", "-f", "eth_targets.txt", "-r", "1:FFFFF", "-n", "0x100000", "-S", "-t", "2"]),
+    # > 10000 rows with -z 2: bloom entries = 2 x items (keyhunt.cpp:7608); the 330 KB cache itself
+    # is not committed, only its digest (the target file comes from tests/golden/make_many_targets.py)
+    ("rmd160_many_z2", "many.rmd", ["-m", "rmd160", "-f", "many.rmd", "-l", "compress", "-r", "1:FFFFF", "-n", "0x100000", "-z", "2", "-S", "-t", "2"]),
 ]
 
 
@@ -135,17 +138,24 @@ def gen_data() -> None:
     index = {}
     for name, src, argv in DATA_RUNS:
         with tempfile.TemporaryDirectory() as td:
-            shutil.copy(os.path.join(DATA, src), td)
+            if src == "many.rmd":
+                import sys
+                sys.path.insert(0, os.path.join(REPO, "tests", "golden"))
+                import make_many_targets
+                make_many_targets.write(os.path.join(td, src))
+            else:
+                shutil.copy(os.path.join(DATA, src), td)
             p = subprocess.run(["timeout", "120", REF_BIN] + argv + ["-q"], cwd=td, capture_output=True, text=True)
             files = [f for f in os.listdir(td) if f.startswith("data_")]
             assert len(files) == 1, (name, files, p.stdout, p.stderr)
             f = files[0]
-            shutil.copy(os.path.join(td, f), os.path.join(dst, f))
+            if src != "many.rmd":
+                shutil.copy(os.path.join(td, f), os.path.join(dst, f))
             kf = os.path.join(td, "KEYFOUNDKEYFOUND.txt")
             hits = parse_keyfound(open(kf).read()) if os.path.exists(kf) else []
             index[name] = {"argv": argv, "source": src, "file": f, "size": os.path.getsize(os.path.join(td, f)),
                            "masked_sha256": masked_data_digest(os.path.join(td, f)),
-                           "keys": sorted({h["key"] for h in hits})}
+                           "keys": sorted({h["key"] for h in hits}), "committed": src != "many.rmd"}
             print(name, p.returncode, f, flush=True)
     index["_generator"] = "oracle/make_golden.py --data: oracle/_ref/keyhunt -S (reference CLI built from its sources)"
     with open(os.path.join(dst, "index.json"), "w") as fh:

@@ -4,7 +4,8 @@ writeFileIfNeeded (keyhunt.cpp:7756-7855) and read by readFileAddress (7033-7210
 tests/golden/ref_data/ holds the files the reference CLI wrote for four target files
 (oracle/make_golden.py --data) with their sizes, digests (struct bloom heap pointer masked) and the
 keys that run found.  The engine's CLI must write the same bytes, read its own and the reference's
-files back with the same hits, and reject a corrupted file unless -6 skips the checksums."""
+files back with the same hits, and reject a corrupted file unless -6 skips the checksums.  One case
+has 12032 rows and -z 2, so its bloom is sized past the 10000-entry floor (keyhunt.cpp:7608)."""
 import hashlib
 import json
 import os
@@ -40,7 +41,14 @@ def run_in(td, argv, timeout=300):
 
 def fresh_dir(case):
     td = tempfile.mkdtemp()
-    shutil.copy(os.path.join(DATA, INDEX[case]["source"]), td)
+    src = INDEX[case]["source"]
+    if src == "many.rmd":  # > 10000 rows, generated (tests/golden/make_many_targets.py)
+        import sys
+        sys.path.insert(0, GOLDEN)
+        import make_many_targets
+        make_many_targets.write(os.path.join(td, src))
+    else:
+        shutil.copy(os.path.join(DATA, src), td)
     return td
 
 
@@ -65,7 +73,7 @@ def test_written_data_file_equals_reference_and_reads_back(case):
         shutil.rmtree(td)
 
 
-@pytest.mark.parametrize("case", CASES)
+@pytest.mark.parametrize("case", [c for c in CASES if INDEX[c].get("committed", True)])
 def test_reads_reference_written_data_file(case):
     want = INDEX[case]
     argv = want["argv"][:want["argv"].index("-t")]
