@@ -9,7 +9,8 @@
 // BSGS base schedules -B sequential|backward|both|random|dance|angrygiant and random chunks (-R)
 // follow the reference's cursors (see take_bases).  -e (address/rmd160/xpoint), -c eth (address/rmd160)
 // -m vanity, and -S / -6 (the BSGS table files and the address/rmd160/xpoint data_<hex>.dat target
-// cache, in the reference's formats) are provided; -B ggsb and minikeys are rejected.
+// cache, in the reference's formats) and -B ggsb / --bsgs-block-count / --bsgs-block-size are
+// provided; minikeys are rejected.
 #include <getopt.h>
 #include <pthread.h>
 #include <stdint.h>
@@ -156,8 +157,11 @@ struct options {
   bool save_read = false;      // -S: read the table files if present, else build and write them
   bool skip_checksum = false;  // -6
   int bloom_mult = 1;          // -z (FLAGBLOOMMULTIPLIER)
+  // GGSB (keyhunt.cpp:1477-1499, 1617-1627): -B ggsb or --bsgs-block-count/--bsgs-block-size
+  bool ggsb = false;
+  uint64_t ggsb_count = 0, ggsb_size = 0;
 } opt;
-// keyhunt.cpp:419; ggsb (re-blocked baby tables) is not provided, angrygiant walks like sequential
+// keyhunt.cpp:419; ggsb and angrygiant walk like sequential (ggsb with BSGS_STEP = 2 x block size)
 const char *BSGS_MODES[7] = {"sequential", "backward", "both", "random", "dance", "ggsb", "angrygiant"};
 enum { BM_SEQUENTIAL, BM_BACKWARD, BM_BOTH, BM_RANDOM, BM_DANCE, BM_GGSB, BM_ANGRYGIANT };
 
@@ -546,6 +550,8 @@ std::mutex g_found_mtx;
 //   dance                    rand()%3: TOP, BOTTOM or Rand(current, end) keyhunt.cpp:5706-5750
 // g_cursor plays BSGS_CURRENT (and n_range_start), g_top n_range_end.
 U g_top;
+U g_step;  // BSGS_STEP
+// step = BSGS_STEP: 2N, or 2 x the GGSB block size when the babies are split into several blocks
 bool take_bases(const U &twoN, uint64_t want, std::vector<U> &out) {
   out.clear();
   std::lock_guard<std::mutex> lk(g_cursor_mtx);
@@ -562,7 +568,7 @@ bool take_bases(const U &twoN, uint64_t want, std::vector<U> &out) {
     return true;
   };
   int mode = opt.bsgs_mode;
-  if (mode == BM_SEQUENTIAL || mode == BM_ANGRYGIANT || mode == BM_BACKWARD) {
+  if (mode == BM_SEQUENTIAL || mode == BM_ANGRYGIANT || mode == BM_BACKWARD || mode == BM_GGSB) {
     while (out.size() < want && (mode == BM_BACKWARD ? top() : bottom())) {
     }
     return !out.empty();
@@ -657,7 +663,7 @@ void bsgs_worker(bsgs_job *j) {
   std::vector<U> bases;
   std::vector<uint8_t> list_be;
   while (!r) {
-    if (!take_bases(twoN, j->bases_per_call, bases)) break;
+    if (!take_bases(g_step, j->bases_per_call, bases)) break;
     const uint64_t nb = bases.size();
     // consecutive ascending bases go through kh_bsgs_scan (one progression), others as a list
     std::sort(bases.begin(), bases.end(), [](const U &a, const U &b) { return u_cmp(a, b) < 0; });
@@ -733,8 +739,19 @@ int main(int argc, char **argv) {
   int c;
   U order;
   u_from_hex(ORDER_HEX, order);
-  while ((c = getopt(argc, argv, "m:f:l:r:b:k:n:t:g:qs:I:L:MRec:B:S6v:z:dh")) != -1) {
+  static const struct option long_opts[] = {{"bsgs-block-count", required_argument, 0, 1},
+                                           {"bsgs-block-size", required_argument, 0, 2},
+                                           {0, 0, 0, 0}};
+  while ((c = getopt_long(argc, argv, "m:f:l:r:b:k:n:t:g:qs:I:L:MRec:B:S6v:z:dh", long_opts, nullptr)) != -1) {
     switch (c) {
+      case 1:  // keyhunt.cpp:809-811: implies GGSB
+        opt.ggsb_count = strtoull(optarg, NULL, 10);
+        opt.ggsb = opt.ggsb_count > 0;
+        break;
+      case 2:  // keyhunt.cpp:812-814
+        opt.ggsb_size = strtoull(optarg, NULL, 10);
+        opt.ggsb = opt.ggsb_size > 0;
+        break;
       case 'm': {
         int m = -1;
         for (int i = 0; i < 5; i++)
@@ -814,11 +831,9 @@ int main(int argc, char **argv) {
           if (!strcmp(optarg, BSGS_MODES[i])) idx = i;
         if (idx < 0) {
           fprintf(stderr, "[W] Ignoring unknow bsgs mode %s\n", optarg);
-        } else if (idx == BM_GGSB) {
-          fprintf(stderr, "[E] -B ggsb is not provided by this engine\n");
-          return EXIT_FAILURE;
         } else {
-          opt.bsgs_mode = idx;
+          opt.bsgs_mode = idx;  // GGSB reuses the sequential worker (keyhunt.cpp:2764-2767)
+          if (idx == BM_GGSB) opt.ggsb = true;
         }
         break;
       }
@@ -1007,6 +1022,21 @@ int main(int argc, char **argv) {
     uint64_t Nr = (n / M) * M;
     twoN = u_mul_u64(u_from_u64(Nr), 2);
     printf("[+] N = 0x%llx\n", (unsigned long long)Nr);
+    // GGSB block geometry from sqrt(N) (keyhunt.cpp:1477-1499) and the base step (1617-1627)
+    g_step = twoN;
+    if (opt.ggsb) {
+      uint64_t bc = opt.ggsb_count, bs = opt.ggsb_size;
+      if (bc == 0 && bs == 0) bc = 1;
+      if (bc > 0 && bs == 0)
+        bs = (m + bc - 1) / bc;
+      else if (bs > 0 && bc == 0)
+        bc = (m + bs - 1) / bs;
+      if (bc == 0) bc = 1;
+      if (bs == 0) bs = m;
+      if (bc > 1 && bs) g_step = u_mul_u64(u_from_u64(bs), 2);
+      fprintf(stderr, "[i] BSGS table build: %s layout, creating %llu block(s) of %llu babies each.\n",
+              bc > 1 ? "GGSB" : "classic", (unsigned long long)bc, (unsigned long long)bs);
+    }
     g_running = gpus;
     for (int d = 0; d < gpus; d++) {
       bj[d].device = d;

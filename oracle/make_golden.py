@@ -71,6 +71,9 @@ E2E_RUNS = [
     # deterministic base schedules (keyhunt.cpp:5953 backward, 6211 both)
     ("bsgs_63_backward", ["-m", "bsgs", "-f", "63.pub", "-B", "backward", "-r", "7cce5a0000000000:7cce9a0000000000", "-t", "8"], 300),
     ("bsgs_63_both", ["-m", "bsgs", "-f", "63.pub", "-B", "both", "-r", "7cce5a0000000000:7cce9a0000000000", "-t", "8"], 300),
+    # GGSB: bases every 2 x block size (keyhunt.cpp:1477-1499, 1617-1627), sequential worker
+    ("bsgs_63_ggsb_count4", ["-m", "bsgs", "-f", "63.pub", "-n", "0x1000000", "-k", "4", "-B", "ggsb", "--bsgs-block-count", "4", "-r", "7cce5efdac000000:7cce5efdad000000", "-t", "8"], 300),
+    ("bsgs_63_ggsb_size1024_both", ["-m", "bsgs", "-f", "63.pub", "-n", "0x1000000", "-k", "4", "-B", "both", "--bsgs-block-size", "1024", "-r", "7cce5efdac000000:7cce5efdad000000", "-t", "8"], 300),
 ]
 
 

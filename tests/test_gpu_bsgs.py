@@ -65,7 +65,10 @@ def test_cli_bsgs_matches_reference(name):
     argv = [a for a in ref["argv"] if a not in ("-t", "8")]
     p, hits = run_cli(argv)
     assert p.returncode == ref["exit"], p.stdout[-2000:] + p.stderr[-2000:]
-    assert hits == ref["hits"]
+    # overlapping bases (GGSB strides) let several reference threads print the same key before
+    # the exit; compare each distinct hit once
+    uniq = lambda hs: [h for i, h in enumerate(hs) if h not in hs[:i]]
+    assert uniq(hits) == uniq(ref["hits"])
 
 
 def test_bench_config_k128_known_answer():
