@@ -50,8 +50,14 @@ def test_cli_rejects_out_of_scope_and_bad_nk(tmp_path):
     assert r.returncode == 1 and "too large" in r.stderr
     r = subprocess.run([cli, "-m", "address", "-f", "x", "-S"], capture_output=True, text=True)
     assert r.returncode == 1   # -S is accepted, the missing target file is not
-    r = subprocess.run([cli, "-m", "bsgs", "-f", "x", "-B", "ggsb"], capture_output=True, text=True)
-    assert r.returncode == 1 and "ggsb" in r.stderr
+    # -B ggsb and its long options are accepted (the missing range is what fails here)
+    r = subprocess.run([cli, "-m", "bsgs", "-f", "x", "-B", "ggsb", "--bsgs-block-count", "4"], capture_output=True,
+                       text=True)
+    assert r.returncode == 1 and "ggsb" not in r.stderr and "range" in r.stderr
+    r = subprocess.run([cli, "-h"], capture_output=True, text=True)
+    assert r.returncode == 0 and "Usage" in r.stdout
+    r = subprocess.run([cli, "-m", "rmd160", "-f", "x", "-z", "2", "-r", "1:100000"], capture_output=True, text=True)
+    assert "Bloom Size Multiplier 2" in r.stdout
     # keyhunt.cpp:1185-1193 test the -B index against MODE_BSGS: -B both + -e / -I fail in any mode
     r = subprocess.run([cli, "-m", "address", "-f", "x", "-B", "both", "-e"], capture_output=True, text=True)
     assert r.returncode == 1 and "Endomorphism doesn't work with BSGS" in r.stderr
