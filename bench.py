@@ -11,8 +11,9 @@ Metric (BASELINE.json): "Mkeys/s at 1/2/4/8 GPU (BSGS b125; addr b66); HBM GB/s 
               N_SEQUENTIAL_MAX chunk; keys counted x2 for -l compress (keyhunt.cpp:2889-2891).
   tertiary  : -m xpoint -f tests/63.pub -b 63 (configs[2]), same chunks, one key per point.
   --config 5: the primary on -m bsgs -f tests/130.txt -b 130 -k 512 (configs[4]) instead.
-Ranks split the keyspace (weak scaling, no collective on the data path): rank r of N walks chunk /
-base-batch s*N + r.  The table build (baby steps) is replicated per GPU and not timed; its time is
+Ranks split the keyspace (weak scaling, no collective on the data path): rank r of N walks chunks
+s*N + r, and its own contiguous run of BSGS base batches (r*(W+K) + s), so consecutive kh_bsgs_scan
+calls continue the same lanes.  The table build (baby steps) is replicated per GPU and not timed; its time is
 reported.  torch.distributed (gloo, CPU tensors) provides the barrier and the max over ranks; the
 engine owns the GPU through its own HIP stream, synchronised on both sides of the timed region.
 
@@ -136,8 +137,9 @@ def bsgs_leg(D: Dist, eng, args):
     base0 = 1 << (C["bits"] - 1)
     B = args.bases or C["bases"]
 
+    # rank r walks its own contiguous run of batches, so consecutive steps continue its lanes
     def step(s):
-        batch = s * D.world + D.rank
+        batch = D.rank * (args.warmup + args.steps) + s
         found = eng.bsgs_scan(base0 + batch * B * two_n, B)
         assert not found  # puzzle 125's key lies far from the start of the range
 

@@ -307,6 +307,13 @@ struct kh_ctx {
   uint32_t groups_per_launch = 0;
   uint32_t lanes_alloc = 0;
   int scratch_h = 0;  // inversion-pad entries per lane in d_scratch
+  // continuous BSGS lanes kept across kh_bsgs_scan calls: valid while the lane centres sit at the
+  // first group of the call that would start at cont_next (same target, lanes and group size)
+  bool cont_valid = false;
+  u256 cont_next{};
+  uint32_t cont_L = 0, cont_tgt = 0;
+  int cont_H = 0;
+  uint32_t *d_q = nullptr;  // the current BSGS target {x[8], y[8]}
   uint32_t *d_cx = nullptr, *d_cy = nullptr, *d_scalars = nullptr;
   uint4 *d_scratch = nullptr;
   std::vector<uint32_t> h_scalars;
@@ -389,6 +396,7 @@ kh_ctx::~kh_ctx() {
   (void)hipFree(d_cy);
   (void)hipFree(d_scalars);
   (void)hipFree(d_scratch);
+  (void)hipFree(d_q);
   for (auto &t : tables) (void)hipFree(t.second);
   (void)hipFree(d_hit_count);
   (void)hipFree(d_hits);
@@ -422,6 +430,7 @@ int ensure_lanes(kh_ctx *c, uint32_t L, int H = KH_WALK_H) {
   if (L <= c->lanes_alloc && H <= c->scratch_h) return KH_OK;
   L = std::max(L, c->lanes_alloc);
   H = std::max(H, c->scratch_h);
+  c->cont_valid = false;
   (void)hipFree(c->d_cx);
   (void)hipFree(c->d_cy);
   (void)hipFree(c->d_scalars);
@@ -440,11 +449,12 @@ int ensure_lanes(kh_ctx *c, uint32_t L, int H = KH_WALK_H) {
 }
 
 // delta table T[i] = (i+1)*D, i < H, and T[H] = 2H*D, for D = d*G (d a scalar, may be "negative")
-int get_table(kh_ctx *c, const u256 &d, const uint32_t **out, const int H = KH_WALK_H) {
+// jump > 1 (interleaved lanes): the last entry is the jump between a lane's groups, jump*2H*D
+int get_table(kh_ctx *c, const u256 &d, const uint32_t **out, const int H = KH_WALK_H, uint64_t jump = 1) {
   uint8_t be[32];
   u256_to_be(be, d);
   std::string key((const char *)be, 32);
-  key += std::to_string(H);
+  key += std::to_string(H) + "/" + std::to_string(jump);
   for (auto &t : c->tables)
     if (t.first == key) {
       *out = t.second;
@@ -464,7 +474,19 @@ int get_table(kh_ctx *c, const u256 &d, const uint32_t **out, const int H = KH_W
     memcpy(&h[(size_t)i * 16 + 8], cur.y.d, 32);
   }
   ge d2;
-  ge_double(d2, cur);  // 2H * D
+  if (jump == 1) {
+    ge_double(d2, cur);  // 2H * D
+  } else {
+    u256 e = u256_u64(0), x = d;  // (jump * 2H) * d mod n by double-and-add
+    for (uint64_t k = jump * 2 * (uint64_t)H; k; k >>= 1) {
+      if (k & 1) e = sc_add(e, x);
+      x = sc_add(x, x);
+    }
+    if (!c->comb.mult(d2, e)) {
+      c->err = "group jump scalar is 0";
+      return KH_E_ARG;
+    }
+  }
   memcpy(&h[(size_t)H * 16], d2.x.d, 32);
   memcpy(&h[(size_t)H * 16 + 8], d2.y.d, 32);
   uint32_t *dev = nullptr;
@@ -478,6 +500,7 @@ int get_table(kh_ctx *c, const u256 &d, const uint32_t **out, const int H = KH_W
 // Lane centres: C_g = [Q +] s_g*G.  s: L scalars (already reduced, non-zero)
 int run_setup(kh_ctx *c, const std::vector<u256> &s, const ge *q) {
   uint32_t L = (uint32_t)s.size();
+  c->cont_valid = false;  // the lane centres are about to be replaced
   int r = ensure_lanes(c, L);
   if (r) return r;
   c->h_scalars.resize((size_t)L * 8);
@@ -888,6 +911,7 @@ int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride_be[32], u
 // BSGS
 // ---------------------------------------------------------------------------------------------
 int kh_bsgs_setup(kh_ctx *ctx, uint64_t n, uint64_t k, kh_bsgs_info *info) {
+  if (ctx) ctx->cont_valid = false;
   if (!ctx || !k) return KH_E_ARG;
   (void)hipSetDevice(ctx->device);
   // keyhunt.cpp:1454-1661
@@ -984,6 +1008,7 @@ namespace {
 // (bl1/bd1, reference or blocked layout by `mode`), layers 2/3 (the context's) and the bP rows
 int build_walk(kh_ctx *ctx, int mode, uint8_t *bl1, const bloom_desc &bd1, uint64_t *d_key, uint32_t *d_val) {
   const int H = KH_WALK_H;
+  ctx->cont_valid = false;
   const kh_bsgs_info &I = ctx->info;
   const uint32_t *tab = nullptr;
   int r = get_table(ctx, u256_u64(1), &tab);
@@ -1417,6 +1442,7 @@ int kh_targets_load(kh_ctx *ctx, const char *path, uint32_t flags) {
 
 int kh_bsgs_set_targets(kh_ctx *ctx, const uint8_t *xy, uint32_t n) {
   if (!ctx || (!xy && n)) return KH_E_ARG;
+  ctx->cont_valid = false;
   ctx->targets.resize(n);
   for (uint32_t i = 0; i < n; i++) {
     fe_from_be(ctx->targets[i].x, xy + 64 * i);
@@ -1653,10 +1679,18 @@ static int bsgs_scan_impl(kh_ctx *ctx, const u256 &st, const std::vector<u256> *
   job_geom jc{};
   uint64_t gpr = 0;  // continuous mode: groups per lane per round
   if (cont) {
+    // interleaved lanes: lane g walks groups g, g + L, g + 2L, ... of the call, so after the call
+    // it sits on group g of the call that starts where this one ends (kept across calls)
     jc = plan(ctx, total_groups, 0);
     gpr = std::max<uint64_t>(1, KH_BSGS_ROUND_POINTS / ((uint64_t)jc.L * 2 * H));
     gpr = std::min<uint64_t>(gpr, jc.gpl);
+    r = get_table(ctx, sc_neg(u256_u64(2 * I.m)), &tab, H, jc.L);
+    if (r) return r;
+  } else if (!list) {
+    ctx->cont_valid = false;
   }
+  if (list) ctx->cont_valid = false;
+  const bool keep_lanes = cont && ctx->targets.size() == 1;
   // second check on the GPU: the kernel derives base_key from the candidate's giant index
   const bool gpu_refine = !ctx->refine_host;
   if (gpu_refine) {
@@ -1690,16 +1724,19 @@ static int bsgs_scan_impl(kh_ctx *ctx, const u256 &st, const std::vector<u256> *
     const uint64_t round_max = (uint64_t)ctx->lanes_max * (gpb % 2 == 0 ? 2 : 1);
     const uint64_t g_end = cont ? jc.gpl : total_groups;
     uint64_t g0 = 0;
-    bool need_setup = true;  // continuous mode: (re)start the lanes at group g0
+    // continuous mode: (re)start the lanes at group g0, unless the previous call left them here
+    bool need_setup = !(keep_lanes && ctx->cont_valid && ctx->cont_tgt == tgt && ctx->cont_L == jc.L &&
+                        ctx->cont_H == H && u256_cmp(ctx->cont_next, st) == 0);
+    ctx->cont_valid = false;
     int cur = 0, pending = -1;
     bsgs_round rounds[2];
     bool done = false;
     uint32_t Qw[16];
     memcpy(Qw, Q.x.d, 32);
     memcpy(Qw + 8, Q.y.d, 32);
-    uint32_t *dq = nullptr;
-    HIPCHK(ctx, hipMalloc(&dq, 64));
-    HIPCHK(ctx, hipMemcpy(dq, Qw, 64, hipMemcpyHostToDevice));
+    if (!ctx->d_q) HIPCHK(ctx, hipMalloc(&ctx->d_q, 64));
+    uint32_t *dq = ctx->d_q;
+    HIPCHK(ctx, hipMemcpyAsync(dq, Qw, 64, hipMemcpyHostToDevice, ctx->stream));
     auto enqueue = [&](int slot) -> int {
       bsgs_round &R = rounds[slot];
       uint64_t rg;
@@ -1722,7 +1759,7 @@ static int bsgs_scan_impl(kh_ctx *ctx, const u256 &st, const std::vector<u256> *
       if (!cont || need_setup) {
         uint32_t *hs = ctx->h_scal2[slot];
         for (uint32_t g = 0; g < jg.L; g++) {
-          uint64_t t0 = cont ? (uint64_t)g * jc.gpl * 2 * H + g0 * 2 * H : R.t_round + (uint64_t)g * jg.gpl * 2 * H;
+          uint64_t t0 = cont ? (g0 * jc.L + g) * 2 * H : R.t_round + (uint64_t)g * jg.gpl * 2 * H;
           u256_to_limbs(hs + (size_t)g * 8, centre_scalar(t0));
         }
         HIPCHK(ctx, hipMemcpyAsync(ctx->d_scalars, hs, (size_t)jg.L * 32, hipMemcpyHostToDevice, ctx->stream));
@@ -1753,6 +1790,7 @@ static int bsgs_scan_impl(kh_ctx *ctx, const u256 &st, const std::vector<u256> *
       Aw.scratch = ctx->d_scratch;
       Aw.L = jg.L;
       Aw.lane_stride = jg.gpl * 2 * H;
+      Aw.interleave = cont ? 1 : 0;
       Aw.n_points = cont ? total_groups * 2 * H : rg * 2 * H;
       Aw.bloom = ctx->d_bl[0];
       Aw.bd = ctx->bd[0];
@@ -1881,10 +1919,7 @@ static int bsgs_scan_impl(kh_ctx *ctx, const u256 &st, const std::vector<u256> *
       int nxt = -1;
       if (g0 < g_end) {
         r = enqueue(cur);
-        if (r) {
-          (void)hipFree(dq);
-          return r;
-        }
+        if (r) return r;
         nxt = cur;
         cur ^= 1;
       }
@@ -1897,10 +1932,7 @@ static int bsgs_scan_impl(kh_ctx *ctx, const u256 &st, const std::vector<u256> *
           pending = -1;
           continue;
         }
-        if (r) {
-          (void)hipFree(dq);
-          return r;
-        }
+        if (r) return r;
       }
       pending = nxt;
     }
@@ -1908,7 +1940,13 @@ static int bsgs_scan_impl(kh_ctx *ctx, const u256 &st, const std::vector<u256> *
       (void)hipStreamSynchronize(ctx->stream);
       (void)hipStreamSynchronize(ctx->side);
     }
-    (void)hipFree(dq);
+    if (keep_lanes && !done && g0 == g_end) {  // every lane walked all its groups of this call
+      ctx->cont_valid = true;
+      ctx->cont_next = sc_add(st, sc_reduce(u256_from_u128((u128)n_bases * 2 * I.n)));
+      ctx->cont_tgt = tgt;
+      ctx->cont_L = jc.L;
+      ctx->cont_H = H;
+    }
   }
   *n_found = nf;
   return nf > cap ? KH_E_OVERFLOW : KH_OK;

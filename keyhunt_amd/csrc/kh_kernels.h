@@ -78,6 +78,8 @@ struct walk_args {
   uint64_t lane_stride;  // points per lane in the job
   uint64_t group_base;   // groups each lane already walked in this job
   uint64_t n_points;     // points in the job (indices >= n_points are not probed)
+  uint32_t interleave;   // 0: lane g owns groups [g*gpl, (g+1)*gpl); 1: groups g, g+L, g+2L, ...
+                         // (the table's last entry is then the L*2H*D jump)
   // probe target (target bloom, or BSGS layer 1 / build layer 1)
   const uint8_t *bloom;
   kh::bloom_desc bd;

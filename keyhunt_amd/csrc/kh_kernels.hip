@@ -420,7 +420,8 @@ __global__ void __launch_bounds__(256, walk_lb<MODE>()) k_walk(walk_args A) {
   load_soa(cy, A.cy, A.L, g);
 
   for (uint32_t j = 0; j < A.groups; j++) {
-    const uint64_t cidx = (uint64_t)g * A.lane_stride + (uint64_t)(A.group_base + j) * (2 * H) + H;
+    const uint64_t cidx = A.interleave ? ((A.group_base + j) * (uint64_t)A.L + g) * (2 * H) + H
+                                       : (uint64_t)g * A.lane_stride + (uint64_t)(A.group_base + j) * (2 * H) + H;
     // forward: prefix products of dx_i = T[i].x - C.x
     fe acc;
 #pragma unroll 1

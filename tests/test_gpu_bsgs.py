@@ -256,3 +256,41 @@ def test_gpu_refine_equals_host_refine(mode, oracle, monkeypatch):
     assert res[0] == res[1]
     assert sorted(res[0][0]) == [(0, keys[0]), (1, keys[1])]
     assert res[0][1][1] >= 2
+
+
+def test_bsgs_lanes_continue_across_calls(engine, oracle):
+    """Continuous mode keeps its (interleaved) lanes across kh_bsgs_scan calls whose bases follow
+    on: scanning 8 bases in one call, in 4 calls of 2, or with a jump and a target switch in
+    between gives the same first-level candidates and finds the key in the same base."""
+    n, k = 1 << 32, 2                      # M = 2^17, 32768 giant points per base: 4096-point groups
+    p = oracle.bsgs_params(n, k)
+    engine.bsgs_setup(n, k, layer1=1)
+    engine.bsgs_build()
+    start = 0x1234567890000
+    key = start + 6 * 2 * p.n + 777        # in base 6
+    q = oracle.pubkey(key)
+    engine.bsgs_set_targets([q])
+    c0 = engine.bsgs_candidates()
+    assert engine.bsgs_scan(start, 8) == [(0, key)]
+    one_call = engine.bsgs_candidates() - c0
+    for plan in ([2, 2, 2, 2], [1, 1, 3, 3], "jump"):
+        engine.bsgs_set_targets([q])
+        c0 = engine.bsgs_candidates()
+        got, b = [], 0
+        if plan == "jump":                 # an unrelated range, a second target, then back
+            engine.bsgs_scan(start + 1000 * 2 * p.n, 2)
+            engine.bsgs_set_targets([oracle.pubkey(key + 5)])
+            engine.bsgs_scan(start, 2)
+            engine.bsgs_set_targets([q])
+            c0 = engine.bsgs_candidates()
+            plan = [3, 5]
+        engine.kernel_time_reset()
+        for nb in plan:
+            got += [(b, f) for f in engine.bsgs_scan(start + b * 2 * p.n, nb)]
+            b += nb
+        assert [f for _, f in got] == [(0, key)]
+        if plan == [2, 2, 2, 2]:           # the lanes were started once, then continued
+            from keyhunt_amd.engine import TIME_SETUP
+            assert engine.kernel_time(TIME_SETUP)[0] == 1
+        assert got[0][0] + plan[-1] == 8 and 6 >= got[0][0]
+        assert engine.bsgs_candidates() - c0 == one_call, plan
