@@ -310,9 +310,11 @@ struct kh_ctx {
   // continuous BSGS lanes kept across kh_bsgs_scan calls: valid while the lane centres sit at the
   // first group of the call that would start at cont_next (same target, lanes and group size)
   bool cont_valid = false;
+  int cont_kind = 0;        // 0: BSGS giant walk (target cont_tgt), 1: kh_scan (walk mode cont_km, stride)
   u256 cont_next{};
+  u256 cont_stride{};
   uint32_t cont_L = 0, cont_tgt = 0;
-  int cont_H = 0;
+  int cont_H = 0, cont_km = 0;
   uint32_t *d_q = nullptr;  // the current BSGS target {x[8], y[8]}
   uint32_t *d_cx = nullptr, *d_cy = nullptr, *d_scalars = nullptr;
   uint4 *d_scratch = nullptr;
@@ -755,14 +757,23 @@ int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride_be[32], u
   u256 stride = stride_be ? sc_reduce(u256_from_be(stride_be)) : u256_u64(1);
   if (u256_is_zero(stride)) return KH_E_ARG;
   const uint32_t *tab = nullptr;
-  int r = get_table(ctx, stride, &tab, H);
-  if (r) return r;
+  int r;
 
   uint64_t total_groups = n_keys / (2 * H);
   job_geom jg = plan(ctx, total_groups, 0);
-  std::vector<u256> s(jg.L);
-  for (uint32_t g = 0; g < jg.L; g++) {
-    u128 off = (u128)g * jg.gpl * (2 * H) + H;
+  // large-group modes interleave lanes (lane g walks groups g, g + L, ...) when the lanes divide
+  // the chunk: after the call every lane sits on its group of the chunk that follows, so a call
+  // starting there continues them without a lane setup
+  const bool inter = H == KH_WALK_HB && (uint64_t)jg.L * jg.gpl == total_groups;
+  r = get_table(ctx, stride, &tab, H, inter ? jg.L : 1);
+  if (r) return r;
+  const bool resume = inter && ctx->cont_valid && ctx->cont_kind == 1 && ctx->cont_km == km &&
+                      ctx->cont_L == jg.L && ctx->cont_H == H && u256_cmp(ctx->cont_next, st) == 0 &&
+                      u256_cmp(ctx->cont_stride, stride) == 0;
+  ctx->cont_valid = false;
+  std::vector<u256> s(resume ? 0 : jg.L);
+  for (uint32_t g = 0; g < s.size(); g++) {
+    u128 off = inter ? (u128)g * (2 * H) + H : (u128)g * jg.gpl * (2 * H) + H;
     u256 o = sc_reduce(u256_from_u128(off));
     if (u256_cmp(stride, u256_u64(1)) != 0) {
       // o * stride mod n (o < 2^128): double-and-add over the bits of o
@@ -779,10 +790,12 @@ int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride_be[32], u
       return KH_E_ARG;
     }
   }
-  r = ensure_lanes(ctx, jg.L, H);  // the pad for H entries per lane, before the centres are set
-  if (r) return r;
-  r = run_setup(ctx, s, nullptr);
-  if (r) return r;
+  if (!resume) {
+    r = ensure_lanes(ctx, jg.L, H);  // the pad for H entries per lane, before the centres are set
+    if (r) return r;
+    r = run_setup(ctx, s, nullptr);
+    if (r) return r;
+  }
 
   walk_args A;
   memset(&A, 0, sizeof A);
@@ -792,6 +805,7 @@ int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride_be[32], u
   A.scratch = ctx->d_scratch;
   A.L = jg.L;
   A.lane_stride = jg.gpl * 2 * H;
+  A.interleave = inter ? 1 : 0;
   A.n_points = n_keys;
   A.bloom = ctx->d_tbloom;
   A.bd = ctx->tbd;
@@ -818,10 +832,40 @@ int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride_be[32], u
     ctx->hit_cap = (uint32_t)cap2;
     A.hits = ctx->d_hits;
     A.hit_cap = ctx->hit_cap;
+    if (s.empty()) {  // resumed lanes: compute their start scalars for the redo
+      s.resize(jg.L);
+      for (uint32_t g = 0; g < jg.L; g++) {
+        u128 off = (u128)g * (2 * H) + H;
+        u256 o = sc_reduce(u256_from_u128(off));
+        if (u256_cmp(stride, u256_u64(1)) != 0) {
+          u256 acc = u256_u64(0), x = stride;
+          for (int b = 0; b < 128; b++) {
+            if ((off >> b) & 1) acc = sc_add(acc, x);
+            x = sc_add(x, x);
+          }
+          o = acc;
+        }
+        s[g] = sc_add(st, o);
+      }
+    }
     r = run_setup(ctx, s, nullptr);  // the walk moved the lane centres on: start them again
     if (r) return r;
   }
   if (r) return r;
+  if (inter) {  // the lanes now sit on the chunk that starts at st + n_keys * stride
+    u256 adv = u256_u64(0), x = stride;
+    for (uint64_t k = n_keys; k; k >>= 1) {
+      if (k & 1) adv = sc_add(adv, x);
+      x = sc_add(x, x);
+    }
+    ctx->cont_valid = true;
+    ctx->cont_kind = 1;
+    ctx->cont_km = km;
+    ctx->cont_L = jg.L;
+    ctx->cont_H = H;
+    ctx->cont_stride = stride;
+    ctx->cont_next = sc_add(st, adv);
+  }
 
   // Confirm each bloom hit against the sorted table and resolve the key: parity fix-up
   // (keyhunt.cpp:3619-3636); with -e the image e gives key * lambda^e, and the 04 variants with
@@ -1725,8 +1769,8 @@ static int bsgs_scan_impl(kh_ctx *ctx, const u256 &st, const std::vector<u256> *
     const uint64_t g_end = cont ? jc.gpl : total_groups;
     uint64_t g0 = 0;
     // continuous mode: (re)start the lanes at group g0, unless the previous call left them here
-    bool need_setup = !(keep_lanes && ctx->cont_valid && ctx->cont_tgt == tgt && ctx->cont_L == jc.L &&
-                        ctx->cont_H == H && u256_cmp(ctx->cont_next, st) == 0);
+    bool need_setup = !(keep_lanes && ctx->cont_valid && ctx->cont_kind == 0 && ctx->cont_tgt == tgt &&
+                        ctx->cont_L == jc.L && ctx->cont_H == H && u256_cmp(ctx->cont_next, st) == 0);
     ctx->cont_valid = false;
     int cur = 0, pending = -1;
     bsgs_round rounds[2];
@@ -1942,6 +1986,7 @@ static int bsgs_scan_impl(kh_ctx *ctx, const u256 &st, const std::vector<u256> *
     }
     if (keep_lanes && !done && g0 == g_end) {  // every lane walked all its groups of this call
       ctx->cont_valid = true;
+      ctx->cont_kind = 0;
       ctx->cont_next = sc_add(st, sc_reduce(u256_from_u128((u128)n_bases * 2 * I.n)));
       ctx->cont_tgt = tgt;
       ctx->cont_L = jc.L;
