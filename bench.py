@@ -11,9 +11,9 @@ Metric (BASELINE.json): "Mkeys/s at 1/2/4/8 GPU (BSGS b125; addr b66); HBM GB/s 
               N_SEQUENTIAL_MAX chunk; keys counted x2 for -l compress (keyhunt.cpp:2889-2891).
   tertiary  : -m xpoint -f tests/63.pub -b 63 (configs[2]), same chunks, one key per point.
   --config 5: the primary on -m bsgs -f tests/130.txt -b 130 -k 512 (configs[4]) instead.
-Ranks split the keyspace (weak scaling, no collective on the data path): rank r of N walks chunks
-s*N + r, and its own contiguous run of BSGS base batches (r*(W+K) + s), so consecutive kh_bsgs_scan
-calls continue the same lanes.  The table build (baby steps) is replicated per GPU and not timed; its time is
+Ranks split the keyspace (weak scaling, no collective on the data path): rank r walks its own
+contiguous run of BSGS base batches and of 2^32-key chunks (r*(W+K) + s), so consecutive calls
+continue the same lanes.  The table build (baby steps) is replicated per GPU and not timed; its time is
 reported.  torch.distributed (gloo, CPU tensors) provides the barrier and the max over ranks; the
 engine owns the GPU through its own HIP stream, synchronised on both sides of the timed region.
 
@@ -211,7 +211,7 @@ def rmd160_leg(D: Dist, eng, args):
     base0 = 1 << 65
 
     def step(s):
-        c = s * D.world + D.rank
+        c = D.rank * (args.warmup_rmd + args.steps_rmd) + s  # a contiguous run of chunks per rank
         hits = eng.scan(base0 + c * chunk, chunk, K.KH_MODE_ADDRESS, K.KH_SEARCH_COMPRESS)
         assert not hits
 
@@ -231,7 +231,7 @@ def xpoint_leg(D: Dist, eng, args):
     base0 = 1 << 62
 
     def step(s):
-        c = s * D.world + D.rank
+        c = D.rank * (args.warmup_rmd + args.steps_rmd) + s  # a contiguous run of chunks per rank
         hits = eng.scan(base0 + c * chunk, chunk, K.KH_MODE_XPOINT, K.KH_SEARCH_COMPRESS)
         assert not hits
 
