@@ -1700,9 +1700,9 @@ static int bsgs_scan_impl(kh_ctx *ctx, const u256 &st, const std::vector<u256> *
   // call.  Lanes then own long runs of t, start once, and every round just continues them.
   // Otherwise (bases overlap, SURVEY parity note 13) rounds restart lanes per base run.
   const bool cont = !list && A_pts == I.aux;
-  // group half-size: continuous runs use the large groups (one inversion per 2*KH_WALK_HB points)
-  // when a base holds whole groups; per-base runs keep the reference's 1024-point group
-  const int H = (cont && A_pts % (2 * KH_WALK_HB) == 0 && !getenv("KH_NO_BIG_GROUPS")) ? KH_WALK_HB : KH_WALK_H;
+  // group half-size: the large groups (one inversion per 2*KH_WALK_HB points) whenever a base holds
+  // whole ones (every power-of-two k >= 16); otherwise the reference's 1024-point group
+  const int H = (A_pts % (2 * KH_WALK_HB) == 0 && !getenv("KH_NO_BIG_GROUPS")) ? KH_WALK_HB : KH_WALK_H;
   auto base_of = [&](uint64_t b) {
     return list ? (*list)[b] : sc_add(st, sc_reduce(u256_from_u128((u128)b * 2 * I.n)));
   };
@@ -1764,8 +1764,10 @@ static int bsgs_scan_impl(kh_ctx *ctx, const u256 &st, const std::vector<u256> *
     const ge Q = ctx->targets[tgt];
     // rounds are pipelined: the GPU walks round r+1 while the host refines round r's
     // first-level candidates
-    // per-base rounds: lanes walk 1 or 2 groups (a divisor of gpb), so rounds keep ~lanes_max lanes
-    const uint64_t round_max = (uint64_t)ctx->lanes_max * (gpb % 2 == 0 ? 2 : 1);
+    // per-base rounds (list mode, overlapping bases): up to lanes_max bases per round, each lane
+    // walking a divisor of gpb groups (plan), so large calls start one lane per base and small
+    // ones still fill ~lanes_max lanes
+    const uint64_t round_max = (uint64_t)ctx->lanes_max * gpb;
     const uint64_t g_end = cont ? jc.gpl : total_groups;
     uint64_t g0 = 0;
     // continuous mode: (re)start the lanes at group g0, unless the previous call left them here
