@@ -568,9 +568,8 @@ __global__ void __launch_bounds__(256, walk_lb<MODE>()) k_walk(walk_args A) {
 // the doubling or inverse case (scalars are < n).  One Fermat inversion per lane to go affine,
 // one more when adding Q (the BSGS target).
 // ------------------------------------------------------------------------------------------
-// s*G for a scalar s != 0 given as 8 LE u32 limbs
-__device__ __forceinline__ void comb_mult(ge &r, const uint32_t s[8], const uint32_t *__restrict__ comb) {
-  gej acc;
+// s*G for a scalar s != 0 given as 8 LE u32 limbs, left in Jacobian coordinates
+__device__ __forceinline__ void comb_mult_jac(gej &acc, const uint32_t s[8], const uint32_t *__restrict__ comb) {
   acc.inf = true;
   for (int j = 0; j < 32; j++) {
     uint32_t v = (s[j >> 2] >> ((j & 3) * 8)) & 0xFFu;
@@ -582,6 +581,10 @@ __device__ __forceinline__ void comb_mult(ge &r, const uint32_t s[8], const uint
       gej_add_ge(acc, q);
     }
   }
+}
+__device__ __forceinline__ void comb_mult(ge &r, const uint32_t s[8], const uint32_t *__restrict__ comb) {
+  gej acc;
+  comb_mult_jac(acc, s, comb);
   gej_to_ge(r, acc);
 }
 
@@ -663,46 +666,76 @@ __global__ void __launch_bounds__(64) k_refine(refine_args A) {
     A.cands[j].aux = 0;
     return;
   }
-  ge bp, Q, S;
-  comb_mult(bp, sk, A.comb);
-  fe_neg(bp.y, bp.y);
+  ge Q;
   load_fe(Q.x, A.q);
   load_fe(Q.y, A.q + 8);
-  ge_add(S, Q, bp);  // BSGS_S = Q - base_key*G (AddDirect, keyhunt.cpp:5172)
-  // S + AMP2[i], i < 32: one batched inversion; a zero difference keeps inverse 0, which is what
-  // each of the reference's AddDirect calls computes for it
-  fe pre[32];
-  fe acc;
-  fe_set_u32(acc, 1);
+  // S = Q - base_key*G (AddDirect, keyhunt.cpp:5172) kept in Jacobian coordinates (X, Y, Z): one
+  // batched inversion then serves Z and the 32 differences S - AMP2[i] (three inversions before)
+  gej S;
+  comb_mult_jac(S, sk, A.comb);
+  fe_neg(S.y, S.y);
+  {
+    fe z2, u2, h;  // h = Q.x*Z^2 - X: zero iff Q = +-base_key*G, the AddDirect dx = 0 case
+    fe_sqr(z2, S.z);
+    fe_mul(u2, Q.x, z2);
+    fe_sub(h, u2, S.x);
+    if (fe_is_zero(h)) {  // reproduce AddDirect's inverse-0 value on the affine path (rare)
+      ge bp, Sa;
+      gej_to_ge(bp, S);
+      ge_add(Sa, Q, bp);
+      S.x = Sa.x;
+      S.y = Sa.y;
+      fe_set_u32(S.z, 1);
+    } else {
+      gej_add_ge(S, Q);
+    }
+  }
+  // e_i = AMP2[i].x * Z^2 - X = (AMP2[i].x - S.x) * Z^2: zero exactly when the reference's dx is,
+  // and then (as there) its inverse counts as 0.  Prefix products over Z, e_0, ..., e_31.
+  fe z2, pre[32], acc;
+  fe_sqr(z2, S.z);
+  acc = S.z;
   for (int i = 0; i < 32; i++) {
-    fe ax, dx;
+    fe ax, e;
     load_fe(ax, A.amp2 + i * 16);
-    fe_sub(dx, ax, S.x);
-    if (!fe_is_zero(dx)) fe_mul(acc, acc, dx);
+    fe_mul(e, ax, z2);
+    fe_sub(e, e, S.x);
+    if (!fe_is_zero(e)) fe_mul(acc, acc, e);
     pre[i] = acc;
   }
   fe inv;
   fe_inv(inv, acc);
+  // backward: 1/e_i for i = 31..0 (into pre[i], whose prefix is no longer needed), then 1/Z
+  for (int i = 31; i >= 0; i--) {
+    fe ax, e, d;
+    load_fe(ax, A.amp2 + i * 16);
+    fe_mul(e, ax, z2);
+    fe_sub(e, e, S.x);
+    if (fe_is_zero(e)) {
+      fe_set_u32(d, 0);
+    } else {
+      d = i == 0 ? S.z : pre[i - 1];
+      fe_mul(d, d, inv);
+      fe_mul(inv, inv, e);
+    }
+    pre[i] = d;
+  }
+  // inv = 1/Z now: affine S
+  fe zi2, zi3, sx, sy;
+  fe_sqr(zi2, inv);
+  fe_mul(zi3, zi2, inv);
+  fe_mul(sx, S.x, zi2);
+  fe_mul(sy, S.y, zi3);
   uint32_t mask = 0;
   for (int i = 31; i >= 0; i--) {
-    fe ax, ay, dx, di, dy, s, x;
+    fe ax, ay, di, dy, s, x;
     load_fe(ax, A.amp2 + i * 16);
     load_fe(ay, A.amp2 + i * 16 + 8);
-    fe_sub(dx, ax, S.x);
-    if (fe_is_zero(dx)) {
-      fe_set_u32(di, 0);
-    } else {
-      if (i == 0)
-        fe_set_u32(di, 1);
-      else
-        di = pre[i - 1];
-      fe_mul(di, di, inv);
-      fe_mul(inv, inv, dx);
-    }
-    fe_sub(dy, ay, S.y);
+    fe_mul(di, pre[i], z2);  // 1/dx = Z^2/e (0 stays 0)
+    fe_sub(dy, ay, sy);
     fe_mul(s, dy, di);
     fe_sqr(x, s);
-    fe_sub(x, x, S.x);
+    fe_sub(x, x, sx);
     fe_sub(x, x, ax);
     uint64_t in[4];
     x_bytes_u64(x, in);

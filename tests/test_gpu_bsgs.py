@@ -220,13 +220,16 @@ def test_second_check_masks_gpu_equal_host(engine, oracle):
     near = [key - rnd.randrange(0, 2 * p.m) for _ in range(600)]
     far = [rnd.getrandbits(255) for _ in range(400)]
     edge = [key, key - 2 * p.m, key - 2 * p.m + 1, 1, SECP_N - 1, 0]
-    bases = near + far + edge
+    # S = Q - base*G = +-AMP2[i]: the reference's AddDirect with dx = 0 (inverse taken as 0)
+    amp = [key + s * p.m2 * (1 + 2 * i) for i in (0, 5, 31) for s in (1, -1)]
+    bases = near + far + edge + amp
     g, h = engine.bsgs_second_masks(0, bases)
     assert g == h
     hits = [m for m in g[: len(near)] if m]
     assert len(hits) >= 590   # d in [1, 2M): the AMP2 step covering d hits layer 2
     assert all(bin(m).count("1") <= 2 for m in hits)
     assert g[len(near) + len(far) + 5] == 0  # base key 0: no point
+    assert len(g) == len(bases)
 
 
 @pytest.mark.parametrize("mode", ["continuous", "per_base", "list"])
