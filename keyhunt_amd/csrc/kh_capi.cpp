@@ -340,6 +340,8 @@ struct kh_ctx {
   uint64_t t_entries = 0;  // the target bloom's struct bloom `entries`
   std::vector<uint8_t> h_tbloom;
   uint8_t *d_tbloom = nullptr;
+  uint4 *d_tblk = nullptr;  // blocked target filter (exact targets only)
+  uint32_t tblocks = 0;
 
   // bsgs
   uint32_t l1_layout = KH_LAYER1_BLOCKED;
@@ -403,6 +405,7 @@ kh_ctx::~kh_ctx() {
   (void)hipFree(d_hit_count);
   (void)hipFree(d_hits);
   (void)hipFree(d_tbloom);
+  (void)hipFree(d_tblk);
   for (int i = 0; i < 3; i++) (void)hipFree(d_bl[i]);
   (void)hipFree(d_amp2);
   (void)hipFree(d_ref_start);
@@ -688,6 +691,32 @@ int kh_synchronize(kh_ctx *ctx) {
 // ---------------------------------------------------------------------------------------------
 // address / rmd160 / xpoint
 // ---------------------------------------------------------------------------------------------
+// The blocked target filter the walk probes for exact targets (kh_kernels.hip tblk_probe): 16-byte
+// blocks, KH_BLK_BITS_MUL x the reference bloom's bits; row words w = little-endian u32s of the
+// 20 bytes: block (w0 * blocks) >> 32, bits from 5-bit fields of w1, w2, w3 as blk_masks.
+static int upload_tblk(kh_ctx *c) {
+  const uint64_t blocks = (c->tbd.bits * KH_BLK_BITS_MUL + 127) / 128;
+  std::vector<uint32_t> words(blocks * 4, 0);
+  for (uint64_t r = 0; r < c->n_rows; r++) {
+    const uint8_t *p = &c->rows[r * 20];
+    uint32_t w[4];
+    for (int k = 0; k < 4; k++)
+      w[k] = (uint32_t)p[4 * k] | ((uint32_t)p[4 * k + 1] << 8) | ((uint32_t)p[4 * k + 2] << 16) |
+             ((uint32_t)p[4 * k + 3] << 24);
+    const uint64_t blk = ((uint64_t)w[0] * blocks) >> 32;
+    for (int t = 0; t < 16; t++) {
+      const uint32_t src = w[1 + t / 6];
+      words[blk * 4 + t / 4] |= 1u << ((src >> (5 * (t % 6))) & 31u);
+    }
+  }
+  (void)hipFree(c->d_tblk);
+  c->d_tblk = nullptr;
+  c->tblocks = (uint32_t)blocks;
+  HIPCHK(c, hipMalloc(&c->d_tblk, words.size() * 4));
+  HIPCHK(c, hipMemcpy(c->d_tblk, words.data(), words.size() * 4, hipMemcpyHostToDevice));
+  return KH_OK;
+}
+
 int kh_set_targets(kh_ctx *ctx, const uint8_t *rows, uint64_t n, uint64_t bloom_items) {
   if (!ctx || (!rows && n)) return KH_E_ARG;
   (void)hipSetDevice(ctx->device);
@@ -710,7 +739,7 @@ int kh_set_targets(kh_ctx *ctx, const uint8_t *rows, uint64_t n, uint64_t bloom_
   ctx->d_tbloom = nullptr;
   HIPCHK(ctx, hipMalloc(&ctx->d_tbloom, ctx->tbd.bytes + 4));
   HIPCHK(ctx, hipMemcpy(ctx->d_tbloom, ctx->h_tbloom.data(), ctx->tbd.bytes, hipMemcpyHostToDevice));
-  return KH_OK;
+  return upload_tblk(ctx);
 }
 
 int kh_set_vanity(kh_ctx *ctx, const uint8_t *ranges, uint64_t n, uint32_t probe_len, uint64_t bloom_items) {
@@ -721,6 +750,8 @@ int kh_set_vanity(kh_ctx *ctx, const uint8_t *ranges, uint64_t n, uint32_t probe
   ctx->n_rows = 0;
   ctx->vanity = true;
   ctx->probe_len = probe_len;
+  (void)hipFree(ctx->d_tblk);  // prefixes probe the reference-layout bloom
+  ctx->d_tblk = nullptr;
   // processOneVanity / readFileVanity (keyhunt.cpp:6970-7035): bloom over A's first probe_len bytes
   ctx->t_entries = bloom_entries(bloom_items ? bloom_items : n);
   ctx->tbd = bloom_size(ctx->t_entries);
@@ -730,7 +761,7 @@ int kh_set_vanity(kh_ctx *ctx, const uint8_t *ranges, uint64_t n, uint32_t probe
   ctx->d_tbloom = nullptr;
   HIPCHK(ctx, hipMalloc(&ctx->d_tbloom, ctx->tbd.bytes + 4));
   HIPCHK(ctx, hipMemcpy(ctx->d_tbloom, ctx->h_tbloom.data(), ctx->tbd.bytes, hipMemcpyHostToDevice));
-  return KH_OK;
+  return upload_tblk(ctx);
 }
 
 int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride_be[32], uint64_t n_keys, uint32_t mode,
@@ -809,6 +840,8 @@ int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride_be[32], u
   A.n_points = n_keys;
   A.bloom = ctx->d_tbloom;
   A.bd = ctx->tbd;
+  A.tblk = ctx->vanity || getenv("KH_REF_TARGET_BLOOM") ? nullptr : ctx->d_tblk;
+  A.tblocks = ctx->tblocks;
   A.hit_count = ctx->d_hit_count;
   A.hits = ctx->d_hits;
   A.hit_cap = ctx->hit_cap;

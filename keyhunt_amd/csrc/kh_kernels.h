@@ -87,6 +87,10 @@ struct walk_args {
   kh_dev_hit *hits;
   uint32_t hit_cap;
   uint32_t probe_len;  // hash160 modes: bytes of the hash the bloom keys on (20; vanity: the prefix length)
+  // exact targets: the blocked target filter probed instead of the reference-layout bloom (see
+  // kh_kernels.hip tblk_probe); null for vanity prefixes
+  const uint4 *tblk;
+  uint32_t tblocks;
   // BSGS build
   uint8_t *bl1, *bl2, *bl3;
   kh::bloom_desc bd2, bd3;

@@ -155,9 +155,20 @@ __device__ __forceinline__ void x_bytes_u64(const fe &x, uint64_t in[4]) {
     in[k] = (uint64_t)bswap32(x.d[7 - 2 * k]) | ((uint64_t)bswap32(x.d[6 - 2 * k]) << 32);
 }
 
+// Exact 20-byte targets (hash160, X[0..20), eth address) are uniform, so they go to a split-block
+// filter keyed on their own words, like the blocked BSGS layer 1: with w = the little-endian u32s
+// of the 20 bytes, the 16-byte block is (w0 * blocks) >> 32 and the bit positions are 5-bit fields
+// of w1, w2, w3 (blk_masks).  One 16-B load, no XXH64.  Every filter hit is still confirmed by the
+// host's exact table search (searchbinary), so the reported hits are the reference's.
+__device__ __forceinline__ bool tblk_probe(const walk_args &A, const uint32_t w[5]) {
+  const uint32_t blk = (uint32_t)(((uint64_t)w[0] * A.tblocks) >> 32);
+  return blk_match(A.tblk[blk], w[1], w[2], w[3]);
+}
+
 // one 20-byte hash into the target bloom: the whole hash (address/rmd160), or its first
 // A.probe_len bytes (vanity prefixes, vanityrmdmatch keyhunt.cpp:6677-6703)
 __device__ __forceinline__ bool probe_h160(const walk_args &A, const uint32_t h[5]) {
+  if (A.tblk) return tblk_probe(A, h);
   if (A.probe_len == 20) {
     const uint64_t a = xxh64_20(h, KH_BLOOM_SEED);
     return bloom_probe_lazy(A.bloom, A.bd, a, [&](uint64_t s) { return xxh64_20(h, s); });
@@ -198,6 +209,10 @@ __device__ __forceinline__ void probe_xpoint(const walk_args &A, const fe &x, ui
   uint32_t w[5];
 #pragma unroll
   for (int j = 0; j < 5; j++) w[j] = bswap32(x.d[7 - j]);
+  if (A.tblk) {
+    if (tblk_probe(A, w)) record_hit(A, idx, 3 | tag);
+    return;
+  }
   uint64_t a = xxh64_20(w, KH_BLOOM_SEED);
   if (bloom_probe_lazy(A.bloom, A.bd, a, [&](uint64_t s) { return xxh64_20(w, s); })) record_hit(A, idx, 3 | tag);
 }
@@ -215,6 +230,10 @@ __device__ __forceinline__ void endo_beta(fe &b, int e) {
 __device__ __forceinline__ void probe_eth(const walk_args &A, const fe &x, const fe &y, uint64_t idx) {
   uint32_t w[5];
   eth_address(x, y, w);
+  if (A.tblk) {
+    if (tblk_probe(A, w)) record_hit(A, idx, 5);
+    return;
+  }
   uint64_t a = xxh64_20(w, KH_BLOOM_SEED);
   if (bloom_probe_lazy(A.bloom, A.bd, a, [&](uint64_t s) { return xxh64_20(w, s); })) record_hit(A, idx, 5);
 }
