@@ -124,7 +124,9 @@ int kh_set_targets(kh_ctx *ctx, const uint8_t *rows, uint64_t n, uint64_t bloom_
  * kh_set_targets switches back to exact targets. */
 int kh_set_vanity(kh_ctx *ctx, const uint8_t *ranges, uint64_t n, uint32_t probe_len, uint64_t bloom_items);
 /* Scan keys start + i*stride, i in [0, n_keys) (n_keys a multiple of 1024; stride NULL -> 1).
- * Returns the confirmed hits in the order one reference thread prints them. */
+ * Returns the confirmed hits in the order one reference thread prints them.  A call that starts
+ * where the previous kh_scan of this context ended (same mode, stride and n_keys) reuses its
+ * lanes instead of starting them again: sequential chunks are cheaper, results are the same. */
 int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride[32], uint64_t n_keys, uint32_t mode,
             uint32_t search, kh_hit *hits, uint32_t cap, uint32_t *n_hits);
 
@@ -156,7 +158,8 @@ int kh_targets_load(kh_ctx *ctx, const char *path, uint32_t flags);
 /* targets: n x {x[32], y[32]} affine points (big-endian) */
 int kh_bsgs_set_targets(kh_ctx *ctx, const uint8_t *xy, uint32_t n);
 /* Walk n_bases bases start, start + 2N, ... for every target not yet found.  Keys already found
- * are skipped (like bsgs_found[]).  found: keys found by THIS call. */
+ * are skipped (like bsgs_found[]).  found: keys found by THIS call.  With one target, a call that
+ * starts at the base after the previous call's last one (same n_bases) continues its lanes. */
 int kh_bsgs_scan(kh_ctx *ctx, const uint8_t start[32], uint64_t n_bases, kh_bsgs_found *found, uint32_t cap,
                  uint32_t *n_found);
 /* Same for an arbitrary list of bases (n_bases x 32-byte big-endian keys), e.g. the -B backward /
