@@ -438,6 +438,10 @@ __global__ void __launch_bounds__(256, walk_lb<MODE>()) k_walk(walk_args A) {
   load_soa(cx, A.cx, A.L, g);
   load_soa(cy, A.cy, A.L, g);
 
+  // BSGS walks keep only the even prefix products in the pad and rebuild each odd one with one
+  // multiplication in the backward pass: half the pad traffic for +1/2 multiplication per pair
+  constexpr bool SPARSE = MODE == KM_BSGSB || MODE == KM_BSGS;
+  auto slot = [&](int m) { return (size_t)(SPARSE ? (m >> 1) : m) * L + g; };
   for (uint32_t j = 0; j < A.groups; j++) {
     const uint64_t cidx = A.interleave ? ((A.group_base + j) * (uint64_t)A.L + g) * (2 * H) + H
                                        : (uint64_t)g * A.lane_stride + (uint64_t)(A.group_base + j) * (2 * H) + H;
@@ -452,7 +456,7 @@ __global__ void __launch_bounds__(256, walk_lb<MODE>()) k_walk(walk_args A) {
         acc = dx;
       else
         fe_mul(acc, acc, dx);
-      scr_store(scr, (size_t)i * L + g, acc);
+      if (!SPARSE || (i & 1) == 0) scr_store(scr, slot(i), acc);
     }
     fe t2x, t2y, dxn;
     load_fe_k(t2x, T + H * 16);
@@ -477,7 +481,7 @@ __global__ void __launch_bounds__(256, walk_lb<MODE>()) k_walk(walk_args A) {
     uint64_t poff = 0;
     uint32_t plive = 0;
     fe pre;
-    scr_load(pre, scr, (size_t)(H - 2) * L + g);
+    scr_load(pre, scr, slot(H - 2));
 #pragma unroll 1
     for (int i = H - 1; i >= 0; i--) {
       fe tx, ty, di;
@@ -485,9 +489,15 @@ __global__ void __launch_bounds__(256, walk_lb<MODE>()) k_walk(walk_args A) {
       load_fe_k(ty, T + i * 16 + 8);
       if (i > 0) {
         fe dx;
+        if (SPARSE && ((i - 1) & 1)) {  // prefix[i-1] = prefix[i-2] * dx[i-1] (pre holds prefix[i-2])
+          fe tpx, d1;
+          load_fe_k(tpx, T + (i - 1) * 16);
+          fe_sub(d1, tpx, cx);
+          fe_mul(pre, pre, d1);
+        }
         fe_mul(di, inv, pre);
         // refill `pre` for the next step right after its last use (no register copy)
-        if (i > 1) scr_load(pre, scr, (size_t)(i - 2) * L + g);
+        if (i > 1) scr_load(pre, scr, slot(i - 2));
         fe_sub(dx, tx, cx);
         fe_mul(inv, inv, dx);
       } else {
