@@ -623,14 +623,27 @@ __global__ void __launch_bounds__(256) k_setup(setup_args A) {
   uint32_t s[8];  // 8 LE u32 limbs
 #pragma unroll
   for (int i = 0; i < 8; i++) s[i] = A.scalars[(size_t)g * 8 + i];
+  gej acc;
+  comb_mult_jac(acc, s, A.comb);
   ge r;
-  comb_mult(r, s, A.comb);
-  if (A.has_q) {
+  if (A.has_q) {  // Q + s*G in Jacobian coordinates: one inversion per lane instead of two
     ge q;
     load_fe(q.x, A.q);
     load_fe(q.y, A.q + 8);
-    ge_add(r, q, r);
+    fe z2, u2, h;  // h = Q.x*Z^2 - X: zero iff Q = +-s*G (AddDirect's dx = 0 case)
+    fe_sqr(z2, acc.z);
+    fe_mul(u2, q.x, z2);
+    fe_sub(h, u2, acc.x);
+    if (fe_is_zero(h)) {  // the affine AddDirect value, inverse of 0 taken as 0 (rare)
+      gej_to_ge(r, acc);
+      ge_add(r, q, r);
+      store_soa(A.cx, A.L, g, r.x);
+      store_soa(A.cy, A.L, g, r.y);
+      return;
+    }
+    gej_add_ge(acc, q);
   }
+  gej_to_ge(r, acc);
   store_soa(A.cx, A.L, g, r.x);
   store_soa(A.cy, A.L, g, r.y);
 }
