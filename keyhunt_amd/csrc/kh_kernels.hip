@@ -594,8 +594,8 @@ __global__ void __launch_bounds__(256, walk_lb<MODE>()) k_walk(walk_args A) {
 // Lane setup: C_g = [Q +] s_g * G with a fixed-base byte comb, comb[j][v] = v * 2^(8j) * G.
 // Bytes are added from least to most significant, so the accumulator is always (partial
 // scalar)*G with partial < 2^(8j) while comb[j][v] >= 2^(8j): the mixed addition never meets
-// the doubling or inverse case (scalars are < n).  One Fermat inversion per lane to go affine,
-// one more when adding Q (the BSGS target).
+// the doubling or inverse case (scalars are < n).  One Fermat inversion per lane to go affine;
+// Q (the BSGS target) is added in Jacobian coordinates before it.
 // ------------------------------------------------------------------------------------------
 // s*G for a scalar s != 0 given as 8 LE u32 limbs, left in Jacobian coordinates
 __device__ __forceinline__ void comb_mult_jac(gej &acc, const uint32_t s[8], const uint32_t *__restrict__ comb) {
