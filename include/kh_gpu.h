@@ -203,6 +203,10 @@ int kh_bsgs_second_masks(kh_ctx *ctx, uint32_t target, const uint8_t *base_keys,
                          uint32_t *host_mask);
 /* sorted bP table as the reference's 16-byte bsgs_xvalue rows {value[6], pad[2], index u64 LE} */
 int kh_get_bsgs_table(kh_ctx *ctx, uint8_t *buf, uint64_t cap_rows, uint64_t *rows);
+/* --ptable FILE --load-ptable (keyhunt.cpp:1847-1956): after kh_bsgs_build (or _load), replace the
+ * sorted bP table with n_rows = M3 rows of the same 16-byte layout taken from the reference's raw
+ * table file.  The rows are used as given, as the reference's read-only mapping is. */
+int kh_bsgs_set_table(kh_ctx *ctx, const uint8_t *rows, uint64_t n_rows);
 
 #ifdef __cplusplus
 }

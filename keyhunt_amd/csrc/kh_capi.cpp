@@ -2341,4 +2341,18 @@ int kh_get_bsgs_table(kh_ctx *ctx, uint8_t *buf, uint64_t cap_rows, uint64_t *ro
   return KH_OK;
 }
 
+// --load-ptable (keyhunt.cpp:1871-1892): the rows come from the caller's file, as the reference's
+// mapping of that file replaces the table thread_bPload would have written (5404, 5587).  Like
+// the reference, the rows are taken as they are: neither checked nor re-sorted.
+int kh_bsgs_set_table(kh_ctx *ctx, const uint8_t *rows, uint64_t n_rows) {
+  if (!ctx || !rows) return KH_E_ARG;
+  if (!ctx->bsgs_built) return KH_E_STATE;
+  if (n_rows != ctx->info.m3) {
+    ctx->err = "bP table rows " + std::to_string(n_rows) + " != M3 " + std::to_string(ctx->info.m3);
+    return KH_E_ARG;
+  }
+  ctx->h_rows.assign(rows, rows + n_rows * 16);
+  return KH_OK;
+}
+
 }  // extern "C"

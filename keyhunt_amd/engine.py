@@ -108,6 +108,7 @@ def lib() -> ctypes.CDLL:
     L.kh_bloom_check.argtypes = [P, ctypes.c_uint32, u8p, ctypes.c_uint32, ctypes.c_uint32, u8p]
     L.kh_get_bloom.argtypes = [P, ctypes.c_uint32, u8p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]
     L.kh_get_bsgs_table.argtypes = [P, u8p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]
+    L.kh_bsgs_set_table.argtypes = [P, u8p, ctypes.c_uint64]
     _lib = L
     return L
 
@@ -316,3 +317,7 @@ class Engine:
         buf = ctypes.create_string_buffer(16 * n.value)
         self._chk(lib().kh_get_bsgs_table(self._ctx, buf, n.value, ctypes.byref(n)), "kh_get_bsgs_table")
         return buf.raw
+
+    def set_bsgs_table(self, rows: bytes) -> None:
+        """--load-ptable: use these 16-byte rows as the bP table (keyhunt.cpp:1871-1892)."""
+        self._chk(lib().kh_bsgs_set_table(self._ctx, rows, len(rows) // 16), "kh_bsgs_set_table")

@@ -11,12 +11,15 @@
 // -m vanity, and -S / -6 (the BSGS table files and the address/rmd160/xpoint data_<hex>.dat target
 // cache, in the reference's formats) and -B ggsb / --bsgs-block-count / --bsgs-block-size are
 // provided; minikeys are rejected.
+#include <ctype.h>
+#include <fcntl.h>
 #include <getopt.h>
 #include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/stat.h>
 #include <time.h>
 #include <unistd.h>
 
@@ -160,6 +163,10 @@ struct options {
   // GGSB (keyhunt.cpp:1477-1499, 1617-1627): -B ggsb or --bsgs-block-count/--bsgs-block-size
   bool ggsb = false;
   uint64_t ggsb_count = 0, ggsb_size = 0;
+  // --ptable FILE / --ptable-size S / --load-ptable (keyhunt.cpp:772-787, 1847-1956)
+  const char *ptable = nullptr;
+  uint64_t ptable_size = 0;
+  bool load_ptable = false;
 } opt;
 // keyhunt.cpp:419; ggsb and angrygiant walk like sequential (ggsb with BSGS_STEP = 2 x block size)
 const char *BSGS_MODES[7] = {"sequential", "backward", "both", "random", "dance", "ggsb", "angrygiant"};
@@ -592,6 +599,77 @@ bool take_bases(const U &twoN, uint64_t want, std::vector<U> &out) {
   return !out.empty();
 }
 
+// --ptable FILE (keyhunt.cpp:1847-1956): the reference maps FILE (grown to max(M3 x 16 B,
+// --ptable-size), never shrunk) as its bP table, so the baby-step workers (or -S's .tbl read) leave
+// the sorted rows in it.  The rows are built on the GPU here, and the first worker writes them.
+// With --load-ptable the existing FILE is mapped read-only and its first M3 rows are the table.
+int bsgs_ptable(kh_ctx *ctx, const kh_bsgs_info &info, bool first) {
+  if (!opt.ptable) return KH_OK;
+  const uint64_t bytes = info.m3 * 16;
+  std::vector<uint8_t> rows(bytes);
+  if (opt.load_ptable) {
+    FILE *f = fopen(opt.ptable, "rb");
+    if (!f) {
+      fprintf(stderr, "[E] Cannot open bP table file\n");
+      return KH_E_IO;
+    }
+    struct stat st;
+    if (fstat(fileno(f), &st) != 0) {
+      fclose(f);
+      fprintf(stderr, "[E] Cannot stat bP table file\n");
+      return KH_E_IO;
+    }
+    if ((uint64_t)st.st_size < bytes) {
+      fclose(f);
+      fprintf(stderr, "[E] Existing bP table file too small\n");
+      return KH_E_IO;
+    }
+    bool ok = bytes == 0 || fread(rows.data(), bytes, 1, f) == 1;
+    fclose(f);
+    if (!ok) {
+      fprintf(stderr, "[E] Cannot read bP table file\n");
+      return KH_E_IO;
+    }
+    int r = kh_bsgs_set_table(ctx, rows.data(), info.m3);
+    if (r) fprintf(stderr, "[E] %s\n", kh_last_error(ctx));
+    return r;
+  }
+  if (!first) return KH_OK;
+  uint64_t got = 0;
+  int r = kh_get_bsgs_table(ctx, rows.data(), info.m3, &got);
+  if (r) return r;
+  const uint64_t map_bytes = std::max(bytes, opt.ptable_size);
+  int fd = open(opt.ptable, O_RDWR | O_CREAT, 0600);
+  if (fd < 0) {
+    fprintf(stderr, "[E] Cannot create bP table file\n");
+    return KH_E_IO;
+  }
+  struct stat st;
+  bool ok = fstat(fd, &st) == 0;
+  if (ok && (uint64_t)st.st_size < map_bytes) ok = ftruncate(fd, (off_t)map_bytes) == 0;
+  if (!ok) {
+    close(fd);
+    fprintf(stderr, "[E] Cannot resize bP table file\n");
+    return KH_E_IO;
+  }
+  // mappings under 1 MiB are zeroed first (keyhunt.cpp:1941-1951); larger ones keep their bytes
+  if (map_bytes < (1ull << 20)) {
+    std::vector<uint8_t> zero(map_bytes, 0);
+    ok = pwrite(fd, zero.data(), map_bytes, 0) == (ssize_t)map_bytes;
+  }
+  for (uint64_t o = 0; ok && o < bytes;) {
+    ssize_t w = pwrite(fd, rows.data() + o, bytes - o, (off_t)o);
+    ok = w > 0;
+    if (ok) o += (uint64_t)w;
+  }
+  ok = close(fd) == 0 && ok;
+  if (!ok) {
+    fprintf(stderr, "[E] Cannot write bP table file\n");
+    return KH_E_IO;
+  }
+  return KH_OK;
+}
+
 // -S (keyhunt.cpp:1983-2230, 2504-2652): the files of this N/k in the working directory are read
 // when they are all there, else the tables are built and (by the first GPU's worker) written.
 int bsgs_tables(kh_ctx *ctx, const kh_bsgs_info &info, bool first) {
@@ -651,6 +729,7 @@ void bsgs_worker(bsgs_job *j) {
   r = kh_bsgs_set_layer1(ctx, opt.layer1);
   if (!r) r = kh_bsgs_setup(ctx, j->n, j->k, &info);
   if (!r) r = bsgs_tables(ctx, info, j->first);
+  if (!r) r = bsgs_ptable(ctx, info, j->first);
   size_t nt = j->tx->size();
   std::vector<uint8_t> xy(64 * nt);
   for (size_t i = 0; i < nt; i++) {
@@ -741,6 +820,10 @@ int main(int argc, char **argv) {
   u_from_hex(ORDER_HEX, order);
   static const struct option long_opts[] = {{"bsgs-block-count", required_argument, 0, 1},
                                            {"bsgs-block-size", required_argument, 0, 2},
+                                           {"ptable", required_argument, 0, 3},
+                                           {"ptable-size", required_argument, 0, 4},
+                                           {"load-ptable", no_argument, 0, 5},
+                                           {"ptable-cache", no_argument, 0, 6},
                                            {0, 0, 0, 0}};
   while ((c = getopt_long(argc, argv, "m:f:l:r:b:k:n:t:g:qs:I:L:MRec:B:S6v:z:dh", long_opts, nullptr)) != -1) {
     switch (c) {
@@ -752,6 +835,25 @@ int main(int argc, char **argv) {
         opt.ggsb_size = strtoull(optarg, NULL, 10);
         opt.ggsb = opt.ggsb_size > 0;
         break;
+      case 3: opt.ptable = optarg; break;  // keyhunt.cpp:772-773
+      case 4: {                            // keyhunt.cpp:774-785
+        char *end;
+        uint64_t v = strtoull(optarg, &end, 10);
+        if (*end) {
+          switch (tolower(*end)) {
+            case 'k': v *= 1024ull; break;
+            case 'm': v *= 1024ull * 1024ull; break;
+            case 'g': v *= 1024ull * 1024ull * 1024ull; break;
+            case 't': v *= 1024ull * 1024ull * 1024ull * 1024ull; break;
+          }
+        }
+        opt.ptable_size = v;
+        break;
+      }
+      case 5: opt.load_ptable = true; break;  // keyhunt.cpp:786-787
+      case 6:
+        fprintf(stderr, "[E] --ptable-cache (the MD5 / bucket cache files) is not supported by this engine\n");
+        return EXIT_FAILURE;
       case 'm': {
         int m = -1;
         for (int i = 0; i < 5; i++)
@@ -870,6 +972,10 @@ int main(int argc, char **argv) {
         return EXIT_SUCCESS;
       default: usage(argv[0]); return EXIT_FAILURE;
     }
+  }
+  if (opt.load_ptable && !opt.ptable) {  // keyhunt.cpp:1126-1129
+    fprintf(stderr, "--load-ptable requires --ptable <file>\n");
+    return EXIT_FAILURE;
   }
   if (opt.mode == MODE_BSGS) printf("[+] Mode BSGS %s\n", BSGS_MODES[opt.bsgs_mode]);  // keyhunt.cpp:1209-1211
   if (!opt.file && !(opt.mode == MODE_VANITY && opt.vanity.targets)) {
