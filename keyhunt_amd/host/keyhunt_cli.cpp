@@ -167,6 +167,7 @@ struct options {
   const char *ptable = nullptr;
   uint64_t ptable_size = 0;
   bool load_ptable = false;
+  bool ptable_cache = false;  // --ptable-cache: FILE.md5 + FILE.cache (keyhunt.cpp:1958-1981, 2655-2700)
 } opt;
 // keyhunt.cpp:419; ggsb and angrygiant walk like sequential (ggsb with BSGS_STEP = 2 x block size)
 const char *BSGS_MODES[7] = {"sequential", "backward", "both", "random", "dance", "ggsb", "angrygiant"};
@@ -599,6 +600,90 @@ bool take_bases(const U &twoN, uint64_t want, std::vector<U> &out) {
   return !out.empty();
 }
 
+// --ptable-cache: FILE.md5 holds the file's MD5 as hex text; FILE.cache the 257 bucket starts of
+// the rows by value[0] under that MD5 (struct bptable_cache_file, keyhunt.cpp:137-143, 186-241).
+// With --load-ptable an existing FILE.md5 is trusted (1958-1981); otherwise the MD5 is computed
+// from the file and written.  A cache file of another MD5 or size is rebuilt (2655-2700).  Only
+// the files are produced: the engine's third check does not need the buckets.
+void ptable_cache(const std::vector<uint8_t> &rows, uint64_t m3, bool loaded) {
+  if (!opt.ptable_cache) return;
+  const std::string md5_path = std::string(opt.ptable) + ".md5", cache_path = std::string(opt.ptable) + ".cache";
+  uint8_t md5[16];
+  bool ready = false;
+  auto write_md5 = [&]() {
+    FILE *f = fopen(md5_path.c_str(), "w");
+    bool ok = f && fprintf(f, "%s\n", hex(md5, 16).c_str()) > 0;
+    if (f) fclose(f);
+    if (!ok) fprintf(stderr, "[W] Unable to write bP table MD5 file %s\n", md5_path.c_str());
+  };
+  if (loaded) {
+    char buf[64] = {0};
+    FILE *f = fopen(md5_path.c_str(), "r");
+    if (f) {
+      size_t n = fread(buf, 1, sizeof buf - 1, f);
+      fclose(f);
+      buf[n] = 0;
+      if (char *nl = strchr(buf, '\n')) *nl = 0;
+      if (strlen(buf) >= 32) {
+        buf[32] = 0;
+        ready = hex2bin(buf, md5, 16);
+      }
+    }
+    if (ready) printf("[+] bP table MD5 loaded (%s)\n", md5_path.c_str());
+  }
+  if (!ready) {
+    ready = md5_of_file(opt.ptable, md5);
+    if (ready)
+      write_md5();
+    else
+      fprintf(stderr, "[W] Unable to compute MD5 for bP table %s\n", opt.ptable);
+  }
+  if (!ready) return;
+#pragma pack(push, 1)
+  struct {
+    uint32_t magic, version;
+    uint64_t entries;
+    uint8_t md5[16];
+    uint64_t boundaries[257];
+  } fc, disk;
+#pragma pack(pop)
+  static_assert(sizeof(fc) == 2088, "struct bptable_cache_file");
+  int status = 0;
+  if (FILE *f = fopen(cache_path.c_str(), "rb")) {
+    if (fread(&disk, sizeof disk, 1, f) == 1)
+      status = disk.magic == 0x42505443u && disk.version == 1 && disk.entries == m3 && !memcmp(disk.md5, md5, 16)
+                   ? 1
+                   : -1;
+    fclose(f);
+  }
+  if (status == 1) {
+    printf("[+] bP table cache hit (%s)\n", cache_path.c_str());
+    return;
+  }
+  if (status < 0)
+    printf("[W] bP table cache mismatch (%s); rebuilding\n", cache_path.c_str());
+  else
+    printf("[I] bP table cache not found (%s); creating\n", cache_path.c_str());
+  memset(&fc, 0, sizeof fc);
+  fc.magic = 0x42505443u;  // 'BPTC'
+  fc.version = 1;
+  fc.entries = m3;
+  memcpy(fc.md5, md5, 16);
+  uint64_t pos = 0;
+  for (int bucket = 0; bucket < 256; bucket++) {
+    while (pos < m3 && rows[pos * 16] < bucket) pos++;
+    fc.boundaries[bucket] = pos;
+  }
+  fc.boundaries[256] = m3;
+  FILE *f = fopen(cache_path.c_str(), "wb");
+  bool ok = f && fwrite(&fc, sizeof fc, 1, f) == 1;
+  if (f) fclose(f);
+  if (ok)
+    printf("[+] bP table cache refreshed (%s)\n", cache_path.c_str());
+  else
+    printf("[W] Unable to write bP table cache to %s\n", cache_path.c_str());
+}
+
 // --ptable FILE (keyhunt.cpp:1847-1956): the reference maps FILE (grown to max(M3 x 16 B,
 // --ptable-size), never shrunk) as its bP table, so the baby-step workers (or -S's .tbl read) leave
 // the sorted rows in it.  The rows are built on the GPU here, and the first worker writes them.
@@ -631,8 +716,12 @@ int bsgs_ptable(kh_ctx *ctx, const kh_bsgs_info &info, bool first) {
       return KH_E_IO;
     }
     int r = kh_bsgs_set_table(ctx, rows.data(), info.m3);
-    if (r) fprintf(stderr, "[E] %s\n", kh_last_error(ctx));
-    return r;
+    if (r) {
+      fprintf(stderr, "[E] %s\n", kh_last_error(ctx));
+      return r;
+    }
+    if (first) ptable_cache(rows, info.m3, true);
+    return KH_OK;
   }
   if (!first) return KH_OK;
   uint64_t got = 0;
@@ -667,6 +756,7 @@ int bsgs_ptable(kh_ctx *ctx, const kh_bsgs_info &info, bool first) {
     fprintf(stderr, "[E] Cannot write bP table file\n");
     return KH_E_IO;
   }
+  ptable_cache(rows, info.m3, false);
   return KH_OK;
 }
 
@@ -851,9 +941,7 @@ int main(int argc, char **argv) {
         break;
       }
       case 5: opt.load_ptable = true; break;  // keyhunt.cpp:786-787
-      case 6:
-        fprintf(stderr, "[E] --ptable-cache (the MD5 / bucket cache files) is not supported by this engine\n");
-        return EXIT_FAILURE;
+      case 6: opt.ptable_cache = true; break;  // keyhunt.cpp:788-789
       case 'm': {
         int m = -1;
         for (int i = 0; i < 5; i++)

@@ -107,3 +107,50 @@ def test_ptable_equals_reference_cli_file(work):
     shutil.copy(ref_dir / "bp.tbl", work / "ref.tbl")
     p, keys = _run(work, ["--ptable", "ref.tbl", "--load-ptable"])
     assert keys == [f"{KEY63:x}"]
+
+
+def _cache_model(rows: bytes) -> bytes:
+    """struct bptable_cache_file (keyhunt.cpp:137-143) as build_bptable_cache fills it (186-197)."""
+    import struct
+    m3 = len(rows) // 16
+    b, pos = [], 0
+    for bucket in range(256):
+        while pos < m3 and rows[pos * 16] < bucket:
+            pos += 1
+        b.append(pos)
+    b.append(m3)
+    return struct.pack("<IIQ16s257Q", 0x42505443, 1, m3, hashlib.md5(rows).digest(), *b)
+
+
+def test_ptable_cache_files(work):
+    p, keys = _run(work, ["--ptable", "c.tbl", "--ptable-cache"], BIG)
+    assert p.returncode == 1 and keys == [f"{KEY63:x}"], p.stdout[-2000:] + p.stderr[-2000:]
+    assert "[I] bP table cache not found (c.tbl.cache); creating" in p.stdout
+    assert "[+] bP table cache refreshed (c.tbl.cache)" in p.stdout
+    rows = (work / "c.tbl").read_bytes()
+    assert (work / "c.tbl.md5").read_text() == hashlib.md5(rows).hexdigest() + "\n"
+    assert (work / "c.tbl.cache").read_bytes() == _cache_model(rows)
+    # reload: the MD5 file is trusted and the cache hits
+    p, keys = _run(work, ["--ptable", "c.tbl", "--ptable-cache", "--load-ptable"], BIG)
+    assert p.returncode == 1 and keys == [f"{KEY63:x}"]
+    assert "[+] bP table MD5 loaded (c.tbl.md5)" in p.stdout and "[+] bP table cache hit (c.tbl.cache)" in p.stdout
+    # a cache of another MD5 is rebuilt
+    bad = bytearray(_cache_model(rows))
+    bad[16] ^= 1
+    (work / "c.tbl.cache").write_bytes(bytes(bad))
+    p, _ = _run(work, ["--ptable", "c.tbl", "--ptable-cache", "--load-ptable"], BIG)
+    assert "[W] bP table cache mismatch (c.tbl.cache); rebuilding" in p.stdout
+    assert (work / "c.tbl.cache").read_bytes() == _cache_model(rows)
+
+
+@pytest.mark.skipif(not os.path.exists(REF_BIN), reason="oracle/_ref/keyhunt not built")
+def test_ptable_cache_equals_reference_cli_files(work):
+    ref_dir = work / "ref"
+    ref_dir.mkdir()
+    shutil.copy(work / "63.pub", ref_dir)
+    subprocess.run(["timeout", "120", REF_BIN] + BIG + ["-t", "4", "--ptable", "c.tbl", "--ptable-cache", "-q"],
+                   cwd=ref_dir, capture_output=True, check=False)
+    p, _ = _run(work, ["--ptable", "c.tbl", "--ptable-cache"], BIG)
+    assert p.returncode == 1
+    for f in ("c.tbl", "c.tbl.md5", "c.tbl.cache"):
+        assert (work / f).read_bytes() == (ref_dir / f).read_bytes(), f
