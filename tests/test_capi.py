@@ -90,3 +90,38 @@ def test_bsgsd_rejects_bad_arguments_before_any_gpu_call():
     assert r.returncode == 1 and "sequentially" in r.stderr
     r = subprocess.run([d, "-h"], capture_output=True, text=True)
     assert r.returncode == 0 and "usage" in r.stdout
+
+
+def test_cli_ptable_flags_parse(tmp_path):
+    """--ptable / --ptable-size / --load-ptable / --ptable-cache are accepted (keyhunt.cpp:772-789);
+    --load-ptable alone fails with the reference's message (1126-1129)."""
+    cli = os.path.join(E.PKG, "bin", "keyhunt-amd")
+    if not os.path.exists(cli):
+        pytest.skip("CLI not built")
+    r = subprocess.run([cli, "-m", "bsgs", "-f", "x", "--load-ptable"], capture_output=True, text=True)
+    assert r.returncode == 1 and "--load-ptable requires --ptable <file>" in r.stderr
+    r = subprocess.run([cli, "-m", "bsgs", "-f", "x", "--ptable", "t", "--ptable-size", "1m", "--load-ptable",
+                        "--ptable-cache"], capture_output=True, text=True)
+    assert r.returncode == 1 and "ptable" not in r.stderr and "range" in r.stderr
+
+
+def test_host_md5_matches_hashlib(tmp_path):
+    """The CLI's RFC 1321 MD5 (host/kh_host_util.h, for --ptable-cache) against hashlib."""
+    import hashlib
+    import shutil
+    if not shutil.which("g++"):
+        pytest.skip("no g++")
+    src = tmp_path / "m.cpp"
+    src.write_text('#include "kh_host_util.h"\nint main(int, char **v) { uint8_t o[16];\n'
+                   '  if (!khh::md5_of_file(v[1], o)) return 1;\n'
+                   '  for (int i = 0; i < 16; i++) printf("%02x", o[i]); return 0; }\n')
+    exe = tmp_path / "m"
+    inc = os.path.join(os.path.dirname(E.PKG), "include")
+    subprocess.run(["g++", "-O1", "-std=c++17", "-I", os.path.join(E.PKG, "host"), "-I", inc, "-o", str(exe),
+                    str(src)], check=True)
+    for n in (0, 1, 55, 56, 63, 64, 65, 1000, (1 << 20) + 17):
+        data = bytes((i * 131 + n) & 0xFF for i in range(n))
+        f = tmp_path / f"d{n}"
+        f.write_bytes(data)
+        out = subprocess.run([str(exe), str(f)], capture_output=True, text=True, check=True).stdout
+        assert out == hashlib.md5(data).hexdigest(), n
