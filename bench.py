@@ -108,6 +108,36 @@ class Dist:
             self.dist.destroy_process_group()
 
 
+def rank_batch(rank: int, warmup: int, steps: int, s: int) -> int:
+    """Index of the batch rank `rank` walks at step s (warmup steps included, s < warmup + steps):
+    each rank owns one contiguous run of warmup + steps batches, so consecutive steps continue its
+    lanes (kh_bsgs_scan / kh_scan keep them across calls that follow on).  Runs of different ranks
+    are disjoint and together cover batches 0 .. world*(warmup+steps)-1 (tests/test_dist.py)."""
+    return rank * (warmup + steps) + s
+
+
+def launch_ranks(n: int, argv: list[str], script: str | None = None) -> int:
+    """`bench.py --gpus N` started without WORLD_SIZE: start N rank processes of this script (one per
+    GPU, RANK/LOCAL_RANK/WORLD_SIZE set, gloo rendezvous on 127.0.0.1), forward rank 0's JSON line and
+    return the worst exit status.  Nothing here touches the GPU, so the children start clean."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, script or os.path.abspath(__file__)] + argv, env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL, text=True))
+    out, _ = procs[0].communicate()
+    rcs = [procs[0].returncode] + [p.wait() for p in procs[1:]]
+    sys.stdout.write(out)
+    sys.stdout.flush()
+    return max(abs(rc) for rc in rcs)
+
+
 def timed(D: Dist, eng, warmup: int, steps: int, step_fn):
     for s in range(warmup):
         step_fn(s)
@@ -139,7 +169,7 @@ def bsgs_leg(D: Dist, eng, args):
 
     # rank r walks its own contiguous run of batches, so consecutive steps continue its lanes
     def step(s):
-        batch = D.rank * (args.warmup + args.steps) + s
+        batch = rank_batch(D.rank, args.warmup, args.steps, s)
         found = eng.bsgs_scan(base0 + batch * B * two_n, B)
         assert not found  # puzzle 125's key lies far from the start of the range
 
@@ -211,7 +241,7 @@ def rmd160_leg(D: Dist, eng, args):
     base0 = 1 << 65
 
     def step(s):
-        c = D.rank * (args.warmup_rmd + args.steps_rmd) + s  # a contiguous run of chunks per rank
+        c = rank_batch(D.rank, args.warmup_rmd, args.steps_rmd, s)
         hits = eng.scan(base0 + c * chunk, chunk, K.KH_MODE_ADDRESS, K.KH_SEARCH_COMPRESS)
         assert not hits
 
@@ -231,7 +261,7 @@ def xpoint_leg(D: Dist, eng, args):
     base0 = 1 << 62
 
     def step(s):
-        c = D.rank * (args.warmup_rmd + args.steps_rmd) + s  # a contiguous run of chunks per rank
+        c = rank_batch(D.rank, args.warmup_rmd, args.steps_rmd, s)
         hits = eng.scan(base0 + c * chunk, chunk, K.KH_MODE_XPOINT, K.KH_SEARCH_COMPRESS)
         assert not hits
 
@@ -243,55 +273,118 @@ def xpoint_leg(D: Dist, eng, args):
                        "points_per_launch": pts / la, "points_per_s_in_kernel": pts / (ms / 1e3)}}
 
 
-def cpu_threads() -> int:
+def cpu_host() -> dict:
+    """The host the CPU baseline ran on: model and CPU count (lscpu), the CPUs this process may use,
+    and the threads the baseline used.  On the pool's GPU boxes a one-GPU job's CPU share is 16
+    threads (OMP_NUM_THREADS, set by the box) of a much larger machine, so the baseline uses that
+    share; `per_thread` values let the reader scale it to any core count."""
+    info = {"machine_cpus": os.cpu_count()}
     try:
-        return max(1, min(16, len(os.sched_getaffinity(0))))
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for key, name in (("Model name", "model"), ("Socket(s)", "sockets"), ("Core(s) per socket", "cores_per_socket"),
+                          ("Thread(s) per core", "threads_per_core")):
+            m = re.search(rf"^{re.escape(key)}:\s*(.+)$", out, re.M)
+            if m:
+                info[name] = m.group(1).strip()
     except Exception:
-        return max(1, min(16, os.cpu_count() or 1))
+        pass
+    try:
+        info["affinity_cpus"] = len(os.sched_getaffinity(0))
+    except Exception:
+        info["affinity_cpus"] = os.cpu_count()
+    info["threads_used"] = cpu_threads()
+    return info
 
 
-def cpu_baseline_bsgs(eng, info, q, seconds: float, k: int = 128):
-    sys.path.insert(0, os.path.join(REPO, "oracle"))
-    import oracle
-    # the CPU restatement probes the reference-layout layer 1: rebuild it in that layout
-    eng.bsgs_setup(1 << 44, k, layer1=0)
-    eng.bsgs_build()
-    bf1 = eng.get_bloom(1)
-    p = oracle.bsgs_params(1 << 44, k)
-    thr = cpu_threads()
-    t = time.perf_counter()
-    oracle.bsgs_giant_probe(p, bf1, q, 4, thr)
-    cal = time.perf_counter() - t
-    groups = max(4, int(4 * seconds / max(cal, 1e-3)))
-    t = time.perf_counter()
-    oracle.bsgs_giant_probe(p, bf1, q, groups, thr)
-    dt = time.perf_counter() - t
-    pts = thr * groups * 1024
-    return {"value": pts * 2 * info.m / dt / 1e6, "unit": "Mkeys/s", "cores": thr, "kind": "port",
-            "sample": f"{pts} giant-step points ({groups} 1024-point groups x {thr} threads) probed against the "
-                      f"GPU-built k={k} layer-1 bloom, {dt:.1f} s; keys = points x 2M",
-            "giant_points_per_s": pts / dt}
+def cpu_threads() -> int:
+    """The job's CPU share: OMP_NUM_THREADS when the environment sets it (16 per GPU on the pool's
+    boxes), else every CPU this process may run on."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except Exception:
+        aff = os.cpu_count() or 1
+    share = os.environ.get("OMP_NUM_THREADS", "")
+    return max(1, min(aff, int(share))) if share.isdigit() and int(share) > 0 else max(1, aff)
 
 
-def cpu_baseline_rmd160(seconds: int):
-    ref = os.path.join(REPO, "oracle", "_ref", "keyhunt")
-    if not os.path.exists(ref):
+REF_BIN = os.path.join(REPO, "oracle", "_ref", "keyhunt")
+
+
+def run_reference(argv: list[str], files: list[str], seconds: float, setup=None):
+    """Run the reference CLI (oracle/_ref/keyhunt, built from /root/reference's sources by
+    oracle/Makefile.ref) in a scratch directory under /tmp for `seconds` after its tables are ready,
+    with every thread of the job's CPU share, and parse its own last stats line
+    ("Total N keys in S seconds", keyhunt.cpp:2906-2946).  `setup(dir)` may write table files first."""
+    if not os.path.exists(REF_BIN):
         return None
     thr = cpu_threads()
-    with tempfile.TemporaryDirectory() as td:
-        shutil.copy(os.path.join(REPO, "tests", "golden", "data", "66.rmd"), td)
-        p = subprocess.run(["timeout", str(seconds), ref, "-m", "rmd160", "-f", "66.rmd", "-b", "66", "-l", "compress",
-                            "-t", str(thr), "-s", "5", "-q"], cwd=td, capture_output=True, text=True)
-    rates = re.findall(r"Total (\d+) keys in (\d+) seconds", p.stdout)
-    if not rates:
+    with tempfile.TemporaryDirectory(dir="/tmp") as td:
+        for f in files:
+            shutil.copy(os.path.join(REPO, "tests", "golden", "data", f), td)
+        if setup:
+            setup(td)
+        cmd = [REF_BIN] + argv + ["-t", str(thr), "-s", "5", "-q"]
+        p = subprocess.Popen(cmd, cwd=td, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL)
+        out = b""
+        t0 = time.time()
+        os.set_blocking(p.stdout.fileno(), False)
+        last = None
+        while time.time() - t0 < seconds + 120:
+            time.sleep(0.5)
+            try:
+                chunk = p.stdout.read()
+            except Exception:
+                chunk = None
+            if chunk:
+                out += chunk
+            rates = re.findall(rb"Total (\d+) keys in (\d+) seconds", out)
+            if rates:
+                last = tuple(map(int, rates[-1]))
+                if last[1] >= seconds:
+                    break
+            if p.poll() is not None:
+                break
+        if p.poll() is None:
+            p.terminate()
+            try:
+                p.wait(timeout=10)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    if not last or last[1] == 0:
         return None
-    keys, secs = map(int, rates[-1])
+    keys, secs = last
     return {"value": keys / secs / 1e6, "unit": "Mkeys/s", "cores": thr, "kind": "reference",
-            "sample": f"oracle/_ref/keyhunt -m rmd160 -f 66.rmd -b 66 -l compress -t {thr}: {keys} keys in {secs} s "
-                      f"(reference's own stats line)"}
+            "per_thread": keys / secs / 1e6 / thr, "host": cpu_host(),
+            "sample": f"oracle/_ref/keyhunt {' '.join(argv)} -t {thr}: {keys} keys in {secs} s (the reference's "
+                      f"own stats line, keys counted as it counts them)"}
+
+
+def cpu_baseline_bsgs(eng, C: dict, seconds: float):
+    """The reference's BSGS giant-step loop (thread_process_bsgs, keyhunt.cpp:4549-4888) on the host,
+    on the same workload (-b bits -k K from 2^(bits-1)).  Its 120-s-per-core baby-step build is
+    skipped: the engine writes the four -S table files (kh_bsgs_save: the reference's format, byte
+    for byte, tests/test_gpu_tables.py) and the reference reads them (-S -6, keyhunt.cpp:1983-2240)."""
+    pub = {125: "125.txt", 130: "130.txt"}[C["bits"]]
+    return run_reference(["-m", "bsgs", "-f", pub, "-b", str(C["bits"]), "-k", str(C["k"]), "-S", "-6"], [pub],
+                         seconds, setup=lambda d: eng.bsgs_save(d))
+
+
+def cpu_baseline_rmd160(seconds: float):
+    return run_reference(["-m", "rmd160", "-f", "66.rmd", "-b", "66", "-l", "compress"], ["66.rmd"], seconds)
+
+
+def cpu_baseline_xpoint(seconds: float):
+    return run_reference(["-m", "xpoint", "-f", "63.pub", "-b", "63"], ["63.pub"], seconds)
 
 
 def main():
+    if "WORLD_SIZE" not in os.environ:
+        pre = argparse.ArgumentParser(add_help=False)
+        pre.add_argument("--gpus", type=int, default=1)
+        n = pre.parse_known_args()[0].gpus
+        if n > 1:
+            sys.exit(launch_ranks(n, sys.argv[1:]))
     # stdout carries exactly one JSON line (rank 0); native libraries (gloo, HIP) may print on fd 1,
     # so fd 1 is pointed at stderr for the run and the JSON goes to the saved descriptor.
     json_out = os.fdopen(os.dup(1), "w")
@@ -316,16 +409,20 @@ def main():
 
     import keyhunt_amd as K
     D = Dist()
+    if args.gpus != D.world:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={D.world}: launch one rank per GPU")
     ndev = K.device_count()
     # one process per GPU; on a box with fewer GPUs than ranks (rehearsal) ranks share devices
     eng = K.Engine(D.local % max(1, ndev))
     prim = bsgs_leg(D, eng, args)
     sec = None if args.no_secondary else rmd160_leg(D, eng, args)
     ter = None if args.no_secondary else xpoint_leg(D, eng, args)
-    cpu_b = cpu_r = None
+    cpu_b = cpu_r = cpu_x = None
     if D.rank == 0 and D.world == 1 and not args.no_cpu_baseline:
-        cpu_b = cpu_baseline_bsgs(eng, prim["info"], prim["q"], args.cpu_seconds, BSGS_CONFIGS[args.config]["k"])
-        cpu_r = cpu_baseline_rmd160(int(args.cpu_seconds + 5))
+        cpu_b = cpu_baseline_bsgs(eng, BSGS_CONFIGS[args.config], args.cpu_seconds)
+        if not args.no_secondary:
+            cpu_r = cpu_baseline_rmd160(args.cpu_seconds)
+            cpu_x = cpu_baseline_xpoint(args.cpu_seconds)
     eng.close()
     D.barrier()
     if D.rank == 0:
@@ -354,7 +451,7 @@ def main():
         if ter:
             line["tertiary"] = {"workload": "-m xpoint -f tests/63.pub -b 63", "value": ter["value"],
                                 "unit": "Mkeys/s", "ms_per_step": ter["ms_per_step"], "steps": args.steps_rmd,
-                                "kernel": ter["kernel"]}
+                                "kernel": ter["kernel"], "cpu_baseline": cpu_x}
         json_out.write(json.dumps(line) + "\n")
         json_out.flush()
     D.close()

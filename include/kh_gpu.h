@@ -47,7 +47,9 @@ extern "C" {
 #define KH_MODE_ADDRESS 0  /* -m address / -m rmd160: hash160 probes */
 #define KH_MODE_XPOINT 1   /* -m xpoint: X[0..20) probes */
 #define KH_MODE_ETH 2      /* -m address|rmd160 -c eth: Keccak-256(X||Y)[12..32) probes (the search kind is
-                              ignored; keyhunt.cpp:3524-3548, 3703-3760, 5663-5669); not with KH_MODE_ENDO */
+                              ignored; keyhunt.cpp:3524-3548, 3703-3760, 5663-5669).  With KH_MODE_ENDO the
+                              reference's six images: eth of P, -P, beta P, -beta P, beta P (again, its
+                              slip at 3533) and -beta^2 P, each hit keyed as 3736-3744 derives it */
 #define KH_MODE_ENDO 0x10  /* OR into the mode: -e, also probe (beta*X, Y) and (beta^2*X, Y), i.e. keys
                               lambda*k and lambda^2*k (keyhunt.cpp:3408-3440, 3476-3830) */
 #define KH_SEARCH_COMPRESS 0
@@ -70,7 +72,9 @@ extern "C" {
 /* with KH_MODE_ENDO, kind also carries the image and (for 04 hashes) the Y sign: */
 #define KH_KIND_ENDO1 0x10 /* matched on (beta*X, Y): key = lambda*k (+- as reported) */
 #define KH_KIND_ENDO2 0x20 /* matched on (beta^2*X, Y): key = lambda^2*k */
-#define KH_KIND_NEGY 0x40  /* 04||X||-Y matched: key negated */
+#define KH_KIND_NEGY 0x40  /* 04||X||-Y (or, -c eth, -Y) matched: key negated */
+/* -e -c eth: ETH | ENDO2 without NEGY is the reference's repeated beta P image (slot 4), reported
+   after its ETH | ENDO1 twin with key n - lambda^2 k, as the reference prints it */
 
 typedef struct kh_ctx kh_ctx;
 

@@ -769,7 +769,7 @@ int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride_be[32], u
   if (!ctx || !start || !n_hits || (n_keys % (2 * KH_WALK_H)) || n_keys == 0) return KH_E_ARG;
   const bool endo = (mode & KH_MODE_ENDO) != 0;
   mode &= ~(uint32_t)KH_MODE_ENDO;
-  if (mode > KH_MODE_ETH || search > KH_SEARCH_BOTH || (mode == KH_MODE_ETH && endo)) return KH_E_ARG;
+  if (mode > KH_MODE_ETH || search > KH_SEARCH_BOTH) return KH_E_ARG;
   if (!ctx->d_tbloom) return KH_E_STATE;
   (void)hipSetDevice(ctx->device);
   int km = mode == KH_MODE_XPOINT ? KM_XPOINT
@@ -907,7 +907,7 @@ int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride_be[32], u
   // uncompressed, then xpoint.
   auto order = [](uint32_t kind) {
     uint32_t base = kind & 15u, e = (kind >> KH_DKIND_ENDO_SHIFT) & 3u, neg = (kind & KH_DKIND_NEG) ? 1u : 0u;
-    return base < 2 ? 2 * e + base : base == 2 ? 6 + 2 * e + neg : 12 + e;
+    return base < 2 ? 2 * e + base : base == 2 || base == KH_KIND_ETH ? 6 + 2 * e + neg : 12 + e;
   };
   std::vector<kh_dev_hit> dh(ctx->h_hits.begin(), ctx->h_hits.begin() + nd);
   std::sort(dh.begin(), dh.end(), [&](const kh_dev_hit &a, const kh_dev_hit &b) {
@@ -921,6 +921,21 @@ int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride_be[32], u
       fe{{1, 0, 0, 0, 0, 0, 0, 0}},
       fe{{0x719501eeu, 0xc1396c28u, 0x12f58995u, 0x9cf04975u, 0xac3434e9u, 0x6e64479eu, 0x657c0710u, 0x7ae96a2bu}},
       fe{{0x8e6afa40u, 0x3ec693d6u, 0xed0a766au, 0x630fb68au, 0x53cbcb16u, 0x919bb861u, 0x9a83f8efu, 0x851695d4u}}};
+  // -e -c eth: a hit on (beta X, Y) is also the reference's slot-4 hit (keyhunt.cpp:3533), whose key
+  // it derives as lambda^2 k, checks against the image, and so negates (3736-3744): appended as
+  // kind ETH | ENDO2 (an image the GPU never probes in this mode) right after its slot-2 twin
+  if (endo && mode == KH_MODE_ETH) {
+    std::vector<kh_dev_hit> d2;
+    for (auto &h : dh) {
+      d2.push_back(h);
+      if (h.kind == (KH_KIND_ETH | (1u << KH_DKIND_ENDO_SHIFT))) {
+        kh_dev_hit t = h;
+        t.kind = KH_KIND_ETH | (2u << KH_DKIND_ENDO_SHIFT);
+        d2.push_back(t);
+      }
+    }
+    dh.swap(d2);
+  }
   std::vector<kh_hit> out;
   for (auto &h : dh) {
     u256 k = sc_add(st, sc_reduce(u256_from_u128((u128)h.idx)));
@@ -949,7 +964,9 @@ int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride_be[32], u
     } else if (base == KH_KIND_04) {
       hash160_uncomp(xe, ye, w);
     } else if (base == KH_KIND_ETH) {
-      eth_address(P.x, P.y, w);
+      if (endo && e == 2 && !neg)  // the slot-4 twin: its image is eth(beta P)
+        fe_mul(xe, P.x, BETA[1]);
+      eth_address(xe, ye, w);
     } else {
       for (int j = 0; j < 5; j++) w[j] = bswap32(xe.d[7 - j]);
     }
@@ -966,7 +983,9 @@ int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride_be[32], u
     kh_hit o;
     memset(&o, 0, sizeof o);
     u256 kr = e ? sc_mul(k, LAMBDA[e]) : k;  // (beta^e x, y) = lambda^e * (x, y)
-    if (compressed) {
+    if (base == KH_KIND_ETH && endo && e == 2 && !neg) {
+      kr = sc_neg(kr);  // the slot-4 twin: lambda^2 k gives (beta^2 X, Y), not the image: negated
+    } else if (compressed) {
       uint32_t odd = P.y.d[0] & 1;  // the image keeps Y
       if (odd != (base == KH_KIND_03 ? 1u : 0u)) kr = sc_neg(kr);
     } else if (neg) {

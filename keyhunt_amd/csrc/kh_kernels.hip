@@ -226,16 +226,17 @@ __device__ __forceinline__ void endo_beta(fe &b, int e) {
   for (int i = 0; i < 8; i++) b.d[i] = e == 1 ? B1[i] : B2[i];
 }
 
-// Ethereum address (Keccak-256 of X||Y, bytes 12..31); kind 5 (keyhunt.cpp:3524-3548, 3703-3760)
-__device__ __forceinline__ void probe_eth(const walk_args &A, const fe &x, const fe &y, uint64_t idx) {
+// Ethereum address (Keccak-256 of X||Y, bytes 12..31); kind 5 | tag (keyhunt.cpp:3524-3548, 3703-3760)
+__device__ __forceinline__ void probe_eth(const walk_args &A, const fe &x, const fe &y, uint64_t idx,
+                                          uint32_t tag = 0) {
   uint32_t w[5];
   eth_address(x, y, w);
   if (A.tblk) {
-    if (tblk_probe(A, w)) record_hit(A, idx, 5);
+    if (tblk_probe(A, w)) record_hit(A, idx, 5 | tag);
     return;
   }
   uint64_t a = xxh64_20(w, KH_BLOOM_SEED);
-  if (bloom_probe_lazy(A.bloom, A.bd, a, [&](uint64_t s) { return xxh64_20(w, s); })) record_hit(A, idx, 5);
+  if (bloom_probe_lazy(A.bloom, A.bd, a, [&](uint64_t s) { return xxh64_20(w, s); })) record_hit(A, idx, 5 | tag);
 }
 
 template <int MODE>
@@ -243,6 +244,25 @@ __device__ __forceinline__ void probe_point(const walk_args &A, const fe &x, con
   if (idx >= A.n_points) return;
   if constexpr (MODE == KM_ETH) {
     probe_eth(A, x, y, idx);
+    return;
+  }
+  if constexpr (MODE == (KM_ETH | KM_ENDO)) {
+    // -e -c eth (keyhunt.cpp:3524-3536): the reference's six images per point are eth(P), eth(-P),
+    // eth(beta P), eth(-beta P), eth(beta P) again (it passes endomorphism_beta where beta2 is
+    // meant, 3533) and eth(-beta^2 P).  The repeated image is probed once; the host reports its
+    // second hit (kind ETH | ENDO2 without NEG) with the key the reference derives for it.
+    fe ny;
+    fe_neg(ny, y);
+    probe_eth(A, x, y, idx, 0);
+    probe_eth(A, x, ny, idx, KH_DKIND_NEG);
+    fe b, xe;
+    endo_beta(b, 1);
+    fe_mul(xe, x, b);
+    probe_eth(A, xe, y, idx, 1u << KH_DKIND_ENDO_SHIFT);
+    probe_eth(A, xe, ny, idx, (1u << KH_DKIND_ENDO_SHIFT) | KH_DKIND_NEG);
+    endo_beta(b, 2);
+    fe_mul(xe, x, b);
+    probe_eth(A, xe, ny, idx, (2u << KH_DKIND_ENDO_SHIFT) | KH_DKIND_NEG);
     return;
   }
   constexpr int BASE = MODE & 15;
@@ -409,7 +429,7 @@ __device__ __forceinline__ void probe_pair_bsgs(const walk_args &A, const fe &x1
 
 template <int MODE>
 constexpr bool needs_y() {
-  return (MODE & 15) == KM_H160U || (MODE & 15) == KM_H160B || MODE == KM_DUMP || MODE == KM_ETH;
+  return (MODE & 15) == KM_H160U || (MODE & 15) == KM_H160B || MODE == KM_DUMP || (MODE & 15) == KM_ETH;
 }
 
 }  // namespace
@@ -421,7 +441,7 @@ constexpr bool needs_y() {
 // 4 waves/SIMD even with a few spills; the hash160 modes prefer 3).
 template <int MODE>
 constexpr int walk_lb() {
-  return ((MODE & 15) == KM_H160C || (MODE & 15) == KM_H160U || (MODE & 15) == KM_H160B || MODE == KM_ETH)
+  return ((MODE & 15) == KM_H160C || (MODE & 15) == KM_H160U || (MODE & 15) == KM_H160B || (MODE & 15) == KM_ETH)
              ? KH_WALK_LB_HASH
          : MODE == KM_DUMP                                          ? 2
                                                                     : KH_WALK_LB;
@@ -902,6 +922,7 @@ hipError_t launch_walk(int mode, const walk_args &A, hipStream_t st, int H) {
     case KM_H160U | KM_ENDO: hipLaunchKernelGGL(k_walk<KM_H160U | KM_ENDO>, grid, block, 0, st, A); break;
     case KM_H160B | KM_ENDO: hipLaunchKernelGGL(k_walk<KM_H160B | KM_ENDO>, grid, block, 0, st, A); break;
     case KM_XPOINT | KM_ENDO: hipLaunchKernelGGL(k_walk<KM_XPOINT | KM_ENDO>, grid, block, 0, st, A); break;
+    case KM_ETH | KM_ENDO: hipLaunchKernelGGL(k_walk<KM_ETH | KM_ENDO>, grid, block, 0, st, A); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

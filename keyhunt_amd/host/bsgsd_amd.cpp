@@ -339,12 +339,14 @@ int main(int argc, char **argv) {
     fprintf(stderr, "[E] no GPU\n");
     return EXIT_FAILURE;
   }
-  if (opt.gpus <= 0 || opt.gpus > ndev) opt.gpus = ndev;
+  // -g contexts on devices d % ndev: more contexts than devices share a device, each with its own
+  // tables and lanes, all taking bases from the request's one cursor
+  if (opt.gpus <= 0) opt.gpus = ndev;
   g_gpus.resize(opt.gpus);
   bool present = false;
   for (int d = 0; d < opt.gpus; d++) {
     gpu &g = g_gpus[d];
-    int r = kh_open(d, &g.ctx);
+    int r = kh_open(d % ndev, &g.ctx);
     if (!r) r = kh_bsgs_set_layer1(g.ctx, opt.layer1);
     if (!r) r = kh_bsgs_setup(g.ctx, opt.n, opt.k, &g.info);
     if (!r && d == 0) present = files_present(g.info);

@@ -509,7 +509,7 @@ void addr_worker(addr_job *j) {
     uint32_t nh = 0;
     r = kh_scan(ctx, st_be, stride_be, j->nseq,
                 opt.mode == MODE_XPOINT ? (KH_MODE_XPOINT | (opt.endo ? KH_MODE_ENDO : 0))
-                : (opt.eth && (opt.mode == MODE_ADDRESS || opt.mode == MODE_RMD160)) ? KH_MODE_ETH
+                : (opt.eth && (opt.mode == MODE_ADDRESS || opt.mode == MODE_RMD160)) ? (KH_MODE_ETH | (opt.endo ? KH_MODE_ENDO : 0))
                       : (KH_MODE_ADDRESS | (opt.endo ? KH_MODE_ENDO : 0)),
                 (uint32_t)opt.search, hits.data(), (uint32_t)hits.size(), &nh);
     if (r == KH_E_OVERFLOW && nh > hits.size()) {  // a short vanity prefix: take them all
@@ -522,7 +522,7 @@ void addr_worker(addr_job *j) {
       break;
     }
     for (uint32_t i = 0; i < nh; i++) {
-      if (hits[i].kind == KH_KIND_ETH)
+      if ((hits[i].kind & 15u) == KH_KIND_ETH)
         writekeyeth(ctx, hits[i].key);
       else if (opt.mode == MODE_VANITY)
         writevanitykey(ctx, hits[i].compressed != 0, hits[i].key);
@@ -871,7 +871,14 @@ void bsgs_worker(bsgs_job *j) {
       }
       {
         std::lock_guard<std::mutex> lk2(g_keys_mtx);
-        printf("[+] Thread Key found privkey %s   \n", k.c_str());
+        // each BSGS worker of the reference has its own format: the sequential one (also -B ggsb and
+        // angrygiant) continues its string over a backslash-newline, so no newline is printed
+        // (keyhunt.cpp:4826-4827); random 5079, dance 5885, backward 6144, both 6429
+        const int bm = opt.bsgs_mode;
+        printf(bm == BM_SEQUENTIAL || bm == BM_GGSB || bm == BM_ANGRYGIANT ? "[+] Thread Key found privkey %s   "
+               : bm == BM_RANDOM                                          ? "[+] Thread Key found privkey %s    \n"
+                                                                          : "[+] Thread Key found privkey %s   \n",
+               k.c_str());
         printf("[+] Publickey %s\n", pub.c_str());
         FILE *f = fopen("KEYFOUNDKEYFOUND.txt", "a");
         if (f) {
@@ -971,15 +978,18 @@ int main(int argc, char **argv) {
         else if (!strcmp(optarg, "both")) opt.search = KH_SEARCH_BOTH;
         else { fprintf(stderr, "[E] Unknow search type %s\n", optarg); return EXIT_FAILURE; }
         break;
-      case 'r': {
+      case 'r': {  // keyhunt.cpp:1024-1055: START[:END]; START alone runs to the group order
         std::string s(optarg);
         size_t p = s.find(':');
-        if (p == std::string::npos || !u_from_hex(s.substr(0, p).c_str(), opt.start) ||
-            !u_from_hex(s.substr(p + 1).c_str(), opt.end)) {
-          fprintf(stderr, "[E] Invalid range %s\n", optarg);
-          return EXIT_FAILURE;
+        const std::string a = s.substr(0, p), b = p == std::string::npos ? std::string(ORDER_HEX) : s.substr(p + 1);
+        if (!u_from_hex(a.c_str(), opt.start)) {
+          fprintf(stderr, p == std::string::npos ? "[E] Invalid hexstring : %s.\n" : "[E] Invalid hexstring : %s\n",
+                  a.c_str());
+        } else if (!u_from_hex(b.c_str(), opt.end)) {
+          fprintf(stderr, "[E] Invalid hexstring : %s\n", b.c_str());
+        } else {
+          opt.have_range = true;
         }
-        opt.have_range = true;
         break;
       }
       case 'b':
@@ -1076,10 +1086,6 @@ int main(int argc, char **argv) {
   if (!validate_nk(nk_n, opt.kfactor)) return EXIT_FAILURE;
   // keyhunt.cpp:1185-1193 compares the -B index with MODE_BSGS (2), i.e. these two guards fire
   // for -B both whatever -m is (SURVEY 8a parity note 7); BSGS itself ignores -e and -I
-  if (opt.eth && opt.endo && (opt.mode == MODE_ADDRESS || opt.mode == MODE_RMD160)) {
-    fprintf(stderr, "[E] -e with -c eth is not provided by this engine\n");
-    return EXIT_FAILURE;
-  }
   if (opt.bsgs_mode == BM_BOTH && opt.endo) {
     fprintf(stderr, "[E] Endomorphism doesn't work with BSGS\n");
     return EXIT_FAILURE;
@@ -1096,15 +1102,25 @@ int main(int argc, char **argv) {
     printf("[+] Bit Range %d\n", opt.bits);
   } else if (opt.have_range) {
     if (u_is_zero(opt.start)) opt.start = u_from_u64(1);
-    if (u_cmp(opt.start, opt.end) == 0 || u_cmp(opt.start, order) >= 0 || u_cmp(opt.end, order) > 0) {
-      fprintf(stderr, "[E] invalid range (random mode is outside this engine's scope)\n");
-      return EXIT_FAILURE;
+    if (u_cmp(opt.start, opt.end) == 0) {
+      fprintf(stderr, "[E] Start and End range can't be the same\nFallback to random mode!\n");
+      opt.have_range = false;
+    } else if (u_cmp(opt.start, order) >= 0 || u_cmp(opt.end, order) > 0) {
+      fprintf(stderr, "[E] Start and End range can't be great than N\nFallback to random mode!\n");
+      opt.have_range = false;
+    } else {
+      if (u_cmp(opt.start, opt.end) > 0) {
+        fprintf(stderr, "[W] Opps, start range can't be great than end range. Swapping them\n");
+        std::swap(opt.start, opt.end);
+      }
+      printf("[+] Range \n");
     }
-    if (u_cmp(opt.start, opt.end) > 0) std::swap(opt.start, opt.end);
-    printf("[+] Range \n");
-  } else {
-    fprintf(stderr, "[E] a range (-r or -b) is required: random mode is outside this engine's scope\n");
-    return EXIT_FAILURE;
+  }
+  if (!opt.have_bits && !opt.have_range) {
+    // no usable range (keyhunt.cpp:1250-1255, 1534-1540): the address family walks sequentially
+    // from 1 to the group order; BSGS starts at a random key below the order and walks up
+    opt.start = opt.mode == MODE_BSGS ? u_rand_range(u_from_u64(1), order) : u_from_u64(1);
+    opt.end = order;
   }
   printf("[+] -- from : 0x%s\n[+] -- to   : 0x%s\n", u_hex(opt.start).c_str(), u_hex(opt.end).c_str());
   int ndev = 0;
@@ -1113,8 +1129,11 @@ int main(int argc, char **argv) {
     fprintf(stderr, "[E] no GPU found\n");
     return EXIT_FAILURE;
   }
-  int gpus = opt.gpus > 0 ? std::min(opt.gpus, ndev) : ndev;
-  printf("[+] GPUs : %d\n", gpus);
+  // -g contexts: one host thread + kh_ctx each, on device d % ndev.  More contexts than devices
+  // share a device (as the reference's -t threads share the host's cores); each keeps its own
+  // tables and lanes, and they all take work from the one cursor (keyhunt.cpp:3321-3324, 4600-4617).
+  int gpus = opt.gpus > 0 ? opt.gpus : ndev;
+  printf("[+] GPUs : %d (%d context%s)\n", std::min(gpus, ndev), gpus, gpus == 1 ? "" : "s");
   g_cursor = opt.start;
   g_end = opt.end;
   g_top = opt.end;
@@ -1162,7 +1181,7 @@ int main(int argc, char **argv) {
       printf("[+] Sorting data ... done! %llu values were loaded and sorted\n", (unsigned long long)(rows.size() / 20));
     g_running = gpus;
     for (int d = 0; d < gpus; d++) {
-      aj[d].device = d;
+      aj[d].device = d % ndev;
       aj[d].rows = &rows;
       // initBloomFilter (keyhunt.cpp:7608): max(10000, items), times -z above the floor
       const uint64_t nitems = items ? items : rows.size() / 20;
@@ -1233,17 +1252,28 @@ int main(int argc, char **argv) {
     }
     g_running = gpus;
     for (int d = 0; d < gpus; d++) {
-      bj[d].device = d;
+      bj[d].device = d % ndev;
       bj[d].first = d == 0;
       bj[d].tx = &tx;
       bj[d].ty = &ty;
       bj[d].comp = &comp;
       bj[d].n = n;
       bj[d].k = opt.kfactor;
-      // ~2^31 giant points per engine call: enough lanes to fill the GPU, ~0.1 s per call
+      // ~2^31 giant points per engine call: enough lanes to fill the GPU, ~0.1 s per call; a range
+      // of fewer bases than that is dealt out evenly over the contexts (the reference's threads
+      // take one base each, keyhunt.cpp:4600-4617)
       {
         uint64_t aux = Nr / M, pts = ((aux + 1023) / 1024) * 1024;
         bj[d].bases_per_call = std::max<uint64_t>(1, (1ULL << 31) / pts);
+        const U span = u_sub(opt.end, opt.start);
+        if (g_step.v[1] == 0 && g_step.v[2] == 0 && g_step.v[3] == 0 && g_step.v[4] == 0) {
+          uint64_t rem = 0;
+          U nb = u_divmod_u64(span, g_step.v[0], &rem);
+          if (u_bitlen(nb) <= 40) {
+            const uint64_t bases = nb.v[0] + (rem ? 1 : 0), share = (bases + gpus - 1) / gpus;
+            bj[d].bases_per_call = std::max<uint64_t>(1, std::min(bj[d].bases_per_call, share));
+          }
+        }
       }
       th.emplace_back(bsgs_worker, &bj[d]);
     }

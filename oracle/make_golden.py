@@ -74,7 +74,33 @@ E2E_RUNS = [
     # GGSB: bases every 2 x block size (keyhunt.cpp:1477-1499, 1617-1627), sequential worker
     ("bsgs_63_ggsb_count4", ["-m", "bsgs", "-f", "63.pub", "-n", "0x1000000", "-k", "4", "-B", "ggsb", "--bsgs-block-count", "4", "-r", "7cce5efdac000000:7cce5efdad000000", "-t", "8"], 300),
     ("bsgs_63_ggsb_size1024_both", ["-m", "bsgs", "-f", "63.pub", "-n", "0x1000000", "-k", "4", "-B", "both", "--bsgs-block-size", "1024", "-r", "7cce5efdac000000:7cce5efdad000000", "-t", "8"], 300),
+    # -e -c eth: the six eth images per point, with the reference's repeated beta image
+    # (keyhunt.cpp:3524-3536, 3703-3760; tests/golden/make_eth_endo_targets.py)
+    ("address_eth_endo_2p20", ["-m", "address", "-c", "eth", "-e", "-f", "eth_endo.txt", "-r", "1:100000", "-n", "0x100000", "-t", "8"], 300),
+    ("address_eth_2p20_endo", ["-m", "address", "-c", "eth", "-e", "-f", "eth_targets.txt", "-r", "1:100000", "-n", "0x100000", "-t", "8"], 300),
+    # -r START without END runs to the group order (keyhunt.cpp:1028-1033): BSGS ends at "All points
+    # were found"; the address family never ends, so it is stopped after `tmo` s and only hits
+    # below the "cmp_below" key are compared
+    ("bsgs_63_start_only", ["-m", "bsgs", "-f", "63.pub", "-r", "7cce5a0000000000", "-t", "8"], 300),
+    ("xpoint_63_start_only", ["-m", "xpoint", "-f", "63.pub", "-r", "7cce5efdac000000", "-n", "0x100000", "-t", "8"], 20),
+    # no range at all: sequential from 1 (keyhunt.cpp:1250-1255)
+    ("address_1to32_no_range", ["-m", "address", "-f", "1to32.txt", "-l", "compress", "-n", "0x100000", "-t", "8"], 20),
 ]
+# stopped runs: compare the hits with keys below this bound
+CMP_BELOW = {"xpoint_63_start_only": 0x7cce5efdad000000, "address_1to32_no_range": 1 << 24}
+
+# the hit blocks the reference prints on stdout (writekey 6914, writekeyeth 6946, writevanitykey
+# 6728) and the two BSGS lines, taken apart because the reference's threads may interleave them
+# (the sequential worker's first line has no newline, 4826-4827; random 5079, dance 5885,
+# backward 6144 and both 6429 end it with one)
+STDOUT_BLOCK = re.compile(r"\nHit! Private Key: [^\n]*\npubkey: [^\n]*\nAddress [^\n]*\nrmd160 [^\n]*\n"
+                          r"|\n Hit!!!! Private Key: [^\n]*\naddress: [^\n]*\n"
+                          r"|\nVanity Private Key: [^\n]*\npubkey: [^\n]*\nAddress [^\n]*\nrmd160 [^\n]*\n"
+                          r"|\[\+\] Thread Key found privkey [0-9a-f]+ *\n?|\[\+\] Publickey [^\n]*\n")
+
+
+def stdout_blocks(text: str) -> list[str]:
+    return sorted(STDOUT_BLOCK.findall(text))
 
 
 # -S table files (keyhunt.cpp:2504-2652) written by the reference for small (n, k): their sha256
@@ -203,9 +229,14 @@ def gen_e2e(only: list[str] | None = None) -> None:
             for fn in ("KEYFOUNDKEYFOUND.txt", "VANITYKEYFOUND.txt"):
                 kf = os.path.join(td, fn)
                 text += open(kf).read() if os.path.exists(kf) else ""
-            hits = parse_keyfound(text)
-            results[name] = {"argv": argv, "exit": p.returncode, "hits": sorted(hits, key=lambda h: int(h["key"], 16)),
-                             "stdout_hit_lines": [ln.strip() for ln in p.stdout.split("\n") if "Hit!" in ln or "Key found" in ln]}
+            hits = sorted(parse_keyfound(text), key=lambda h: int(h["key"], 16))
+            blocks = stdout_blocks(p.stdout)
+            results[name] = {"argv": argv, "exit": p.returncode, "hits": hits, "stdout_blocks": blocks}
+            if name in CMP_BELOW:
+                lim = CMP_BELOW[name]
+                results[name].update(cmp_below=hex(lim), killed_after=tmo,
+                                     hits=[h for h in hits if int(h["key"], 16) < lim],
+                                     stdout_blocks=[b for b in blocks if int(re.search(r"Key: ([0-9a-f]+)", b).group(1), 16) < lim])
             print(f"{name}: exit={p.returncode} hits={len(hits)}", flush=True)
     results["_generator"] = "oracle/make_golden.py running oracle/_ref/keyhunt (reference CLI built from its sources)"
     with open(path, "w") as f:

@@ -1,4 +1,5 @@
-"""Helpers to run the engine's CLI (keyhunt_amd/bin/keyhunt-amd) like the reference binary."""
+"""Helpers to run the engine's CLI (keyhunt_amd/bin/keyhunt-amd) like the reference binary and to
+compare a run with a reference-CLI fixture of tests/golden/ref_e2e.json (oracle/make_golden.py)."""
 import os
 import re
 import shutil
@@ -8,6 +9,12 @@ import tempfile
 from conftest import DATA, REPO
 
 CLI = os.path.join(REPO, "keyhunt_amd", "bin", "keyhunt-amd")
+
+# the hit blocks keyhunt prints on stdout (same pattern as oracle/make_golden.py's STDOUT_BLOCK)
+STDOUT_BLOCK = re.compile(r"\nHit! Private Key: [^\n]*\npubkey: [^\n]*\nAddress [^\n]*\nrmd160 [^\n]*\n"
+                          r"|\n Hit!!!! Private Key: [^\n]*\naddress: [^\n]*\n"
+                          r"|\nVanity Private Key: [^\n]*\npubkey: [^\n]*\nAddress [^\n]*\nrmd160 [^\n]*\n"
+                          r"|\[\+\] Thread Key found privkey [0-9a-f]+ *\n?|\[\+\] Publickey [^\n]*\n")
 
 
 def parse_keyfound(text: str) -> list[dict]:
@@ -24,13 +31,51 @@ def parse_keyfound(text: str) -> list[dict]:
     return sorted(hits, key=lambda h: int(h["key"], 16))
 
 
-def run_cli(argv: list[str], timeout: int = 600):
+def run_cli(argv: list[str], timeout: int = 600, kill_after: int | None = None):
+    """Run the CLI in a scratch copy of tests/golden/data; returns (CompletedProcess, hits from
+    KEYFOUNDKEYFOUND.txt / VANITYKEYFOUND.txt).  kill_after: stop it with SIGTERM after that many
+    seconds (exit 124, as `timeout` reports), for runs that never end by themselves."""
     with tempfile.TemporaryDirectory() as td:
         for fn in os.listdir(DATA):
             shutil.copy(os.path.join(DATA, fn), td)
-        p = subprocess.run([CLI] + argv + ["-q", "-s", "0"], cwd=td, capture_output=True, text=True, timeout=timeout)
+        cmd = [CLI] + argv + ["-q", "-s", "0"]
+        if kill_after:
+            cmd = ["timeout", "-k", "10", str(kill_after)] + cmd
+        p = subprocess.run(cmd, cwd=td, capture_output=True, text=True, timeout=timeout)
         text = ""
         for fn in ("KEYFOUNDKEYFOUND.txt", "VANITYKEYFOUND.txt"):
             kf = os.path.join(td, fn)
             text += open(kf).read() if os.path.exists(kf) else ""
         return p, parse_keyfound(text)
+
+
+def _uniq(xs):
+    return [x for i, x in enumerate(xs) if x not in xs[:i]]
+
+
+def check_against_reference(ref: dict, argv: list[str], name: str):
+    """Run `argv` and compare exit status, KEYFOUND records and stdout hit blocks with the fixture.
+    BSGS fixtures compare each distinct hit once: overlapping bases let several reference threads
+    print the same key before the exit.  Fixtures of runs stopped after `killed_after` seconds
+    compare the hits below `cmp_below` (the reference's threads covered those keys in time)."""
+    kill = 8 if ref.get("killed_after") else None
+    p, hits = run_cli(argv, kill_after=kill)
+    assert p.returncode == ref["exit"], p.stdout[-2000:] + p.stderr[-2000:]
+    blocks = sorted(STDOUT_BLOCK.findall(p.stdout))
+    if "cmp_below" in ref:
+        lim = int(ref["cmp_below"], 16)
+        hits = [h for h in hits if int(h["key"], 16) < lim]
+        blocks = [b for b in blocks if int(re.search(r"Key: ([0-9a-f]+)", b).group(1), 16) < lim]
+    ref_hits, ref_blocks = ref["hits"], ref["stdout_blocks"]
+    if name.startswith("bsgs"):
+        hits, ref_hits, blocks, ref_blocks = _uniq(hits), _uniq(ref_hits), _uniq(blocks), _uniq(ref_blocks)
+    assert hits == ref_hits
+    if ref.get("killed_after"):
+        # the stopped reference lost the tail of its block-buffered stdout: what it printed is there
+        rest = list(blocks)
+        for b in ref_blocks:
+            assert b in rest, b
+            rest.remove(b)
+    else:
+        assert blocks == ref_blocks
+    return p
