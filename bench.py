@@ -17,12 +17,19 @@ continue the same lanes.  The table build (baby steps) is replicated per GPU and
 reported.  torch.distributed (gloo, CPU tensors) provides the barrier and the max over ranks; the
 engine owns the GPU through its own HIP stream, synchronised on both sides of the timed region.
 
-roofline: dominant kernel = the BSGS giant-step walk.  achieved = algorithmic bytes per launch / mean
-launch time from HIP events recorded by the engine on its own stream.  Algorithmic bytes per giant
-point: 64 B with the default blocked layer 1 (one random 64-B line per probe), 128 B with the
-reference layout (~2 random lines per probe).  traffic: HBM bytes per launch from the
-committed rocprofv3 PMC summary (profiles/), or null.  The walk is VALU-bound, so a "valu" object
-reports VALU lane-instructions/s (PMC instructions per point x points/s) against the gfx950 peak.
+roofline: dominant kernel of each leg (the giant-step walk k_walk<7, 2048>; k_walk<0, 2048> and
+k_walk<3, 2048> for rmd160 / xpoint), from HIP events the engine records on its own stream around
+its launches.  The walks are bound by VALU issue, so "bound" is "valu":
+achieved = VALU wave-instructions per launch (rocprofv3 SQ_INSTS_VALU per point, committed under
+profiles/, x this run's points per launch) / mean launch time; peak = 1024 SIMDs x 2.4 GHz / 4
+cycles: one wave64 VALU instruction per SIMD per quad-cycle, the unit the SQ counters use and the
+measured issue cost of the 32-bit multiply-accumulate and carry ops the field math is made of
+(4.1-5.5 cycles at 4 waves/SIMD; only add/xor/mov issue in 2).  frac_at_measured_clock divides by
+the same peak at the clock the counters saw (GRBM_GUI_ACTIVE / 8 / kernel time: DVFS).  The HBM
+side is reported too ("hbm"): algorithmic bytes (BSGS: 64 B per giant point, one random line of the
+blocked layer 1; the reference layout's is 128 B) / launch time against 8 TB/s, and
+traffic = HBM bytes per launch from the PMC counters with the guide's gfx950 corrections
+(tools/pmc_summary.py), or null.
 cpu_baseline: rank 0 at N=1 only.  BSGS: the oracle's restatement of the giant-step loop
 (oracle/kh_oracle.c, keyhunt.cpp:4644-4880) on all host threads against the same GPU-built bloom
 (kind "port").  rmd160: the reference binary built from its own sources (oracle/_ref/keyhunt, kind
@@ -47,8 +54,11 @@ METRIC = "Mkeys/s at 1/2/4/8 GPU (BSGS b125; addr b66); HBM GB/s fraction"
 HBM_PEAK_GBS = 8000.0
 ALGO_BYTES_PER_GIANT_POINT = {0: 128, 1: 64}      # by layer-1 layout (reference, blocked)
 WALK_KERNEL = {0: "k_walk<4, 2048>", 1: "k_walk<7, 2048>"}    # KM_BSGS, KM_BSGSB on 4096-point groups
-# 256 CU x 4 SIMD x 32 lanes/clk (a wave64 VALU op issues over 2 clk) x 2.4 GHz, MI355X_MICROARCH.md
-VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
+# 1024 SIMDs x 2.4 GHz / 4 cycles per wave64 VALU instruction (SQ quad-cycle; measured issue cost of
+# v_mad_u64_u32 / v_add_co / v_addc_co / v_bitop3 at 4 waves per SIMD: 4.1-5.5 cycles)
+SIMDS = 256 * 4
+VALU_ISSUE_CYCLES = 4
+VALU_PEAK_GIPS = SIMDS * 2.4e9 / VALU_ISSUE_CYCLES / 1e9
 RANDOM16_CEILING_GPS = 51.36   # measured random 16-B nontemporal loads/s, 24 GB footprint (profiles/)
 PUZZLE125 = "0233709eb11e0d4439a729f21c2c443dedb727528229713f0065721ba8fa46f00e"
 PUZZLE130 = "03633cbe3ec02b9401c5effa144c5b4d22f87940259634858fc7e59b1c09937852"
@@ -181,14 +191,7 @@ def bsgs_leg(D: Dist, eng, args):
     ms_launch = ms / la
     bpp = ALGO_BYTES_PER_GIANT_POINT[info.layer1_layout]
     kname = WALK_KERNEL[info.layer1_layout]
-    achieved = pts_launch * bpp / (ms_launch / 1e3) / 1e9
-    traffic, tsrc = pmc_traffic(kname, pts_launch)
-    ipp = pmc_entry(kname).get("valu_lane_instructions_per_point")
-    valu = None
-    if ipp:
-        a = ipp * pts_launch / (ms_launch / 1e3) / 1e12
-        valu = {"achieved": a, "peak": VALU_PEAK_TOPS, "unit": "T lane-instr/s", "frac": a / VALU_PEAK_TOPS,
-                "lane_instructions_per_giant_point": ipp, "source": tsrc}
+    roof = walk_roofline(kname, pts_launch, ms_launch, bpp, la)
     # the probe is one random 16-B load per giant point: its own ceiling is the chip's random-load
     # rate at this footprint (tools/ubench_random2.hip, profiles/r01l_random16B.txt: 24 GB, nt loads)
     rand = {"achieved": pts_launch / (ms_launch / 1e3) / 1e9, "ceiling": RANDOM16_CEILING_GPS, "unit": "G loads/s",
@@ -202,26 +205,42 @@ def bsgs_leg(D: Dist, eng, args):
         "build_seconds": build_s,
         "candidates": eng.bsgs_candidates(),
         "info": info,
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": tsrc,
-                     "algorithmic_bytes_per_launch": pts_launch * bpp,
-                     "kernel": kname, "launches": la, "mean_launch_ms": ms_launch,
-                     "giant_points_per_launch": pts_launch,
-                     "algorithmic_bytes_per_giant_point": bpp},
-        "valu": valu,
+        "roofline": roof,
         "q": q,
     }
     return res
 
 
-def pmc_traffic(kernel: str, points_per_launch: float):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary of this kernel (bytes per point
-    measured as TCC_EA0_RDREQ x 64 B + WRITE_SIZE x 1 KiB, MI355X_MICROARCH.md HBM section), scaled
-    to this run's points per launch; None when no summary is present."""
-    d = pmc_entry(kernel)
-    if "hbm_bytes_per_point" not in d:
-        return None, None
-    return d["hbm_bytes_per_point"] * points_per_launch, d["source"]
+def walk_roofline(kname: str, pts_launch: float, ms_launch: float, algo_bytes_per_point: float, launches: int) -> dict:
+    """The roofline object of one walk kernel (see the module docstring): VALU issue bound, with the
+    HBM side alongside.  Counter-derived figures come from the newest profiles/r*_pmc_summary.json
+    holding this kernel and are scaled to this run's points per launch."""
+    d = pmc_entry(kname)
+    secs = ms_launch / 1e3
+    roof = {"bound": "valu", "achieved": None, "peak": VALU_PEAK_GIPS, "unit": "G VALU wave-instr/s", "frac": None,
+            "traffic": None, "kernel": kname, "launches": launches, "mean_launch_ms": ms_launch,
+            "points_per_launch": pts_launch, "source": d.get("source")}
+    if "valu_wave_instructions_per_dispatch" in d:
+        wipp = d["valu_wave_instructions_per_dispatch"] / d["points_per_dispatch"]
+        a = wipp * pts_launch / secs / 1e9
+        roof.update(achieved=a, frac=a / VALU_PEAK_GIPS, valu_wave_instructions_per_point=wipp,
+                    valu_lane_instructions_per_point=wipp * 64)
+        if d.get("effective_clock_ghz"):
+            clk = d["effective_clock_ghz"]
+            roof.update(effective_clock_ghz=clk, frac_at_measured_clock=a / (SIMDS * clk / VALU_ISSUE_CYCLES))
+    hbm = {"achieved": pts_launch * algo_bytes_per_point / secs / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "algorithmic_bytes_per_point": algo_bytes_per_point}
+    hbm["frac"] = hbm["achieved"] / HBM_PEAK_GBS
+    if "hbm_bytes_per_point" in d:
+        roof["traffic"] = d["hbm_bytes_per_point"] * pts_launch
+        hbm.update(traffic_bytes_per_point=d["hbm_bytes_per_point"],
+                   traffic_achieved=d["hbm_bytes_per_point"] * pts_launch / secs / 1e9)
+        hbm["traffic_frac"] = hbm["traffic_achieved"] / HBM_PEAK_GBS
+        for key in ("probe_read_bytes_per_point", "pad_bytes_per_point"):
+            if key in d:
+                hbm[key] = d[key]
+    roof["hbm"] = hbm
+    return roof
 
 
 def pmc_entry(kernel: str) -> dict:
@@ -248,9 +267,10 @@ def rmd160_leg(D: Dist, eng, args):
     T = timed(D, eng, args.warmup_rmd, args.steps_rmd, step)
     la, ms, pts = eng.kernel_time(K.engine.TIME_ADDRESS)
     keys = D.world * args.steps_rmd * chunk * 2
+    # algorithmic HBM bytes ~0 per key: the 16-B target filter block is L2-resident
     return {"value": keys / T / 1e6, "ms_per_step": T / args.steps_rmd * 1e3,
-            "kernel": {"name": "k_walk<KM_H160C>", "launches": la, "mean_launch_ms": ms / la,
-                       "points_per_launch": pts / la, "points_per_s_in_kernel": pts / (ms / 1e3)}}
+            "points_per_s_in_kernel": pts / (ms / 1e3),
+            "roofline": walk_roofline("k_walk<0, 2048>", pts / la, ms / la, 0, la)}
 
 
 def xpoint_leg(D: Dist, eng, args):
@@ -269,8 +289,8 @@ def xpoint_leg(D: Dist, eng, args):
     la, ms, pts = eng.kernel_time(K.engine.TIME_XPOINT)
     keys = D.world * args.steps_rmd * chunk
     return {"value": keys / T / 1e6, "ms_per_step": T / args.steps_rmd * 1e3,
-            "kernel": {"name": "k_walk<KM_XPOINT>", "launches": la, "mean_launch_ms": ms / la,
-                       "points_per_launch": pts / la, "points_per_s_in_kernel": pts / (ms / 1e3)}}
+            "points_per_s_in_kernel": pts / (ms / 1e3),
+            "roofline": walk_roofline("k_walk<3, 2048>", pts / la, ms / la, 0, la)}
 
 
 def cpu_host() -> dict:
@@ -440,18 +460,19 @@ def main():
             "build_seconds": prim["build_seconds"],
             "first_level_candidates": prim["candidates"],
             "roofline": prim["roofline"],
-            "valu": prim["valu"],
             "random_access": prim["random_access"],
             "cpu_baseline": cpu_b,
         }
         if sec:
             line["secondary"] = {"workload": "-m rmd160 -f tests/66.rmd -b 66 -l compress", "value": sec["value"],
                                  "unit": "Mkeys/s", "ms_per_step": sec["ms_per_step"], "steps": args.steps_rmd,
-                                 "kernel": sec["kernel"], "cpu_baseline": cpu_r}
+                                 "points_per_s_in_kernel": sec["points_per_s_in_kernel"],
+                                 "roofline": sec["roofline"], "cpu_baseline": cpu_r}
         if ter:
             line["tertiary"] = {"workload": "-m xpoint -f tests/63.pub -b 63", "value": ter["value"],
                                 "unit": "Mkeys/s", "ms_per_step": ter["ms_per_step"], "steps": args.steps_rmd,
-                                "kernel": ter["kernel"], "cpu_baseline": cpu_x}
+                                "points_per_s_in_kernel": ter["points_per_s_in_kernel"],
+                                "roofline": ter["roofline"], "cpu_baseline": cpu_x}
         json_out.write(json.dumps(line) + "\n")
         json_out.flush()
     D.close()

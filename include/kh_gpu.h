@@ -200,6 +200,13 @@ int kh_field_ops(kh_ctx *ctx, const uint8_t *a, const uint8_t *b, uint32_t n, ui
 int kh_bloom_check(kh_ctx *ctx, uint32_t layer, const uint8_t *items, uint32_t n, uint32_t len, uint8_t *out);
 /* copy a bloom back: layer 0 = target bloom, 1..3 = BSGS layers (256 shards concatenated, unpadded) */
 int kh_get_bloom(kh_ctx *ctx, uint32_t layer, uint8_t *buf, uint64_t cap, uint64_t *bytes);
+/* Parity hook: with logging enabled (cleared on every call), kh_bsgs_scan / _list record every
+ * first-level candidate -- layer-1 bloom positive, keyhunt.cpp:4819-4823 -- as (base ordinal within
+ * its call, giant index a = 1024 j + i within the base, layer-2 mask of its second check), in
+ * giant-step order per round.  kh_bsgs_get_candidates copies up to cap of them. */
+int kh_bsgs_log_candidates(kh_ctx *ctx, int enable);
+int kh_bsgs_get_candidates(kh_ctx *ctx, uint64_t *base_index, uint32_t *a, uint32_t *mask, uint64_t cap,
+                           uint64_t *n);
 /* bsgs_secondcheck's layer-2 hit mask for n base keys (32-byte big-endian each) against target
  * `target`, from the GPU kernel (k_refine) and from the host code: bit i set when the point
  * Q - base_key*G + AMP2[i] passes bloom_bPx2nd (keyhunt.cpp:5151-5184) */

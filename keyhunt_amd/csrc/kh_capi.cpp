@@ -357,6 +357,10 @@ struct kh_ctx {
   std::vector<ge> targets;
   std::vector<uint8_t> found;
   uint64_t candidates = 0;
+  // parity hook (kh_bsgs_log_candidates): every first-level candidate of the scans that follow
+  bool log_cands = false;
+  std::vector<uint64_t> cand_log_base;
+  std::vector<uint32_t> cand_log_a, cand_log_mask;
   uint64_t second_hits = 0;          // layer-2 positives of the second check (all candidates)
   // second check on the GPU (k_refine) unless KH_REFINE=host
   bool refine_host = false;
@@ -1989,6 +1993,13 @@ static int bsgs_scan_impl(kh_ctx *ctx, const u256 &st, const std::vector<u256> *
           for (auto &x : th) x.join();
         }
       }
+      if (ctx->log_cands)
+        for (auto &h : dh) {
+          const uint64_t t = R.t_round + h.idx;
+          ctx->cand_log_base.push_back(t / A_pts);
+          ctx->cand_log_a.push_back((uint32_t)(t % A_pts));
+          ctx->cand_log_mask.push_back(h.aux);
+        }
       // third checks for the (rare) layer-2 hits, in giant-step order; stop at the first key
       for (size_t i = 0; i < dh.size(); i++) {
         if (!dh[i].aux) continue;
@@ -2068,6 +2079,27 @@ int kh_bsgs_scan_list(kh_ctx *ctx, const uint8_t *bases, uint64_t n_bases, kh_bs
 // ---------------------------------------------------------------------------------------------
 // measurement
 // ---------------------------------------------------------------------------------------------
+int kh_bsgs_log_candidates(kh_ctx *ctx, int enable) {
+  if (!ctx) return KH_E_ARG;
+  ctx->log_cands = enable != 0;
+  ctx->cand_log_base.clear();
+  ctx->cand_log_a.clear();
+  ctx->cand_log_mask.clear();
+  return KH_OK;
+}
+
+int kh_bsgs_get_candidates(kh_ctx *ctx, uint64_t *base_index, uint32_t *a, uint32_t *mask, uint64_t cap,
+                           uint64_t *n) {
+  if (!ctx || !n) return KH_E_ARG;
+  *n = ctx->cand_log_base.size();
+  for (uint64_t i = 0; i < *n && i < cap; i++) {
+    if (base_index) base_index[i] = ctx->cand_log_base[i];
+    if (a) a[i] = ctx->cand_log_a[i];
+    if (mask) mask[i] = ctx->cand_log_mask[i];
+  }
+  return *n > cap ? KH_E_OVERFLOW : KH_OK;
+}
+
 int kh_bsgs_second_masks(kh_ctx *ctx, uint32_t target, const uint8_t *base_keys, uint32_t n, uint32_t *gpu_mask,
                          uint32_t *host_mask) {
   if (!ctx || !base_keys || !gpu_mask || !host_mask) return KH_E_ARG;

@@ -248,6 +248,19 @@ class Engine:
         self._chk(lib().kh_bsgs_refine_stats(self._ctx, ctypes.byref(a), ctypes.byref(b)), "kh_bsgs_refine_stats")
         return a.value, b.value
 
+    def bsgs_log_candidates(self, enable: bool = True) -> None:
+        self._chk(lib().kh_bsgs_log_candidates(self._ctx, int(enable)), "kh_bsgs_log_candidates")
+
+    def bsgs_logged_candidates(self) -> list[tuple[int, int, int]]:
+        """(base ordinal, a, layer-2 mask) of every first-level candidate since bsgs_log_candidates."""
+        n = ctypes.c_uint64()
+        lib().kh_bsgs_get_candidates(self._ctx, None, None, None, ctypes.c_uint64(0), ctypes.byref(n))
+        m = max(n.value, 1)
+        b, a, k = (ctypes.c_uint64 * m)(), (ctypes.c_uint32 * m)(), (ctypes.c_uint32 * m)()
+        self._chk(lib().kh_bsgs_get_candidates(self._ctx, b, a, k, ctypes.c_uint64(m), ctypes.byref(n)),
+                  "kh_bsgs_get_candidates")
+        return [(b[i], a[i], k[i]) for i in range(n.value)]
+
     def bsgs_second_masks(self, target: int, base_keys: list[int]) -> tuple[list[int], list[int]]:
         """(GPU, host) layer-2 masks of bsgs_secondcheck for each base key (parity hook)."""
         n = len(base_keys)

@@ -205,6 +205,23 @@ static void ge_add(ge *r, const ge *p, const ge *q) {
   r->x = rx; r->y = ry; r->inf = 0;
 }
 static void ge_neg(ge *r, const ge *p) { *r = *p; if (!p->inf) fe_neg(&r->y, &p->y); }
+/* Secp256K1::AddDirect (secp256k1/SECP256K1.cpp:455-478): the chord formula with no special cases;
+ * ModInv of dx = 0 leaves 0 (IntMod.cpp:497-500), so then s = 0 and x = -p1.x - p2.x.  Fermat's
+ * 0^(p-2) is 0 as well. */
+static void ge_add_direct(ge *r, const ge *p1, const ge *p2) {
+  fe dx, dy, inv, s, s2, rx, ry, t;
+  fe_sub(&dy, &p2->y, &p1->y);
+  fe_sub(&dx, &p2->x, &p1->x);
+  fe_inv(&inv, &dx);
+  fe_mul(&s, &dy, &inv);
+  fe_sqr(&s2, &s);
+  fe_sub(&rx, &s2, &p1->x);
+  fe_sub(&rx, &rx, &p2->x);
+  fe_sub(&t, &p2->x, &rx);
+  fe_mul(&ry, &t, &s);
+  fe_sub(&ry, &ry, &p2->y);
+  r->x = rx; r->y = ry; r->inf = 0;
+}
 
 static void gej_double(gej *r, const gej *p) {
   if (p->inf || u256_is_zero(&p->y)) { r->inf = 1; return; }
@@ -993,10 +1010,10 @@ static int bsgs_third(const bsgs_ctx *c, const fe *start, uint32_t a, const ge *
   sc_add(&base, start, &off);
   ge bp, nbp, S;
   scalar_mult_g(&bp, &base); ge_neg(&nbp, &bp);
-  ge_add(&S, Q, &nbp);
+  ge_add_direct(&S, Q, &nbp);
   for (int i = 0; i < 32; i++) {
     ge T; uint8_t xr[32];
-    ge_add(&T, &S, &c->amp3[i]);
+    ge_add_direct(&T, &S, &c->amp3[i]);
     fe_to_be(xr, &T.x);
     fe calc = {{(i == 0) ? p->m3 : (uint64_t)i * 2 * p->m3 + p->m3, 0, 0, 0}};
     if (or_bloom_check(c->bf3 + xr[0] * p->bytes[2], p->bits[2], p->hashes[2], xr, 32)) {
@@ -1028,15 +1045,40 @@ static int bsgs_second(const bsgs_ctx *c, const fe *start, uint32_t a, const ge 
   sc_add(&base, start, &off);
   ge bp, nbp, S;
   scalar_mult_g(&bp, &base); ge_neg(&nbp, &bp);
-  ge_add(&S, Q, &nbp);
+  ge_add_direct(&S, Q, &nbp);
   for (int i = 0; i < 32; i++) {
     ge T; uint8_t xr[32];
-    ge_add(&T, &S, &c->amp2[i]);
+    ge_add_direct(&T, &S, &c->amp2[i]);
     fe_to_be(xr, &T.x);
     if (or_bloom_check(c->bf2 + xr[0] * p->bytes[1], p->bits[1], p->hashes[1], xr, 32))
       if (bsgs_third(c, &base, (uint32_t)i, Q, key)) return 1;
   }
   return 0;
+}
+
+/* The layer-2 probes of bsgs_secondcheck (keyhunt.cpp:5151-5184) for base keys given directly: bit i
+ * of masks[j] is bloom_check(bloom_bPx2nd[X[0]], X) of S + AMP2[i], S = Q - base_keys[j]*G, for all
+ * 32 i (the reference stops at the first i whose third check finds the key; the engine's k_refine
+ * computes every bit).  A base key of 0 (no point) gives 0. */
+void or_bsgs_second_masks(const or_bsgs_params *p, const uint8_t *bf2, const uint8_t *base_keys_be, uint64_t n,
+                          const uint8_t qx[32], const uint8_t qy[32], uint32_t *masks) {
+  bsgs_ctx c; bsgs_ctx_init(&c, p, 0, bf2, 0, 0);
+  ge Q; fe_from_be(&Q.x, qx); fe_from_be(&Q.y, qy); Q.inf = 0;
+  for (uint64_t j = 0; j < n; j++) {
+    fe base; fe_from_be(&base, base_keys_be + 32 * j);
+    while (u256_cmp(&base, &SC_N) >= 0) u256_sub(&base, &base, &SC_N);
+    masks[j] = 0;
+    if (u256_is_zero(&base)) continue;
+    ge bp, nbp, S;
+    scalar_mult_g(&bp, &base); ge_neg(&nbp, &bp);
+    ge_add_direct(&S, &Q, &nbp);
+    for (int i = 0; i < 32; i++) {
+      ge T; uint8_t xr[32];
+      ge_add_direct(&T, &S, &c.amp2[i]);
+      fe_to_be(xr, &T.x);
+      if (or_bloom_check(bf2 + xr[0] * p->bytes[1], p->bits[1], p->hashes[1], xr, 32)) masks[j] |= 1u << i;
+    }
+  }
 }
 
 /* Refine one first-level candidate (base, a) for target (qx,qy).  Returns 1 + key. */

@@ -13,6 +13,7 @@ import subprocess
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "liboracle.so")
 _lib = None
+SECP_N = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141
 
 
 def build() -> str:
@@ -264,6 +265,15 @@ class BsgsTables:
         ok = lib().or_bsgs_refine(ctypes.byref(self.p), self.bf2, self.bf3, self.table, be32(base),
                                   ctypes.c_uint32(a), be32(q[0]), be32(q[1]), key)
         return int.from_bytes(key.raw, "big") if ok else None
+
+
+def bsgs_second_masks(tabs: "BsgsTables", base_keys: list[int], q: tuple[int, int]) -> list[int]:
+    """Layer-2 masks of bsgs_secondcheck (keyhunt.cpp:5151-5184) for the given base keys."""
+    n = len(base_keys)
+    buf = b"".join(be32(k % SECP_N) for k in base_keys) or bytes(32)
+    out = (ctypes.c_uint32 * max(n, 1))()
+    lib().or_bsgs_second_masks(ctypes.byref(tabs.p), tabs.bf2, buf, ctypes.c_uint64(n), be32(q[0]), be32(q[1]), out)
+    return list(out[:n])
 
 
 def bsgs_giant_probe(p: BsgsParams, bf1, q: tuple[int, int], n_groups_per_thread: int, threads: int) -> int:

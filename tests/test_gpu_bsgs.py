@@ -1,6 +1,6 @@
 """BSGS parity on the GPU: baby-step tables (three bloom layers + sorted bP table) bit-identical to
-the reference's at small M (tests/golden/ref_vectors.json), first-level candidate sets identical to
-the CPU oracle, and found keys identical to the reference CLI on known-answer windows
+the reference's at small M (tests/golden/ref_vectors.json), first-level candidates (base, giant
+index) and their layer-2 masks identical to the CPU oracle's, and found keys identical to the reference CLI on known-answer windows
 (tests/golden/ref_e2e.json), including the benchmark configuration (k = 128)."""
 import hashlib
 import json
@@ -42,13 +42,18 @@ def test_candidates_and_key_vs_oracle(engine, oracle, n, k):
     q = oracle.pubkey(key)
     # the key sits near the END of the 4th base (beyond the 3rd base's overlap when k = 3)
     start = key - 4 * 2 * p.n + 12345
-    # no hit in the first 3 bases: identical candidate counts; found in the 4th
+    # no hit in the first 3 bases: the same first-level candidates (base, giant index a) as the
+    # oracle's sequential worker, and the same layer-2 masks of their second checks; found in the 4th
     engine.bsgs_set_targets([q])
-    c0 = engine.bsgs_candidates()
+    engine.bsgs_log_candidates(True)
     assert engine.bsgs_scan(start, 3) == []
-    got_c = engine.bsgs_candidates() - c0
+    got = engine.bsgs_logged_candidates()
+    engine.bsgs_log_candidates(False)
     okey, ocands = tabs.scan(start, 3, q)
-    assert okey is None and got_c == len(ocands)
+    assert okey is None and len(ocands) > 0
+    assert sorted((b, a) for b, a, _ in got) == sorted(ocands)
+    omask = oracle.bsgs_second_masks(tabs, [start + b * 2 * p.n + a * 2 * p.m for b, a, _ in got], q)
+    assert [m for _, _, m in got] == omask
     found = engine.bsgs_scan(start + 3 * 2 * p.n, 1)
     assert found == [(0, key)]
     okey, _ = tabs.scan(start, 4, q)
@@ -203,15 +208,19 @@ def test_scan_list_equals_scan(engine, oracle):
     assert engine.bsgs_scan_list([start + 3 * 2 * p.n, start + 9 * 2 * p.n]) == []
 
 
-def test_second_check_masks_gpu_equal_host(engine, oracle):
-    """k_refine (the GPU second check) against the host's bsgs_secondcheck twin, bit for bit: base
-    keys inside the target's 2M window (true layer-2 hits, one bit each) and random ones (FPs only)."""
+@pytest.mark.parametrize("n,k", [(1 << 22, 2), (1 << 24, 3)])
+def test_second_check_masks_gpu_equal_oracle(engine, oracle, n, k):
+    """k_refine (the GPU second check) against the oracle's bsgs_secondcheck (keyhunt.cpp:5151-5184,
+    AddDirect restated with its dx = 0 value) and the engine's host twin, bit for bit: base keys
+    inside the target's 2M window (true layer-2 hits), random ones (FPs only), edges, and bases with
+    S = +-AMP2[i] (the reference's AddDirect with dx = 0)."""
     import random
     rnd = random.Random(1234)
-    n, k = 1 << 22, 2
     p = oracle.bsgs_params(n, k)
+    tabs = oracle.BsgsTables(p)
     engine.bsgs_setup(n, k)
     engine.bsgs_build()
+    assert engine.get_bloom(2) == tabs.bf2.raw
     key = 0x3F00DEADBEEF0123
     engine.bsgs_set_targets([oracle.pubkey(key)])
     near = [key - rnd.randrange(0, 2 * p.m) for _ in range(600)]
@@ -222,6 +231,7 @@ def test_second_check_masks_gpu_equal_host(engine, oracle):
     bases = near + far + edge + amp
     g, h = engine.bsgs_second_masks(0, bases)
     assert g == h
+    assert g == oracle.bsgs_second_masks(tabs, bases, oracle.pubkey(key))
     hits = [m for m in g[: len(near)] if m]
     assert len(hits) >= 590   # d in [1, 2M): the AMP2 step covering d hits layer 2
     assert all(bin(m).count("1") <= 2 for m in hits)

@@ -161,3 +161,22 @@ def test_oracle_keccak_and_eth_against_reference_vectors(oracle):
         assert (x.to_bytes(32, "big") + y.to_bytes(32, "big")).hex() == v["xy"]
         assert oracle.keccak256(bytes.fromhex(v["xy"])).hex() == v["keccak"]
         assert oracle.eth_address(x, y).hex() == v["address"]
+
+
+def test_oracle_second_masks_window(oracle):
+    """bsgs_secondcheck's layer-2 probes (keyhunt.cpp:5151-5184): for base = key - d, S = d*G and
+    S + AMP2[i] = (d - (2i+1)M2)*G, whose X is a layer-2 baby X exactly when |d - (2i+1)M2| is in
+    [1, M2]: bit min(d // (2 M2), 31) is set for every d in [1, 64 M2] but the odd multiples of M2
+    (there S = -AMP2[i], AddDirect's dx = 0); other bits only as FPs.  Base key 0 gives 0."""
+    import random
+    p = oracle.bsgs_params(1 << 22, 2)
+    t = oracle.BsgsTables(p)
+    key = 0x3F00DEADBEEF0123
+    q = oracle.pubkey(key)
+    rnd = random.Random(7)
+    ds = [1, p.m2 - 1, p.m2 + 1, 2 * p.m2, 64 * p.m2] + [rnd.randrange(1, 64 * p.m2 + 1) for _ in range(60)]
+    ds = [d for d in ds if d % (2 * p.m2) != p.m2]
+    masks = oracle.bsgs_second_masks(t, [key - d for d in ds], q)
+    for d, m in zip(ds, masks):
+        assert (m >> min(d // (2 * p.m2), 31)) & 1, (d, hex(m))
+    assert oracle.bsgs_second_masks(t, [0], q) == [0]

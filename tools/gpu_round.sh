@@ -28,12 +28,15 @@ fi
 if has pmc; then
   i=0
   for c in "TCC_EA0_RDREQ_sum TCC_HIT_sum TCC_MISS_sum" "WRITE_SIZE" "FETCH_SIZE" \
-           "SQ_INSTS_VALU SQ_WAVES SQ_INSTS_SALU SQ_INSTS_SMEM" \
+           "SQ_INSTS_VALU SQ_WAVES SQ_INSTS_SALU SQ_INSTS_SMEM GRBM_GUI_ACTIVE" \
            "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU"; do
     i=$((i + 1))
     timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d $O/pmc/p$i -o run -- \
       python3 $R/tools/pmc_run.py > $O/pmc_p$i.log 2>&1 || { echo "pmc pass $i rc=$?"; tail -20 $O/pmc_p$i.log; exit 1; }
   done
+  # the same workload's kernel durations (a run of its own, no counters)
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/pmc/trace -o run -- \
+    python3 $R/tools/pmc_run.py > $O/pmc_trace.log 2>&1 || { echo "pmc trace rc=$?"; tail -20 $O/pmc_trace.log; exit 1; }
   echo "pmc ok"
 fi
 if has config5; then

@@ -1,7 +1,17 @@
-"""Aggregate rocprofv3 --pmc passes (gpurun_out/pmc*/<pass>/run_counter_collection.csv) into a per-kernel
-summary: counters per dispatch and per point.  Corrections (MI355X_MICROARCH.md, HBM section):
-FETCH_SIZE is TCC_EA0_RDREQ x 64 B (KB units); we report read bytes = TCC_EA0_RDREQ x 64 B and write
-bytes = WRITE_SIZE x 1024 B.  Both are per dispatch of the profiled geometry."""
+"""Aggregate rocprofv3 --pmc passes (<src>/<pass>/run_counter_collection.csv) into a per-kernel summary:
+counters per dispatch and per point, HBM bytes with the MI355X_MICROARCH.md corrections, and the
+VALU issue rate.
+
+HBM (guide, HBM section): reads = TCC_EA0_RDREQ x 64 B, writes = WRITE_SIZE x 1 KiB (exact for 16-B
+per-lane streaming stores).  On gfx950 a wide coalesced read (16 B/lane, the inversion pad's
+loads) is tallied at HALF its bytes, so the pad's read bytes are counted separately: the pad is
+written once and read back once per group, so its read bytes equal the dispatch's write bytes
+(WRITE_SIZE; the few hit/candidate records are noise).  Then
+  pad_read      = WRITE_SIZE x 1 KiB                    (exact)
+  other_read    = TCC_EA0_RDREQ x 64 B - pad_read / 2    (the probes' random 16-B loads: 64 B each)
+  hbm_bytes     = other_read + pad_read + pad_write.
+VALU: SQ_INSTS_VALU counts wave-instructions; lane-instructions per point = x 64 / points (each
+lane walks its own points).  Clock: GRBM_GUI_ACTIVE / 8 (summed over the 8 XCDs) / kernel time."""
 import csv
 import glob
 import json
@@ -10,9 +20,10 @@ from collections import defaultdict
 
 src = sys.argv[1]
 out = sys.argv[2]
-points = json.loads(sys.argv[3])   # {"k_walk<4>": points_per_dispatch, ...}
+points = json.loads(sys.argv[3])   # {"k_walk<7, 2048>": points_per_dispatch, ...}
+durations = json.loads(sys.argv[4]) if len(sys.argv) > 4 else {}  # kernel -> mean ns (kernel trace)
 agg = defaultdict(lambda: defaultdict(list))
-for f in glob.glob(f"{src}/*/run_counter_collection.csv"):
+for f in glob.glob(f"{src}/*/run_counter_collection.csv") + glob.glob(f"{src}/*/*/run_counter_collection.csv"):
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"].split("(")[0].replace("void ", "").strip()
         agg[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
@@ -23,14 +34,21 @@ for k, d in agg.items():
     per = {c: sum(v) / len(v) for c, v in d.items()}
     p = points[k]
     e = {"counters_per_dispatch": per, "points_per_dispatch": p}
-    if "TCC_EA0_RDREQ_sum" in per:
-        e["hbm_read_bytes_per_dispatch"] = per["TCC_EA0_RDREQ_sum"] * 64
-    if "WRITE_SIZE" in per:
-        e["hbm_write_bytes_per_dispatch"] = per["WRITE_SIZE"] * 1024
-    if "hbm_read_bytes_per_dispatch" in e and "hbm_write_bytes_per_dispatch" in e:
-        e["hbm_bytes_per_point"] = (e["hbm_read_bytes_per_dispatch"] + e["hbm_write_bytes_per_dispatch"]) / p
+    if "TCC_EA0_RDREQ_sum" in per and "WRITE_SIZE" in per:
+        wr = per["WRITE_SIZE"] * 1024
+        rd_counted = per["TCC_EA0_RDREQ_sum"] * 64
+        other = rd_counted - wr / 2
+        e.update(hbm_read_bytes_counted_per_dispatch=rd_counted, hbm_write_bytes_per_dispatch=wr,
+                 pad_read_bytes_per_dispatch=wr, probe_read_bytes_per_dispatch=other,
+                 hbm_bytes_per_dispatch=other + 2 * wr,
+                 hbm_bytes_per_point=(other + 2 * wr) / p, probe_read_bytes_per_point=other / p,
+                 pad_bytes_per_point=2 * wr / p, uncorrected_bytes_per_point=(rd_counted + wr) / p)
     if "SQ_INSTS_VALU" in per:
+        e["valu_wave_instructions_per_dispatch"] = per["SQ_INSTS_VALU"]
         e["valu_lane_instructions_per_point"] = per["SQ_INSTS_VALU"] * 64 / p
+    if "GRBM_GUI_ACTIVE" in per and k in durations:
+        e["kernel_ns"] = durations[k]
+        e["effective_clock_ghz"] = per["GRBM_GUI_ACTIVE"] / 8 / durations[k]
     res[k] = e
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps(res, indent=1))
