@@ -1896,6 +1896,10 @@ static int bsgs_scan_impl(kh_ctx *ctx, const u256 &st, const std::vector<u256> *
       Aw.n_points = cont ? total_groups * 2 * H : rg * 2 * H;
       Aw.bloom = ctx->d_bl[0];
       Aw.bd = ctx->bd[0];
+      // blocked layer 1: shard stride in 16-B blocks when the whole layer's block index fits 32 bits
+      Aw.bstride16 = ctx->bd[0].stride % 16 == 0 && ctx->bd[0].stride / 16 < (1u << 24)
+                         ? (uint32_t)(ctx->bd[0].stride / 16)
+                         : 0xFFFFFFFFu;
       Aw.hit_count = ctx->d_cnt2[slot];
       Aw.hits = ctx->d_hits2[slot];
       Aw.hit_cap = ctx->cand_cap;

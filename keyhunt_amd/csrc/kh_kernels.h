@@ -43,6 +43,23 @@ static_assert(KH_WALK_H >= 64 && KH_WALK_H <= 512 && (512 % KH_WALK_H) == 0,
 // FP 5.6e-7 (Poisson block load) vs the reference's 1e-6; one 16-byte load per probe, no hashing.
 #define KH_BLK_BITS_MUL 3
 
+// Variant switches of the BSGS giant walk (k_walk<KM_BSGSB, KH_WALK_HB>), A/B-measured:
+//   KH_TAB_LDS   the delta table staged in LDS (one 1024-thread workgroup per CU, ds_read_b128
+//                broadcasts) instead of scalar-cache reads into SGPRs
+//   KH_TAB_VCOPY the table values a step uses twice copied to VGPRs once (a carry chain with an SGPR
+//                operand and a carry-in reads two scalars, over gfx9's constant-bus limit of one, so
+//                the compiler copies the SGPR in every such instruction)
+//   KH_REC32     the probe's block index in 32-bit arithmetic (mul_hi + mad_u24)
+#ifndef KH_TAB_LDS
+#define KH_TAB_LDS 0
+#endif
+#ifndef KH_TAB_VCOPY
+#define KH_TAB_VCOPY 0
+#endif
+#ifndef KH_REC32
+#define KH_REC32 0
+#endif
+
 enum kh_walk_mode {
   KM_H160C = 0,   // hash160(02||X), hash160(03||X)          -l compress
   KM_H160U = 1,   // hash160(04||X||Y)                       -l uncompress
@@ -91,6 +108,7 @@ struct walk_args {
   // kh_kernels.hip tblk_probe); null for vanity prefixes
   const uint4 *tblk;
   uint32_t tblocks;
+  uint32_t bstride16;  // BSGS blocked layer 1: shard stride in 16-byte blocks (KH_REC32 when < 2^24)
   // BSGS build
   uint8_t *bl1, *bl2, *bl3;
   kh::bloom_desc bd2, bd3;

@@ -362,6 +362,12 @@ __device__ __forceinline__ uint4 ld_nt16(const uint4 *p) {
 }
 // {global block index (shard*stride + block*16)/16, limbs 4, 3, 2} of one point
 __device__ __forceinline__ uint4 blk_record(const walk_args &A, const fe &x) {
+#if KH_REC32
+  if (A.bstride16 < (1u << 24)) {  // wave-uniform: the whole layer's block index fits 32 bits
+    const uint32_t idx = __umul24(x.d[7] >> 24, A.bstride16) + blk_index(x.d[5], A.bd);
+    return make_uint4(idx, x.d[4], x.d[3], x.d[2]);
+  }
+#endif
   const uint64_t off = (uint64_t)(x.d[7] >> 24) * A.bd.stride + (uint64_t)blk_index(x.d[5], A.bd) * 16;
   return make_uint4((uint32_t)(off >> 4), x.d[4], x.d[3], x.d[2]);
 }
@@ -447,11 +453,61 @@ constexpr int walk_lb() {
                                                                     : KH_WALK_LB;
 }
 
+// KH_TAB_LDS: the giant walk's table in LDS, one 1024-thread workgroup per CU
+template <int MODE, int H>
+constexpr bool tab_lds() {
+  return KH_TAB_LDS && MODE == KM_BSGSB && H == KH_WALK_HB;
+}
+template <int MODE, int H>
+constexpr int walk_threads() {
+  return tab_lds<MODE, H>() ? 1024 : 256;
+}
+template <int MODE, int H>
+constexpr int walk_blocks_per_cu() {
+  return tab_lds<MODE, H>() ? 1 : walk_lb<MODE>();  // either way walk_lb waves per SIMD
+}
+// a uniform 32-bit value copied into a VGPR (KH_TAB_VCOPY): later carry chains then read it there
+__device__ __forceinline__ uint32_t to_vgpr(uint32_t s) {
+  uint32_t v;
+  asm("v_mov_b32 %0, %1" : "=v"(v) : "s"(s));
+  return v;
+}
+__device__ __forceinline__ void fe_to_vgpr(fe &a) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) a.d[i] = to_vgpr(a.d[i]);
+}
+
 template <int MODE, int H = KH_WALK_H>
-__global__ void __launch_bounds__(256, walk_lb<MODE>()) k_walk(walk_args A) {
+__global__ void __launch_bounds__((walk_threads<MODE, H>()), (walk_blocks_per_cu<MODE, H>())) k_walk(walk_args A) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  constexpr bool LDS = tab_lds<MODE, H>();
+  // table entry i: x in words [0,8), y in [8,16); LDS: uint4 [i*4 .. i*4+3]
+  __shared__ uint4 tabl[LDS ? (H + 1) * 4 : 1];
+  if constexpr (LDS) {
+    const uint4 *src = reinterpret_cast<const uint4 *>(A.tab);
+    for (uint32_t k = threadIdx.x; k < (uint32_t)(H + 1) * 4; k += blockDim.x) tabl[k] = src[k];
+    __syncthreads();
+  }
   if (g >= A.L) return;
   kconst_ptr T = (kconst_ptr)A.tab;  // (H+1) x {x[8], y[8]}, wave-uniform reads
+  auto ld_tx = [&](fe &x, int i) {
+    if constexpr (LDS) {
+      const uint4 a = tabl[i * 4], b = tabl[i * 4 + 1];
+      x.d[0] = a.x; x.d[1] = a.y; x.d[2] = a.z; x.d[3] = a.w;
+      x.d[4] = b.x; x.d[5] = b.y; x.d[6] = b.z; x.d[7] = b.w;
+    } else {
+      load_fe_k(x, T + i * 16);
+    }
+  };
+  auto ld_ty = [&](fe &y, int i) {
+    if constexpr (LDS) {
+      const uint4 a = tabl[i * 4 + 2], b = tabl[i * 4 + 3];
+      y.d[0] = a.x; y.d[1] = a.y; y.d[2] = a.z; y.d[3] = a.w;
+      y.d[4] = b.x; y.d[5] = b.y; y.d[6] = b.z; y.d[7] = b.w;
+    } else {
+      load_fe_k(y, T + i * 16 + 8);
+    }
+  };
   uint4 *__restrict__ scr = A.scratch;
   const size_t L = A.L;
   fe cx, cy;
@@ -470,7 +526,7 @@ __global__ void __launch_bounds__(256, walk_lb<MODE>()) k_walk(walk_args A) {
 #pragma unroll 1
     for (int i = 0; i < H; i++) {
       fe tx, dx;
-      load_fe_k(tx, T + i * 16);
+      ld_tx(tx, i);
       fe_sub(dx, tx, cx);
       if (i == 0)
         acc = dx;
@@ -479,8 +535,8 @@ __global__ void __launch_bounds__(256, walk_lb<MODE>()) k_walk(walk_args A) {
       if (!SPARSE || (i & 1) == 0) scr_store(scr, slot(i), acc);
     }
     fe t2x, t2y, dxn;
-    load_fe_k(t2x, T + H * 16);
-    load_fe_k(t2y, T + H * 16 + 8);
+    ld_tx(t2x, H);
+    ld_ty(t2y, H);
     fe_sub(dxn, t2x, cx);
     fe inv, inv_n;
     fe_mul(inv, acc, dxn);
@@ -505,13 +561,17 @@ __global__ void __launch_bounds__(256, walk_lb<MODE>()) k_walk(walk_args A) {
 #pragma unroll 1
     for (int i = H - 1; i >= 0; i--) {
       fe tx, ty, di;
-      load_fe_k(tx, T + i * 16);
-      load_fe_k(ty, T + i * 16 + 8);
+      ld_tx(tx, i);
+      ld_ty(ty, i);
+      if constexpr (KH_TAB_VCOPY && MODE == KM_BSGSB && !LDS) {
+        fe_to_vgpr(tx);  // used by dx and C.x + T.x
+        fe_to_vgpr(ty);  // used by both dy
+      }
       if (i > 0) {
         fe dx;
         if (SPARSE && ((i - 1) & 1)) {  // prefix[i-1] = prefix[i-2] * dx[i-1] (pre holds prefix[i-2])
           fe tpx, d1;
-          load_fe_k(tpx, T + (i - 1) * 16);
+          ld_tx(tpx, i - 1);
           fe_sub(d1, tpx, cx);
           fe_mul(pre, pre, d1);
         }
@@ -523,8 +583,6 @@ __global__ void __launch_bounds__(256, walk_lb<MODE>()) k_walk(walk_args A) {
       } else {
         di = inv;
       }
-      fe nty;
-      fe_neg(nty, ty);
       if constexpr (MODE == KM_BSGSB) {
         // The previous pair's block loads are issued first and tested after this pair's field
         // math: the loads fly during it.  Only their addresses cross the loop edge (ALU values),
@@ -549,6 +607,8 @@ __global__ void __launch_bounds__(256, walk_lb<MODE>()) k_walk(walk_args A) {
         plive = (cidx - off < A.n_points ? 1u : 0u) | (i < H - 1 && cidx + off < A.n_points ? 2u : 0u);
         continue;
       }
+      fe nty;
+      fe_neg(nty, ty);
       if constexpr (MODE == KM_BSGS) {
         // both points first, then one lockstep probe of the pair (two loads in flight per lane)
         fe xm, xp, s, dy, sx;
@@ -892,9 +952,12 @@ namespace kh {
 hipError_t launch_walk(int mode, const walk_args &A, hipStream_t st, int H) {
   dim3 block(256), grid((A.L + 255) / 256);
   if (H == KH_WALK_HB) {
+    constexpr int TB = walk_threads<KM_BSGSB, KH_WALK_HB>();
     switch (mode) {
       case KM_BSGS: hipLaunchKernelGGL((k_walk<KM_BSGS, KH_WALK_HB>), grid, block, 0, st, A); break;
-      case KM_BSGSB: hipLaunchKernelGGL((k_walk<KM_BSGSB, KH_WALK_HB>), grid, block, 0, st, A); break;
+      case KM_BSGSB:
+        hipLaunchKernelGGL((k_walk<KM_BSGSB, KH_WALK_HB>), dim3((A.L + TB - 1) / TB), dim3(TB), 0, st, A);
+        break;
       case KM_XPOINT: hipLaunchKernelGGL((k_walk<KM_XPOINT, KH_WALK_HB>), grid, block, 0, st, A); break;
       case KM_H160C: hipLaunchKernelGGL((k_walk<KM_H160C, KH_WALK_HB>), grid, block, 0, st, A); break;
       default: return hipErrorInvalidValue;

@@ -228,6 +228,18 @@ __device__ __forceinline__ uint64_t mad_acc(uint32_t a, uint32_t b, uint64_t acc
 }
 #endif
 
+#if defined(__HIP_DEVICE_COMPILE__)
+// acc + a*b where the sum provably fits 64 bits (no carry to count)
+__device__ __forceinline__ uint64_t mad_nc(uint32_t a, uint32_t b, uint64_t acc) {
+  uint64_t d, m;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(d), "=s"(m) : "v"(a), "v"(b), "v"(acc));
+  return d;
+}
+#endif
+#ifndef KH_SAFE_ADDC
+#define KH_SAFE_ADDC 1
+#endif
+
 KH_HD void fe_mul(fe &r, const fe &a, const fe &b) {
   uint32_t t[16];
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -240,7 +252,11 @@ KH_HD void fe_mul(fe &r, const fe &a, const fe &b) {
     for (int i = 0; i < 8; i++) {
       const int j = k - i;
       if (j < 0 || j > 7) continue;
-      acc = mad_acc(a.d[i], b.d[j], acc, cnt);
+      // column 0 and the first product of column 1 cannot carry: (2^32-1)^2 + 2^32 - 1 < 2^64
+      if (KH_SAFE_ADDC && (k == 0 || (k == 1 && i == 0)))
+        acc = mad_nc(a.d[i], b.d[j], acc);
+      else
+        acc = mad_acc(a.d[i], b.d[j], acc, cnt);
     }
     t[k] = (uint32_t)acc;
     acc = (acc >> 32) | ((uint64_t)cnt << 32);
@@ -283,7 +299,12 @@ KH_HD void fe_sqr(fe &r, const fe &a) {
     for (int i = 0; i < 8; i++) {
       const int j = k - i;
       if (j <= i || j > 7) continue;
-      acc = mad_acc(a.d[i], a.d[j], acc, cnt);
+      // columns 1 and 2 hold one cross product each and column 3 starts on an accumulator of at
+      // most 2^32 - 1: their first products cannot carry
+      if (KH_SAFE_ADDC && k <= 3 && i == 0)
+        acc = mad_nc(a.d[i], a.d[j], acc);
+      else
+        acc = mad_acc(a.d[i], a.d[j], acc, cnt);
     }
     t[k] = (uint32_t)acc;
     acc = (acc >> 32) | ((uint64_t)cnt << 32);

@@ -32,8 +32,11 @@ def test_field_ops_vs_reference(engine):
 
 def test_field_ops_random(engine):
     rng = random.Random(1234)
-    a = [rng.randrange(P) for _ in range(4096)] + [0, 1, P - 1, 2**255, P - 2**32]
-    b = [rng.randrange(P) for _ in range(4096)] + [P - 1, P - 1, P - 1, 2**255, 2**32]
+    # carry-heavy edges: all-ones limbs in every product column and reduction position
+    edges = [P - 1 - k for k in range(4)] + [2**224 - 1, 2**192 - 1, (2**256 - 1) // 3, 2**128 - 1, P - 2**128,
+                                             2**255 - 1]
+    a = [rng.randrange(P) for _ in range(4096)] + [0, 1, P - 1, 2**255, P - 2**32] + edges + edges[::-1]
+    b = [rng.randrange(P) for _ in range(4096)] + [P - 1, P - 1, P - 1, 2**255, 2**32] + edges + edges
     got = engine.field_ops(a, b)
     for x, y, (mul, sqr, inv, add, sub) in zip(a, b, got):
         assert mul == x * y % P

@@ -13,5 +13,5 @@ import json, sys
 for n in sys.argv[1:]:
     d = json.load(open(f"gpurun_out/ab/{n}.json"))
     print(n, d["giant_points_per_s"] / 1e9, d["roofline"]["mean_launch_ms"],
-          d["secondary"]["kernel"]["points_per_s_in_kernel"] / 1e9, d["tertiary"]["kernel"]["points_per_s_in_kernel"] / 1e9)
+          d["secondary"]["points_per_s_in_kernel"] / 1e9, d["tertiary"]["points_per_s_in_kernel"] / 1e9)
 P

@@ -1,5 +1,5 @@
 // ubench_field3.hip -- field mul/sqr: hipcc-scheduled (kh_math.h) vs the generated single-statement
-// asm forms (kh_field_asm.h), single and paired (development tool).
+// asm forms (kh_field_asm.h, generated: python3 tools/gen_field_asm.py), single and paired (development tool).
 //   timing: 2 independent chains per lane, ITERS steps, launch bounds (256, 4) as in the BSGS walk;
 //   correctness: every variant's final values equal the kh_math.h device result, and a one-step
 //   check of 2^18 lanes x edge-case inputs against the host (portable) code.
