@@ -14,11 +14,17 @@
 // built and written (bsgsd sets FLAGSAVEREADFILE = 1, bsgsd.cpp:238).  Requests are served one
 // at a time ("One client at the time", BSGSD.md).
 //
-// Options: -k K, -n N, -i IP (127.0.0.1), -p PORT (8080), -6 (skip file checksums), -g GPUs
-// (default all), -L reference|blocked (layer-1 layout), -t (accepted; one host thread per GPU).
+// Like the reference daemon, the .tbl file is followed by its MD5 in keyhunt_bsgs_2_<M3>.tbl.md5
+// whenever it is written or read (bsgsd.cpp:1625-1670, 2073-2095).
+//
+// Options: -k K, -n N, -i IP (127.0.0.1), -p PORT (8080), -6 (skip file checksums), -g contexts
+// (default: one per GPU; more than the GPUs share them), -L reference|blocked (layer-1 layout),
+// -t (accepted; one host thread per context), --ptable FILE, --ptable-size SIZE, --load-ptable,
+// --ptable-cache (the bP table file, its FILE.md5 and FILE.cache, bsgsd.cpp:1314-1470, 1719-1755).
 #include <arpa/inet.h>
 #include <ctype.h>
 #include <errno.h>
+#include <fcntl.h>
 #include <getopt.h>
 #include <netinet/in.h>
 #include <signal.h>
@@ -26,6 +32,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <sys/socket.h>
+#include <sys/stat.h>
 #include <unistd.h>
 
 #include <atomic>
@@ -55,6 +62,9 @@ struct options {
   bool skip_checksum = false;
   int gpus = 0;
   uint32_t layer1 = KH_LAYER1_BLOCKED;
+  const char *ptable = nullptr;
+  uint64_t ptable_size = 0;
+  bool load_ptable = false, ptable_cache = false;
 } opt;
 
 std::vector<gpu> g_gpus;
@@ -70,23 +80,157 @@ bool send_all(int fd, const char *buf, size_t len) {
   return true;
 }
 
-// -S files of this N/k: read when all four exist, else build (+ write from the first GPU)
-int load_or_build(gpu &g, bool first, bool files_present) {
-  if (files_present) return kh_bsgs_load(g.ctx, ".", opt.skip_checksum ? KH_LOAD_SKIP_CHECKSUM : 0);
-  int r = kh_bsgs_build(g.ctx);
-  if (!r && first) r = kh_bsgs_save(g.ctx, ".");
-  return r;
+std::string tbl_name(const kh_bsgs_info &I) {
+  char f[96];
+  snprintf(f, sizeof f, "keyhunt_bsgs_2_%llu.tbl", (unsigned long long)I.m3);
+  return f;
 }
 
 bool files_present(const kh_bsgs_info &I) {
-  char f[4][96];
+  char f[3][96];
   snprintf(f[0], 96, "keyhunt_bsgs_4_%llu.blm", (unsigned long long)I.m);
   snprintf(f[1], 96, "keyhunt_bsgs_6_%llu.blm", (unsigned long long)I.m2);
   snprintf(f[2], 96, "keyhunt_bsgs_7_%llu.blm", (unsigned long long)I.m3);
-  snprintf(f[3], 96, "keyhunt_bsgs_2_%llu.tbl", (unsigned long long)I.m3);
   for (auto &x : f)
     if (access(x, R_OK) != 0) return false;
+  return access(tbl_name(I).c_str(), R_OK) == 0;
+}
+
+// MD5 of `path` into path.md5, reporting an earlier one (bsgsd.cpp:1444-1462, 1648-1665)
+bool md5_refresh(const std::string &path, uint8_t md5[16], bool report) {
+  const std::string md5_path = path + ".md5";
+  if (!md5_of_file(path.c_str(), md5)) {
+    fprintf(stderr, "[W] Unable to compute MD5 for bP table %s\n", path.c_str());
+    return false;
+  }
+  uint8_t disk[16];
+  if (report && read_md5_file(md5_path.c_str(), disk))
+    printf(memcmp(disk, md5, 16) == 0 ? "[+] bP table MD5 verified (%s)\n" : "[W] bP table MD5 mismatch (%s); refreshing\n",
+           md5_path.c_str());
+  if (!write_md5_file(md5_path.c_str(), md5)) fprintf(stderr, "[W] Unable to write bP table MD5 file %s\n", md5_path.c_str());
   return true;
+}
+
+// The table files of the first context, in the reference daemon's order (bsgsd.cpp:1314-1470,
+// 1473-1755, 2073-2095): the --ptable file is opened (read-only with --load-ptable: its rows are the
+// table), the -S files are read when all four exist (the .tbl only without --ptable), --ptable-cache
+// then writes CACHE_TARGET.md5 / .cache from the rows the target holds AT THAT POINT (a fresh --ptable
+// file still holds zeros), and only then are the tables built and the files written.  `rows` returns
+// the --load-ptable rows for every context.
+int first_tables(gpu &g, std::vector<uint8_t> &rows, bool &present) {
+  const kh_bsgs_info &I = g.info;
+  const uint64_t bytes = I.m3 * 16;
+  const std::string tbl = tbl_name(I);
+  std::string target;  // bptable_cache_target
+  std::vector<uint8_t> target_rows(bytes, 0);
+  uint8_t md5[16];
+  bool md5_ready = false;
+  if (opt.ptable) {
+    target = opt.ptable;
+    if (opt.load_ptable) {
+      FILE *f = fopen(opt.ptable, "rb");
+      if (!f) {
+        fprintf(stderr, "[E] Cannot open bP table file\n");
+        return KH_E_IO;
+      }
+      struct stat st;
+      if (fstat(fileno(f), &st) != 0 || (uint64_t)st.st_size < bytes) {
+        fclose(f);
+        fprintf(stderr, "[E] Existing bP table file too small\n");
+        return KH_E_IO;
+      }
+      rows.resize(bytes);
+      const bool ok = bytes == 0 || fread(rows.data(), bytes, 1, f) == 1;
+      fclose(f);
+      if (!ok) {
+        fprintf(stderr, "[E] Cannot read bP table file\n");
+        return KH_E_IO;
+      }
+      target_rows = rows;
+      md5_ready = md5_refresh(opt.ptable, md5, true);
+    } else {
+      const uint64_t map_bytes = std::max(bytes, opt.ptable_size);
+      int fd = open(opt.ptable, O_RDWR | O_CREAT, 0600);
+      if (fd < 0) {
+        fprintf(stderr, "[E] Cannot create bP table file\n");
+        return KH_E_IO;
+      }
+      struct stat st;
+      bool ok = fstat(fd, &st) == 0;
+      if (ok && (uint64_t)st.st_size < map_bytes) ok = ftruncate(fd, (off_t)map_bytes) == 0;
+      if (ok && map_bytes < (1ull << 20)) {  // small mappings are zeroed (bsgsd.cpp:1424-1431)
+        std::vector<uint8_t> zero(map_bytes, 0);
+        ok = pwrite(fd, zero.data(), map_bytes, 0) == (ssize_t)map_bytes;
+      }
+      if (ok && bytes) ok = pread(fd, target_rows.data(), bytes, 0) == (ssize_t)bytes;
+      close(fd);
+      if (!ok) {
+        fprintf(stderr, "[E] Cannot resize bP table file\n");
+        return KH_E_IO;
+      }
+    }
+  }
+  present = files_present(I);
+  if (present) {
+    int r = kh_bsgs_load(g.ctx, ".", opt.skip_checksum ? KH_LOAD_SKIP_CHECKSUM : 0);
+    if (r) return r;
+    if (!opt.ptable) {  // the .tbl was read: it is now the cache target, with its MD5 refreshed
+      target = tbl;
+      uint64_t got = 0;
+      r = kh_get_bsgs_table(g.ctx, target_rows.data(), I.m3, &got);
+      if (r) return r;
+      md5_ready = md5_refresh(tbl, md5, true);
+    }
+  }
+  if (opt.ptable_cache && !target.empty()) {
+    if (!md5_ready) md5_ready = md5_refresh(target, md5, false);
+    if (md5_ready) {
+      const std::string cache = target + ".cache";
+      const int st = bptable_cache_status(cache.c_str(), md5, I.m3);
+      if (st == 1) {
+        printf("[+] bP table cache hit (%s)\n", cache.c_str());
+      } else {
+        printf(st < 0 ? "[W] bP table cache mismatch (%s); rebuilding\n" : "[I] bP table cache not found (%s); creating\n",
+               cache.c_str());
+        if (bptable_cache_write(cache.c_str(), md5, target_rows.data(), I.m3))
+          printf("[+] bP table cache refreshed (%s)\n", cache.c_str());
+        else
+          printf("[W] Unable to write bP table cache to %s\n", cache.c_str());
+      }
+    }
+  }
+  if (!present) {
+    const bool had_tbl = access(tbl.c_str(), F_OK) == 0;
+    int r = kh_bsgs_build(g.ctx);
+    if (!r) r = kh_bsgs_save(g.ctx, ".");
+    if (r) return r;
+    if (opt.load_ptable && !had_tbl) {
+      unlink(tbl.c_str());  // the table came from the --ptable file: no .tbl is written
+    } else {
+      md5_refresh(tbl, md5, false);
+    }
+  }
+  if (present && opt.ptable && !opt.load_ptable) {
+    // the reference never reads the .tbl with --ptable: it rebuilds and rewrites it (the same
+    // bytes) and its MD5 (bsgsd.cpp:2073-2095)
+    uint8_t m[16];
+    md5_refresh(tbl, m, false);
+  }
+  if (opt.ptable && !opt.load_ptable) {  // the built rows land in the --ptable file
+    std::vector<uint8_t> built(bytes);
+    uint64_t got = 0;
+    int r = kh_get_bsgs_table(g.ctx, built.data(), I.m3, &got);
+    if (r) return r;
+    int fd = open(opt.ptable, O_RDWR);
+    bool ok = fd >= 0 && (bytes == 0 || pwrite(fd, built.data(), bytes, 0) == (ssize_t)bytes);
+    if (fd >= 0) ok = close(fd) == 0 && ok;
+    if (!ok) {
+      fprintf(stderr, "[E] Cannot write bP table file\n");
+      return KH_E_IO;
+    }
+  }
+  if (opt.load_ptable) return kh_bsgs_set_table(g.ctx, rows.data(), I.m3);
+  return KH_OK;
 }
 
 // the walk of one request: bases from, from + 2N, ... while base < to, over every GPU
@@ -139,7 +283,7 @@ bool search(const fe &qx, const fe &qy, const U &from, const U &to, U &key) {
   return found;
 }
 
-void record_key(const U &key, bool compressed) {
+void record_key(const U &key, bool compressed, bool at_base) {
   uint8_t kb[32], pxy[64];
   u_to_be32(key, kb);
   kh_pubkeys(g_gpus[0].ctx, kb, 1, pxy);
@@ -152,7 +296,10 @@ void record_key(const U &key, bool compressed) {
     pub = hex(&p, 1) + hex(pxy, 64);
   }
   const std::string k = u_hex(key);
-  printf("[+] Thread Key found privkey %s\n[+] Publickey %s\n", k.c_str(), pub.c_str());
+  // a key at the very start of a base is caught by the reference's base-point check, whose line
+  // ends in two spaces (bsgsd.cpp:2544-2548); the giant-step path prints none (2724)
+  printf(at_base ? "[+] Thread Key found privkey %s  \n[+] Publickey %s\n" : "[+] Thread Key found privkey %s\n[+] Publickey %s\n",
+         k.c_str(), pub.c_str());
   FILE *f = fopen("KEYFOUNDKEYFOUND.txt", "a");
   if (f) {
     fprintf(f, "Key found privkey %s\nPublickey %s\n", k.c_str(), pub.c_str());
@@ -260,6 +407,18 @@ void handle(int fd) {
   bool compressed = false;
   U from, to;
   if (!parse_pubkey(pub.c_str(), qx, qy, compressed)) {
+    // Secp256K1::ParsePublicKeyHex's own message first (SECP256K1.cpp:327-372); a 04 key of the
+    // wrong length makes the reference exit (361), here it is refused like the others
+    const size_t len = pub.size();
+    const std::string pfx = len >= 2 ? pub.substr(0, 2) : "";
+    if (len < 2)
+      printf("ParsePublicKeyHex: Error invalid public key specified (66 or 130 character length)\n");
+    else if ((pfx == "02" || pfx == "03") && len != 66)
+      printf("ParsePublicKeyHex: Error invalid public key specified (66 character length)\n");
+    else if (pfx == "04" && len != 130)
+      printf("ParsePublicKeyHex: Error invalid public key specified (130 character length)\n");
+    else if (pfx != "02" && pfx != "03" && pfx != "04")
+      printf("ParsePublicKeyHex: Error invalid public key specified (Unexpected prefix (only 02,03 or 04 allowed)\n");
     printf("Invalid publickey format from client %s\n", pub.c_str());
     send_all(fd, bad, strlen(bad));
     return;
@@ -271,7 +430,11 @@ void handle(int fd) {
   }
   U key;
   const bool ok = search(qx, qy, from, to, key);
-  if (ok) record_key(key, compressed);
+  if (ok) {
+    uint64_t rem = 1;
+    if (u_cmp(key, from) >= 0) u_divmod_u64(u_sub(key, from), 2 * g_gpus[0].info.n, &rem);
+    record_key(key, compressed, rem == 0);
+  }
   const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   std::string body = ok ? u_hex(key) + "\n" : std::string("404 Not Found\n");
   std::string reply;
@@ -294,8 +457,30 @@ int main(int argc, char **argv) {
   printf("[+] Version 0.2.230519 Satoshi Quest (bsgsd-amd: MI355X engine)\n");
   int c;
   bool have_n = false;
-  while ((c = getopt(argc, argv, "6hk:n:t:p:i:g:L:B:")) != -1) {
+  static const struct option long_opts[] = {{"ptable", required_argument, 0, 1},
+                                           {"ptable-size", required_argument, 0, 2},
+                                           {"load-ptable", no_argument, 0, 3},
+                                           {"ptable-cache", no_argument, 0, 4},
+                                           {0, 0, 0, 0}};
+  while ((c = getopt_long(argc, argv, "6hk:n:t:p:i:g:L:B:", long_opts, nullptr)) != -1) {
     switch (c) {
+      case 1: opt.ptable = optarg; break;  // bsgsd.cpp:828-829
+      case 2: {                            // bsgsd.cpp:830-841
+        char *end;
+        uint64_t v = strtoull(optarg, &end, 10);
+        if (*end) {
+          switch (tolower(*end)) {
+            case 'k': v *= 1024ull; break;
+            case 'm': v *= 1024ull * 1024ull; break;
+            case 'g': v *= 1024ull * 1024ull * 1024ull; break;
+            case 't': v *= 1024ull * 1024ull * 1024ull * 1024ull; break;
+          }
+        }
+        opt.ptable_size = v;
+        break;
+      }
+      case 3: opt.load_ptable = true; break;
+      case 4: opt.ptable_cache = true; break;
       case '6':
         opt.skip_checksum = true;
         fprintf(stderr, "[W] Skipping checksums on files\n");
@@ -327,11 +512,16 @@ int main(int argc, char **argv) {
         break;
       case 'h':
       default:
-        printf("usage: %s [-k K] [-n N] [-i IP] [-p PORT] [-6] [-g GPUS] [-L reference|blocked]\n", argv[0]);
+        printf("usage: %s [-k K] [-n N] [-i IP] [-p PORT] [-6] [-g CONTEXTS] [-L reference|blocked]\n"
+               "       [--ptable FILE [--ptable-size SIZE] [--load-ptable] [--ptable-cache]]\n", argv[0]);
         return c == 'h' ? EXIT_SUCCESS : EXIT_FAILURE;
     }
   }
   (void)have_n;
+  if (opt.load_ptable && !opt.ptable) {  // bsgsd.cpp:951-954
+    fprintf(stderr, "--load-ptable requires --ptable <file>\n");
+    return EXIT_FAILURE;
+  }
   if (!validate_nk(opt.n, opt.k)) return EXIT_FAILURE;
   printf("[+] Mode BSGS secuential\n[+] N = 0x%llx\n", (unsigned long long)opt.n);
   int ndev = 0;
@@ -344,13 +534,19 @@ int main(int argc, char **argv) {
   if (opt.gpus <= 0) opt.gpus = ndev;
   g_gpus.resize(opt.gpus);
   bool present = false;
+  std::vector<uint8_t> ptable_rows;
   for (int d = 0; d < opt.gpus; d++) {
     gpu &g = g_gpus[d];
     int r = kh_open(d % ndev, &g.ctx);
     if (!r) r = kh_bsgs_set_layer1(g.ctx, opt.layer1);
     if (!r) r = kh_bsgs_setup(g.ctx, opt.n, opt.k, &g.info);
-    if (!r && d == 0) present = files_present(g.info);
-    if (!r) r = load_or_build(g, d == 0, present);
+    if (!r && d == 0) {
+      r = first_tables(g, ptable_rows, present);
+    } else if (!r) {  // the first context left the four files (or the --ptable rows) for the others
+      r = kh_bsgs_load(g.ctx, ".", opt.skip_checksum ? KH_LOAD_SKIP_CHECKSUM : 0);
+      if (r == KH_E_IO) r = kh_bsgs_build(g.ctx);  // --load-ptable without a .tbl
+      if (!r && opt.load_ptable) r = kh_bsgs_set_table(g.ctx, ptable_rows.data(), g.info.m3);
+    }
     if (r) {
       fprintf(stderr, "[E] GPU %d: %s (%s)\n", d, kh_strerror(r), g.ctx ? kh_last_error(g.ctx) : "");
       return EXIT_FAILURE;

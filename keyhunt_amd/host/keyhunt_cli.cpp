@@ -610,52 +610,21 @@ void ptable_cache(const std::vector<uint8_t> &rows, uint64_t m3, bool loaded) {
   const std::string md5_path = std::string(opt.ptable) + ".md5", cache_path = std::string(opt.ptable) + ".cache";
   uint8_t md5[16];
   bool ready = false;
-  auto write_md5 = [&]() {
-    FILE *f = fopen(md5_path.c_str(), "w");
-    bool ok = f && fprintf(f, "%s\n", hex(md5, 16).c_str()) > 0;
-    if (f) fclose(f);
-    if (!ok) fprintf(stderr, "[W] Unable to write bP table MD5 file %s\n", md5_path.c_str());
-  };
   if (loaded) {
-    char buf[64] = {0};
-    FILE *f = fopen(md5_path.c_str(), "r");
-    if (f) {
-      size_t n = fread(buf, 1, sizeof buf - 1, f);
-      fclose(f);
-      buf[n] = 0;
-      if (char *nl = strchr(buf, '\n')) *nl = 0;
-      if (strlen(buf) >= 32) {
-        buf[32] = 0;
-        ready = hex2bin(buf, md5, 16);
-      }
-    }
+    ready = read_md5_file(md5_path.c_str(), md5);
     if (ready) printf("[+] bP table MD5 loaded (%s)\n", md5_path.c_str());
   }
   if (!ready) {
     ready = md5_of_file(opt.ptable, md5);
-    if (ready)
-      write_md5();
-    else
+    if (ready) {
+      if (!write_md5_file(md5_path.c_str(), md5))
+        fprintf(stderr, "[W] Unable to write bP table MD5 file %s\n", md5_path.c_str());
+    } else {
       fprintf(stderr, "[W] Unable to compute MD5 for bP table %s\n", opt.ptable);
+    }
   }
   if (!ready) return;
-#pragma pack(push, 1)
-  struct {
-    uint32_t magic, version;
-    uint64_t entries;
-    uint8_t md5[16];
-    uint64_t boundaries[257];
-  } fc, disk;
-#pragma pack(pop)
-  static_assert(sizeof(fc) == 2088, "struct bptable_cache_file");
-  int status = 0;
-  if (FILE *f = fopen(cache_path.c_str(), "rb")) {
-    if (fread(&disk, sizeof disk, 1, f) == 1)
-      status = disk.magic == 0x42505443u && disk.version == 1 && disk.entries == m3 && !memcmp(disk.md5, md5, 16)
-                   ? 1
-                   : -1;
-    fclose(f);
-  }
+  const int status = bptable_cache_status(cache_path.c_str(), md5, m3);
   if (status == 1) {
     printf("[+] bP table cache hit (%s)\n", cache_path.c_str());
     return;
@@ -664,21 +633,7 @@ void ptable_cache(const std::vector<uint8_t> &rows, uint64_t m3, bool loaded) {
     printf("[W] bP table cache mismatch (%s); rebuilding\n", cache_path.c_str());
   else
     printf("[I] bP table cache not found (%s); creating\n", cache_path.c_str());
-  memset(&fc, 0, sizeof fc);
-  fc.magic = 0x42505443u;  // 'BPTC'
-  fc.version = 1;
-  fc.entries = m3;
-  memcpy(fc.md5, md5, 16);
-  uint64_t pos = 0;
-  for (int bucket = 0; bucket < 256; bucket++) {
-    while (pos < m3 && rows[pos * 16] < bucket) pos++;
-    fc.boundaries[bucket] = pos;
-  }
-  fc.boundaries[256] = m3;
-  FILE *f = fopen(cache_path.c_str(), "wb");
-  bool ok = f && fwrite(&fc, sizeof fc, 1, f) == 1;
-  if (f) fclose(f);
-  if (ok)
+  if (bptable_cache_write(cache_path.c_str(), md5, rows.data(), m3))
     printf("[+] bP table cache refreshed (%s)\n", cache_path.c_str());
   else
     printf("[W] Unable to write bP table cache to %s\n", cache_path.c_str());

@@ -435,4 +435,65 @@ inline bool md5_of_file(const char *path, uint8_t out[16]) {
   return ok;
 }
 
+// FILE.md5 as keyhunt writes and reads it: the hex MD5 and a newline (keyhunt.cpp:186-241)
+inline bool read_md5_file(const char *path, uint8_t out[16]) {
+  char buf[64] = {0};
+  FILE *f = fopen(path, "r");
+  if (!f) return false;
+  size_t n = fread(buf, 1, sizeof buf - 1, f);
+  fclose(f);
+  buf[n] = 0;
+  if (char *nl = strchr(buf, '\n')) *nl = 0;
+  if (strlen(buf) < 32) return false;
+  buf[32] = 0;
+  return hex2bin(buf, out, 16);
+}
+inline bool write_md5_file(const char *path, const uint8_t md5[16]) {
+  FILE *f = fopen(path, "w");
+  bool ok = f && fprintf(f, "%s\n", hex(md5, 16).c_str()) > 0;
+  if (f) ok = fclose(f) == 0 && ok;
+  return ok;
+}
+
+// FILE.cache: struct bptable_cache_file {magic 'BPTC', version 1, entries, md5, 257 bucket starts by
+// value[0] of the 16-byte rows} (keyhunt.cpp:137-143, 186-241; bsgsd.cpp:255-360)
+#pragma pack(push, 1)
+struct bptable_cache_file {
+  uint32_t magic, version;
+  uint64_t entries;
+  uint8_t md5[16];
+  uint64_t boundaries[257];
+};
+#pragma pack(pop)
+static_assert(sizeof(bptable_cache_file) == 2088, "struct bptable_cache_file");
+// 1: a cache of this MD5 and row count, -1: another one, 0: none readable
+inline int bptable_cache_status(const char *path, const uint8_t md5[16], uint64_t m3) {
+  bptable_cache_file disk;
+  FILE *f = fopen(path, "rb");
+  if (!f) return 0;
+  int st = 0;
+  if (fread(&disk, sizeof disk, 1, f) == 1)
+    st = disk.magic == 0x42505443u && disk.version == 1 && disk.entries == m3 && !memcmp(disk.md5, md5, 16) ? 1 : -1;
+  fclose(f);
+  return st;
+}
+inline bool bptable_cache_write(const char *path, const uint8_t md5[16], const uint8_t *rows, uint64_t m3) {
+  bptable_cache_file fc;
+  memset(&fc, 0, sizeof fc);
+  fc.magic = 0x42505443u;
+  fc.version = 1;
+  fc.entries = m3;
+  memcpy(fc.md5, md5, 16);
+  uint64_t pos = 0;
+  for (int bucket = 0; bucket < 256; bucket++) {
+    while (pos < m3 && rows[pos * 16] < bucket) pos++;
+    fc.boundaries[bucket] = pos;
+  }
+  fc.boundaries[256] = m3;
+  FILE *f = fopen(path, "wb");
+  bool ok = f && fwrite(&fc, sizeof fc, 1, f) == 1;
+  if (f) ok = fclose(f) == 0 && ok;
+  return ok;
+}
+
 }  // namespace khh

@@ -14,8 +14,11 @@ TEST INFRASTRUCTURE.  Runs in the development container only (needs /root/refere
   tests/golden/ref_data/         the -S target caches (data_<hex>.dat) the reference CLI writes for
                                  address / rmd160 / xpoint / eth target files, with
                                  ref_data/index.json (name, size, masked sha256, hit set of the run).
+  tests/golden/ref_bsgsd.json    a transcript of the reference daemon (oracle/_ref/bsgsd): every
+                                 request of BSGSD_REQUESTS with the raw reply bytes and the lines the
+                                 daemon printed for it, plus its KEYFOUNDKEYFOUND.txt.
 
-Usage:  python oracle/make_golden.py [--vectors] [--e2e] [--tables] [--data]
+Usage:  python oracle/make_golden.py [--vectors] [--e2e] [--tables] [--data] [--bsgsd]
 """
 from __future__ import annotations
 
@@ -243,16 +246,127 @@ def gen_e2e(only: list[str] | None = None) -> None:
         json.dump(results, f, indent=1, sort_keys=True)
 
 
+PUB63 = "0365ec2994b8cc0a20d40dd69edfe55ca32a54bcbbaa6b0ddcff36049301a54579"
+
+
+def http_post(body: str) -> bytes:
+    b = body.encode()
+    return (b"POST / HTTP/1.1\r\nHost: 127.0.0.1\r\nContent-Type: application/json\r\nContent-Length: %d\r\n\r\n"
+            % len(b)) + b
+
+
+# (name, raw request bytes) for the daemon transcript (bsgsd.cpp:3307-3579): found (both range
+# spellings, and a key at the very start of a base, bsgsd.cpp:2544-2561), not found, malformed
+# lines, a bad pubkey prefix / length, and the HTTP POST forms
+BSGSD_REQUESTS = [
+    ("line_found", f"{PUB63} 7cce5efdac000000:7cce5efdad000000\n".encode()),
+    ("line_found_3tok", f"{PUB63} 7cce5efdac000000 7cce5efdad000000\n".encode()),
+    ("line_found_at_base", f"{PUB63} 7cce5efdaccf6808:7cce5efdadcf6808\n".encode()),
+    ("line_not_found", f"{PUB63} 4000000000000000:4000000001000000\n".encode()),
+    ("line_one_token", b"nonsense\n"),
+    ("line_no_colon", f"{PUB63} 7cce5efdac000000\n".encode()),
+    ("line_bad_hex", f"{PUB63} zz:7cce5efdad000000\n".encode()),
+    ("line_bad_prefix", b"0565ec2994b8cc0a20d40dd69edfe55ca32a54bcbbaa6b0ddcff36049301a54579 1:2\n"),
+    ("line_short_02", b"0265ec2994b8 1:2\n"),
+    ("http_found", http_post(json.dumps({"pubkey": PUB63, "from": "7cce5efdac000000", "to": "7cce5efdad000000"}))),
+    ("http_not_found", http_post(json.dumps({"pubkey": PUB63, "from": "4000000000000000", "to": "4000000001000000"}))),
+    ("http_missing_field", http_post(json.dumps({"pubkey": PUB63}))),
+    ("http_bad_hex", http_post(json.dumps({"pubkey": PUB63, "from": "xyz", "to": "7cce5efdad000000"}))),
+]
+BSGSD_ARGS = ["-n", "0x1000000", "-k", "2"]
+
+
+def mask_elapsed(reply: bytes) -> bytes:
+    return re.sub(rb"X-Elapsed-Seconds: [0-9.]+", b"X-Elapsed-Seconds: *", reply)
+
+
+# daemon starts whose table files are recorded: (name, extra args, fresh directory?)
+BSGSD_STARTS = [
+    ("default", [], True),
+    ("default_restart", [], False),
+    ("ptable_cache", ["--ptable", "pt.bin", "--ptable-cache"], True),
+    ("ptable_load_cache", ["--ptable", "pt.bin", "--load-ptable", "--ptable-cache"], False),
+]
+
+
+def start_ref_daemon(cwd: str, extra: list[str]):
+    import socket
+    import time
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    logp = os.path.join(cwd, "daemon.log")
+    log = open(logp, "w")
+    # line-buffered stdout so each request's lines can be told apart
+    p = subprocess.Popen(["stdbuf", "-oL", os.path.join(HERE, "_ref", "bsgsd")] + BSGSD_ARGS + extra +
+                         ["-t", "4", "-p", str(port), "-i", "127.0.0.1"], cwd=cwd, stdout=log, stderr=subprocess.STDOUT)
+    t0 = time.time()
+    while "Listening in" not in open(logp).read():
+        assert p.poll() is None and time.time() - t0 < 300, "reference daemon did not start"
+        time.sleep(0.2)
+    return p, port, logp
+
+
+def table_digests(d: str) -> dict:
+    return {f: masked_table_digest(os.path.join(d, f)) for f in sorted(os.listdir(d)) if f != "daemon.log"}
+
+
+def gen_bsgsd() -> None:
+    import socket
+    import time
+    subprocess.run(["make", "-s", "-C", HERE, "-f", "Makefile.ref", "-j8"], check=True)
+    out = {"args": BSGSD_ARGS, "requests": [], "starts": [],
+           "_generator": "oracle/make_golden.py --bsgsd running oracle/_ref/bsgsd"}
+    with tempfile.TemporaryDirectory() as td:
+        p, port, logp = start_ref_daemon(td, [])
+        for name, req in BSGSD_REQUESTS:
+            before = len(open(logp).read())
+            with socket.create_connection(("127.0.0.1", port), timeout=300) as c:
+                c.sendall(req)
+                reply = b""
+                while True:
+                    b = c.recv(4096)
+                    if not b:
+                        break
+                    reply += b
+            time.sleep(0.3)
+            lines = [ln for ln in open(logp).read()[before:].split("\n")
+                     if ln and not ln.startswith(("[+] Accepting", "[+] Closing"))]
+            out["requests"].append({"name": name, "request": req.decode(), "reply": mask_elapsed(reply).decode(),
+                                    "stdout": lines})
+            print(name, reply[:60], lines, flush=True)
+        p.kill()
+        p.wait()
+        out["keyfound"] = open(os.path.join(td, "KEYFOUNDKEYFOUND.txt")).read()
+    d = None
+    for name, extra, fresh in BSGSD_STARTS:
+        if fresh:
+            if d:
+                shutil.rmtree(d)
+            d = tempfile.mkdtemp()
+        p, port, logp = start_ref_daemon(d, extra)
+        p.kill()
+        p.wait()
+        msgs = [ln.strip() for ln in open(logp).read().split("\n") if "bP table" in ln]
+        out["starts"].append({"name": name, "extra": extra, "fresh": fresh, "files": table_digests(d), "bptable_lines": msgs})
+        print(name, out["starts"][-1], flush=True)
+    shutil.rmtree(d)
+    with open(os.path.join(REPO, "tests", "golden", "ref_bsgsd.json"), "w") as f:
+        json.dump(out, f, indent=1)
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--vectors", action="store_true")
     ap.add_argument("--e2e", action="store_true")
     ap.add_argument("--tables", action="store_true")
     ap.add_argument("--data", action="store_true")
+    ap.add_argument("--bsgsd", action="store_true")
     ap.add_argument("--only", nargs="*")
     a = ap.parse_args()
-    if not a.vectors and not a.e2e and not a.tables and not a.data:
-        a.vectors = a.e2e = a.tables = a.data = True
+    if not a.vectors and not a.e2e and not a.tables and not a.data and not a.bsgsd:
+        a.vectors = a.e2e = a.tables = a.data = a.bsgsd = True
     if a.vectors:
         gen_vectors()
     if a.e2e:
@@ -261,3 +375,5 @@ if __name__ == "__main__":
         gen_tables()
     if a.data:
         gen_data()
+    if a.bsgsd:
+        gen_bsgsd()

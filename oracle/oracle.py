@@ -238,13 +238,27 @@ def bsgs_params(n: int, k: int) -> BsgsParams:
 
 
 class BsgsTables:
-    def __init__(self, p: BsgsParams):
+    def __init__(self, p: BsgsParams, build: bool = True):
         self.p = p
         self.bf1 = ctypes.create_string_buffer(256 * p.bytes[0])
         self.bf2 = ctypes.create_string_buffer(256 * p.bytes[1])
         self.bf3 = ctypes.create_string_buffer(256 * p.bytes[2])
         self.table = (BxRow * p.m3)()
-        lib().or_bsgs_build(ctypes.byref(p), self.bf1, self.bf2, self.bf3, self.table)
+        if build:
+            lib().or_bsgs_build(ctypes.byref(p), self.bf1, self.bf2, self.bf3, self.table)
+
+    @classmethod
+    def from_raw(cls, p: BsgsParams, bf1: bytes, bf2: bytes, bf3: bytes, table: bytes) -> "BsgsTables":
+        """Tables given as bytes (reference layout), e.g. ones already checked byte-identical to the
+        reference's: skips the oracle's own (slow, single-threaded) baby-step build."""
+        t = cls(p, build=False)
+        assert len(bf1) == len(t.bf1.raw) and len(bf2) == len(t.bf2.raw) and len(bf3) == len(t.bf3.raw)
+        assert len(table) == ctypes.sizeof(t.table)
+        ctypes.memmove(t.bf1, bf1, len(bf1))
+        ctypes.memmove(t.bf2, bf2, len(bf2))
+        ctypes.memmove(t.bf3, bf3, len(bf3))
+        ctypes.memmove(t.table, table, len(table))
+        return t
 
     def table_bytes(self) -> bytes:
         return ctypes.string_at(self.table, ctypes.sizeof(self.table))

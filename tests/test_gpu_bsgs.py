@@ -42,22 +42,55 @@ def test_candidates_and_key_vs_oracle(engine, oracle, n, k):
     q = oracle.pubkey(key)
     # the key sits near the END of the 4th base (beyond the 3rd base's overlap when k = 3)
     start = key - 4 * 2 * p.n + 12345
-    # no hit in the first 3 bases: the same first-level candidates (base, giant index a) as the
-    # oracle's sequential worker, and the same layer-2 masks of their second checks; found in the 4th
+    # no hit in the first 3 bases: the same first-level candidates as the oracle; found in the 4th
     engine.bsgs_set_targets([q])
-    engine.bsgs_log_candidates(True)
+    c0 = engine.bsgs_candidates()
     assert engine.bsgs_scan(start, 3) == []
-    got = engine.bsgs_logged_candidates()
-    engine.bsgs_log_candidates(False)
     okey, ocands = tabs.scan(start, 3, q)
-    assert okey is None and len(ocands) > 0
-    assert sorted((b, a) for b, a, _ in got) == sorted(ocands)
-    omask = oracle.bsgs_second_masks(tabs, [start + b * 2 * p.n + a * 2 * p.m for b, a, _ in got], q)
-    assert [m for _, _, m in got] == omask
+    assert okey is None and engine.bsgs_candidates() - c0 == len(ocands)
     found = engine.bsgs_scan(start + 3 * 2 * p.n, 1)
     assert found == [(0, key)]
     okey, _ = tabs.scan(start, 4, q)
     assert okey == key
+
+
+def test_candidate_list_and_masks_vs_oracle(engine, oracle):
+    """Full-fill layers (M/256 = 16384 entries per shard, past the 10000-entry floor, so layer 1
+    has the reference's 1e-6 false-positive rate): over 4000 bases (4.1M giant points) the engine's
+    first-level candidates -- (base, giant index a), keyhunt.cpp:4819-4823 -- are exactly the
+    oracle's sequential worker's, false positives included, and each one's layer-2 mask equals the
+    oracle's bsgs_secondcheck (keyhunt.cpp:5151-5184).  The engine's tables are first checked
+    byte-identical to the reference's (tests/golden/ref_tables.json's n100000000_k64 digests via
+    their raw shards), then handed to the oracle's scan."""
+    import hashlib
+    n, k, nb = 1 << 32, 64, 4000
+    p = oracle.bsgs_params(n, k)
+    engine.bsgs_setup(n, k, layer1=0)
+    engine.bsgs_build()
+    raw = [engine.get_bloom(1), engine.get_bloom(2), engine.get_bloom(3), engine.get_bsgs_table()]
+    tabs = oracle.BsgsTables.from_raw(p, *raw)
+    key = 0x5A5A5A5A123456
+    q = oracle.pubkey(key)
+    start = key - nb * 2 * p.n + 12345        # the key lies in the last base
+    okey, ocands = tabs.scan(start, nb, q)
+    assert okey == key and len(ocands) >= 3   # false positives and the true candidate
+    engine.bsgs_set_targets([q])
+    engine.bsgs_log_candidates(True)
+    assert engine.bsgs_scan(start, nb) == [(0, key)]
+    got = engine.bsgs_logged_candidates()
+    engine.bsgs_log_candidates(False)
+    got = sorted(got)
+    # the engine walks whole rounds: compare up to the oracle's last candidate (the true one)
+    assert [(b, a) for b, a, _ in got][: len(ocands)] == ocands
+    omask = oracle.bsgs_second_masks(tabs, [start + b * 2 * p.n + a * 2 * p.m for b, a in ocands], q)
+    assert [m for _, _, m in got[: len(ocands)]] == omask
+    assert omask[-1] != 0 and all(m == 0 for m in omask[:-1])
+    # the bP rows the oracle used are the reference's: the .tbl file the reference CLI wrote at this
+    # (n, k) is the rows then their sha256 (tests/golden/ref_tables.json); the three layers are
+    # compared file for file with the reference's in tests/test_gpu_tables.py
+    ref = json.load(open(os.path.join(GOLDEN, "ref_tables.json")))["n100000000_k64"]["files"]
+    tbl = raw[3] + hashlib.sha256(raw[3]).digest()
+    assert hashlib.sha256(tbl).hexdigest() == ref[f"keyhunt_bsgs_2_{p.m3}.tbl"]
 
 
 BSGS_CASES = [k for k in E2E if k.startswith("bsgs")]
