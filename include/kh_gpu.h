@@ -200,6 +200,12 @@ int kh_field_ops(kh_ctx *ctx, const uint8_t *a, const uint8_t *b, uint32_t n, ui
 int kh_bloom_check(kh_ctx *ctx, uint32_t layer, const uint8_t *items, uint32_t n, uint32_t len, uint8_t *out);
 /* copy a bloom back: layer 0 = target bloom, 1..3 = BSGS layers (256 shards concatenated, unpadded) */
 int kh_get_bloom(kh_ctx *ctx, uint32_t layer, uint8_t *buf, uint64_t cap, uint64_t *bytes);
+/* bsgsd semantics (bsgsd.cpp:2544-2561): the daemon's worker also tests every base point against the
+ * target, so a key that is exactly a base (offset 0, which the giant/baby steps reach only through the
+ * point at infinity) is found there; keyhunt's own worker (keyhunt.cpp:4625-4640) has no such test and
+ * misses it.  Off by default (the CLI's behaviour); bsgsd-amd turns it on. */
+int kh_bsgs_set_base_check(kh_ctx *ctx, int enable);
+
 /* Parity hook: with logging enabled (cleared on every call), kh_bsgs_scan / _list record every
  * first-level candidate -- layer-1 bloom positive, keyhunt.cpp:4819-4823 -- as (base ordinal within
  * its call, giant index a = 1024 j + i within the base, layer-2 mask of its second check), in

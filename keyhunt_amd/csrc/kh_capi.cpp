@@ -359,6 +359,7 @@ struct kh_ctx {
   uint64_t candidates = 0;
   // parity hook (kh_bsgs_log_candidates): every first-level candidate of the scans that follow
   bool log_cands = false;
+  bool base_check = false;  // kh_bsgs_set_base_check: the daemon's per-base Q == base*G test
   std::vector<uint64_t> cand_log_base;
   std::vector<uint32_t> cand_log_a, cand_log_mask;
   uint64_t second_hits = 0;          // layer-2 positives of the second check (all candidates)
@@ -2006,6 +2007,19 @@ static int bsgs_scan_impl(kh_ctx *ctx, const u256 &st, const std::vector<u256> *
         }
       // third checks for the (rare) layer-2 hits, in giant-step order; stop at the first key
       for (size_t i = 0; i < dh.size(); i++) {
+        const uint64_t t = R.t_round + dh[i].idx;
+        if (ctx->base_check && t % A_pts == 0) {
+          // bsgsd's test of each base point against the target (bsgsd.cpp:2544-2561): a key at the
+          // very start of a base is a candidate at a = 0 whose S = Q - base*G is the point at
+          // infinity, which no second check can refine (the CLI misses it, bsgsd reports it)
+          const u256 b = base_of(t / A_pts);
+          ge bp;
+          if (ctx->comb.mult(bp, b) && fe_eq(bp.x, Q.x) && fe_eq(bp.y, Q.y)) {
+            keys[i] = b;
+            ok[i] = 1;
+            break;
+          }
+        }
         if (!dh[i].aux) continue;
         ctx->second_hits += (uint64_t)__builtin_popcount(dh[i].aux);
         const u256 bk = key_of(i);
@@ -2083,6 +2097,12 @@ int kh_bsgs_scan_list(kh_ctx *ctx, const uint8_t *bases, uint64_t n_bases, kh_bs
 // ---------------------------------------------------------------------------------------------
 // measurement
 // ---------------------------------------------------------------------------------------------
+int kh_bsgs_set_base_check(kh_ctx *ctx, int enable) {
+  if (!ctx) return KH_E_ARG;
+  ctx->base_check = enable != 0;
+  return KH_OK;
+}
+
 int kh_bsgs_log_candidates(kh_ctx *ctx, int enable) {
   if (!ctx) return KH_E_ARG;
   ctx->log_cands = enable != 0;

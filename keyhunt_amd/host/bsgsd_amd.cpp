@@ -539,6 +539,7 @@ int main(int argc, char **argv) {
     gpu &g = g_gpus[d];
     int r = kh_open(d % ndev, &g.ctx);
     if (!r) r = kh_bsgs_set_layer1(g.ctx, opt.layer1);
+    if (!r) r = kh_bsgs_set_base_check(g.ctx, 1);  // bsgsd.cpp:2544-2561
     if (!r) r = kh_bsgs_setup(g.ctx, opt.n, opt.k, &g.info);
     if (!r && d == 0) {
       r = first_tables(g, ptable_rows, present);

@@ -86,6 +86,9 @@ E2E_RUNS = [
     # below the "cmp_below" key are compared
     ("bsgs_63_start_only", ["-m", "bsgs", "-f", "63.pub", "-r", "7cce5a0000000000", "-t", "8"], 300),
     ("xpoint_63_start_only", ["-m", "xpoint", "-f", "63.pub", "-r", "7cce5efdac000000", "-n", "0x100000", "-t", "8"], 20),
+    # a key exactly at a base start: keyhunt's worker reaches it only through the point at infinity
+    # and misses it (bsgsd has an extra per-base test and finds it, tests/golden/ref_bsgsd.json)
+    ("bsgs_63_key_at_base", ["-m", "bsgs", "-f", "63.pub", "-n", "0x1000000", "-k", "2", "-r", "7cce5efdaccf6808:7cce5efdadcf6808", "-t", "8"], 300),
     # no range at all: sequential from 1 (keyhunt.cpp:1250-1255)
     ("address_1to32_no_range", ["-m", "address", "-f", "1to32.txt", "-l", "compress", "-n", "0x100000", "-t", "8"], 20),
 ]
