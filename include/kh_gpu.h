@@ -200,6 +200,16 @@ int kh_field_ops(kh_ctx *ctx, const uint8_t *a, const uint8_t *b, uint32_t n, ui
 int kh_bloom_check(kh_ctx *ctx, uint32_t layer, const uint8_t *items, uint32_t n, uint32_t len, uint8_t *out);
 /* copy a bloom back: layer 0 = target bloom, 1..3 = BSGS layers (256 shards concatenated, unpadded) */
 int kh_get_bloom(kh_ctx *ctx, uint32_t layer, uint8_t *buf, uint64_t cap, uint64_t *bytes);
+/* Memory-mapped bloom files (--mapped, keyhunt.cpp:724-806, 7630-7706; bloom/bloom.cpp:491-747): the
+ * file is the raw bit array of a filter whose geometry the reference derives from the entry count or,
+ * when it reloads an existing file, from the file size (bits = bytes * 8).
+ * kh_bloom_add: bloom_add of n items of len bytes (20, a shorter hash160 prefix, or 32) into the flat
+ * bit array bf of that geometry (host only, no GPU).
+ * kh_bsgs_layer_bits: after kh_bsgs_build / _load, OR the baby-step X's of layer 1, 2 or 3 (the first
+ * M, M2 or M3 babies) into 256 contiguous shards of bytes each, with the given bits and hashes. */
+int kh_bloom_add(uint8_t *bf, uint64_t bits, uint32_t hashes, const uint8_t *items, uint64_t n, uint32_t len);
+int kh_bsgs_layer_bits(kh_ctx *ctx, uint32_t layer, uint64_t bits, uint32_t hashes, uint64_t bytes, uint8_t *shards);
+
 /* bsgsd semantics (bsgsd.cpp:2544-2561): the daemon's worker also tests every base point against the
  * target, so a key that is exactly a base (offset 0, which the giant/baby steps reach only through the
  * point at infinity) is found there; keyhunt's own worker (keyhunt.cpp:4625-4640) has no such test and

@@ -60,6 +60,9 @@ void *kh_gpu_thread_process(void *vargp) {
 	std::vector<kh_hit> hits(1 << 16);
 	uint32_t mode = FLAGMODE == MODE_XPOINT ? KH_MODE_XPOINT : (FLAGCRYPTO == CRYPTO_ETH ? KH_MODE_ETH : KH_MODE_ADDRESS);
 	if (FLAGENDOMORPHISM) mode |= KH_MODE_ENDO;
+	/* the reference numbers its search kinds the other way round (keyhunt.cpp:89-91) */
+	const uint32_t search = FLAGSEARCH == SEARCH_COMPRESS ? KH_SEARCH_COMPRESS
+	                      : FLAGSEARCH == SEARCH_UNCOMPRESS ? KH_SEARCH_UNCOMPRESS : KH_SEARCH_BOTH;
 	Int key_mpz;
 	for (;;) {
 		pthread_mutex_lock(&write_random);
@@ -72,7 +75,7 @@ void *kh_gpu_thread_process(void *vargp) {
 		if (!more) break;
 		key_mpz.Get32Bytes(start_be);
 		uint32_t nh = 0;
-		kh_gpu_check(gpu, kh_scan(gpu, start_be, stride_be, N_SEQUENTIAL_MAX, mode, (uint32_t)FLAGSEARCH, hits.data(),
+		kh_gpu_check(gpu, kh_scan(gpu, start_be, stride_be, N_SEQUENTIAL_MAX, mode, search, hits.data(),
 		                          (uint32_t)hits.size(), &nh), "kh_scan");
 		for (uint32_t i = 0; i < nh; i++) {  /* confirmed by searchbinary, parity-fixed, in print order */
 			Int k;

@@ -1107,14 +1107,18 @@ int kh_bsgs_set_layer1(kh_ctx *ctx, uint32_t layout) {
 namespace {
 // the baby-step walk (thread_bPload, keyhunt.cpp:5284-5472): babies (i+1)G, i < M, into layer 1
 // (bl1/bd1, reference or blocked layout by `mode`), layers 2/3 (the context's) and the bP rows
-int build_walk(kh_ctx *ctx, int mode, uint8_t *bl1, const bloom_desc &bd1, uint64_t *d_key, uint32_t *d_val) {
+// baby steps 1..count (count = M unless a single layer is rebuilt) into bl1 with bd1 and, for the
+// first M2 / M3 of them, into layers 2 / 3 and the bP rows (m2 = m3 = 0: layer bl1 alone)
+int build_walk(kh_ctx *ctx, int mode, uint8_t *bl1, const bloom_desc &bd1, uint64_t *d_key, uint32_t *d_val,
+               uint64_t count = 0, bool one_layer = false) {
   const int H = KH_WALK_H;
   ctx->cont_valid = false;
   const kh_bsgs_info &I = ctx->info;
+  if (!count) count = I.m;
   const uint32_t *tab = nullptr;
   int r = get_table(ctx, u256_u64(1), &tab);
   if (r) return r;
-  uint64_t total_groups = (I.m + 2 * H - 1) / (2 * H);
+  uint64_t total_groups = (count + 2 * H - 1) / (2 * H);
   job_geom jg = plan(ctx, total_groups, 0);
   std::vector<u256> s(jg.L);
   for (uint32_t g = 0; g < jg.L; g++) s[g] = u256_u64(1 + (uint64_t)g * jg.gpl * 2 * H + H);  // baby i <-> key i+1
@@ -1128,15 +1132,15 @@ int build_walk(kh_ctx *ctx, int mode, uint8_t *bl1, const bloom_desc &bd1, uint6
   A.scratch = ctx->d_scratch;
   A.L = jg.L;
   A.lane_stride = jg.gpl * 2 * H;
-  A.n_points = I.m;
+  A.n_points = count;
   A.bl1 = bl1;
   A.bl2 = ctx->d_bl[1];
   A.bl3 = ctx->d_bl[2];
   A.bd = bd1;
   A.bd2 = ctx->bd[1];
   A.bd3 = ctx->bd[2];
-  A.m2 = I.m2;
-  A.m3 = I.m3;
+  A.m2 = one_layer ? 0 : I.m2;
+  A.m3 = one_layer ? 0 : I.m3;
   A.rows_key = d_key;
   A.rows_val = d_val;
   return run_walk(ctx, mode, 3, A, jg.gpl, 4);
@@ -2097,6 +2101,42 @@ int kh_bsgs_scan_list(kh_ctx *ctx, const uint8_t *bases, uint64_t n_bases, kh_bs
 // ---------------------------------------------------------------------------------------------
 // measurement
 // ---------------------------------------------------------------------------------------------
+int kh_bloom_add(uint8_t *bf, uint64_t bits, uint32_t hashes, const uint8_t *items, uint64_t n, uint32_t len) {
+  if (!bf || !bits || (!items && n) || !len || len > 32 || (len > 20 && len != 32)) return KH_E_ARG;
+  bloom_desc d;
+  memset(&d, 0, sizeof d);
+  d.bits = bits;
+  d.hashes = hashes;
+  for (uint64_t i = 0; i < n; i++) host_bloom_add(bf, d, items + i * len, (int)len);
+  return KH_OK;
+}
+
+int kh_bsgs_layer_bits(kh_ctx *ctx, uint32_t layer, uint64_t bits, uint32_t hashes, uint64_t bytes, uint8_t *shards) {
+  if (!ctx || layer < 1 || layer > 3 || !bits || !bytes || !shards || bits > bytes * 8) return KH_E_ARG;
+  if (!ctx->bsgs_built) return KH_E_STATE;
+  (void)hipSetDevice(ctx->device);
+  const kh_bsgs_info &I = ctx->info;
+  const uint64_t count = layer == 1 ? I.m : layer == 2 ? I.m2 : I.m3;
+  bloom_desc d;
+  memset(&d, 0, sizeof d);
+  d.bits = bits;
+  d.bytes = bytes;
+  d.stride = (bytes + 255) / 256 * 256;
+  d.recip = ~0ULL / bits;
+  d.hashes = hashes;
+  std::vector<uint8_t> h(256 * d.stride, 0);
+  for (int i = 0; i < 256; i++) memcpy(&h[(size_t)i * d.stride], shards + (size_t)i * bytes, bytes);
+  uint8_t *dev = nullptr;
+  if (hipMalloc(&dev, h.size() + 4) != hipSuccess) return KH_E_NOMEM;
+  int r = hipMemcpy(dev, h.data(), h.size(), hipMemcpyHostToDevice) == hipSuccess ? KH_OK : KH_E_HIP;
+  if (r == KH_OK) r = build_walk(ctx, KM_BUILD, dev, d, nullptr, nullptr, count, true);
+  if (r == KH_OK && hipMemcpy(h.data(), dev, h.size(), hipMemcpyDeviceToHost) != hipSuccess) r = KH_E_HIP;
+  (void)hipFree(dev);
+  if (r == KH_OK)
+    for (int i = 0; i < 256; i++) memcpy(shards + (size_t)i * bytes, &h[(size_t)i * d.stride], bytes);
+  return r;
+}
+
 int kh_bsgs_set_base_check(kh_ctx *ctx, int enable) {
   if (!ctx) return KH_E_ARG;
   ctx->base_check = enable != 0;

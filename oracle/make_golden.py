@@ -14,6 +14,9 @@ TEST INFRASTRUCTURE.  Runs in the development container only (needs /root/refere
   tests/golden/ref_data/         the -S target caches (data_<hex>.dat) the reference CLI writes for
                                  address / rmd160 / xpoint / eth target files, with
                                  ref_data/index.json (name, size, masked sha256, hit set of the run).
+  tests/golden/ref_mapped.json   --mapped bloom files the reference CLI leaves after run sequences
+                                 (fresh, reload, chunks, size overrides, --create-mapped/--load-bloom,
+                                 BSGS shard files), with the hit sets of the runs.
   tests/golden/ref_bsgsd.json    a transcript of the reference daemon (oracle/_ref/bsgsd): every
                                  request of BSGSD_REQUESTS with the raw reply bytes and the lines the
                                  daemon printed for it, plus its KEYFOUNDKEYFOUND.txt.
@@ -359,6 +362,76 @@ def gen_bsgsd() -> None:
         json.dump(out, f, indent=1)
 
 
+# --mapped bloom files (keyhunt.cpp:724-806, 1131-1172, 1700-1785, 7630-7706; bloom/bloom.cpp:491-747):
+# sequences of reference-CLI runs sharing one directory per sequence; after each run every mapped file
+# is recorded (BSGS shard files per layer: their sizes and the sha256 of their concatenation).  The
+# chunk count divides the 35,944-byte filter: with a remainder the reference maps the filter's last
+# bytes to a chunk past the end (bloom.cpp:38-44) and crashes (-11).
+RMD_ARGS = ["-m", "rmd160", "-f", "1to32.rmd", "-l", "compress", "-r", "1:100000", "-n", "0x100000", "-t", "4"]
+BSGS_ARGS = ["-m", "bsgs", "-f", "63.pub", "-n", "0x1000000", "-k", "2", "-r", "7cce5efdac000000:7cce5efdad000000", "-t", "4"]
+MAPPED_SEQS = [
+    ("rmd160_fresh_then_reload", [RMD_ARGS + ["--mapped"], RMD_ARGS + ["--mapped"]]),
+    ("rmd160_named_chunks", [RMD_ARGS + ["--mapped=tg.dat", "--mapped-chunks", "4"],
+                             RMD_ARGS + ["--mapped=tg.dat", "--mapped-chunks", "4"]]),
+    ("rmd160_size_override", [RMD_ARGS + ["--mapped-size", "1m"], RMD_ARGS + ["--mapped-size", "1m"]]),
+    ("create_then_load", [["--create-mapped=100000", "--bloom-file", "cm.dat"],
+                          RMD_ARGS + ["--mapped", "--bloom-file", "cm.dat", "--load-bloom"]]),
+    ("xpoint_fresh", [["-m", "xpoint", "-f", "1to63_65.txt", "-r", "1:100000", "-n", "0x100000", "-t", "4", "--mapped"]]),
+    ("vanity_fresh", [["-m", "vanity", "-v", "1Kha", "-v", "1PUB", "-l", "compress", "-r", "1:100000", "-n", "0x100000",
+                       "-t", "4", "--mapped=v.dat"]]),
+    ("eth_fresh", [["-m", "address", "-c", "eth", "-f", "eth_targets.txt", "-r", "1:100000", "-n", "0x100000", "-t", "4",
+                    "--mapped"]]),
+    ("bsgs_fresh_then_reload", [BSGS_ARGS + ["--mapped"], BSGS_ARGS + ["--mapped"]]),
+    ("bsgs_size_override", [BSGS_ARGS + ["--mapped-size", "64k"]]),
+]
+
+
+def mapped_files(d: str) -> dict:
+    import hashlib
+    out, layers = {}, {}
+    for f in sorted(os.listdir(d)):
+        m = re.match(r"(bloom2?3?-)(\d+)\.dat$", f)
+        if m:
+            layers.setdefault(m.group(1), {})[int(m.group(2))] = f
+        elif f.endswith(".dat") or re.search(r"\.dat\.\d+$", f):
+            b = open(os.path.join(d, f), "rb").read()
+            out[f] = [len(b), hashlib.sha256(b).hexdigest()]
+    for pfx, shards in layers.items():
+        h = hashlib.sha256()
+        sizes = []
+        for i in range(256):
+            b = open(os.path.join(d, shards[i]), "rb").read()
+            sizes.append(len(b))
+            h.update(b)
+        out[pfx + "*"] = [sizes, h.hexdigest()]
+    return out
+
+
+def gen_mapped() -> None:
+    subprocess.run(["make", "-s", "-C", HERE, "-f", "Makefile.ref", "-j8"], check=True)
+    res = {"_generator": "oracle/make_golden.py --mapped running oracle/_ref/keyhunt"}
+    for name, runs in MAPPED_SEQS:
+        steps = []
+        with tempfile.TemporaryDirectory() as td:
+            for fn in os.listdir(DATA):
+                shutil.copy(os.path.join(DATA, fn), td)
+            for argv in runs:
+                if os.path.exists(os.path.join(td, "KEYFOUNDKEYFOUND.txt")):
+                    os.remove(os.path.join(td, "KEYFOUNDKEYFOUND.txt"))
+                p = subprocess.run(["timeout", "300", REF_BIN] + argv + ["-q"], cwd=td, capture_output=True, text=True)
+                text = ""
+                for fn in ("KEYFOUNDKEYFOUND.txt", "VANITYKEYFOUND.txt"):
+                    if os.path.exists(os.path.join(td, fn)):
+                        text += open(os.path.join(td, fn)).read()
+                        os.remove(os.path.join(td, fn))
+                hits = sorted(parse_keyfound(text), key=lambda h: int(h["key"], 16))
+                steps.append({"argv": argv, "exit": p.returncode, "hits": hits, "files": mapped_files(td)})
+                print(name, argv[-3:], p.returncode, len(hits), {k: v[0] if k.endswith("*") is False else "..." for k, v in steps[-1]["files"].items()}, flush=True)
+        res[name] = steps
+    with open(os.path.join(REPO, "tests", "golden", "ref_mapped.json"), "w") as f:
+        json.dump(res, f, indent=1)
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--vectors", action="store_true")
@@ -366,10 +439,11 @@ if __name__ == "__main__":
     ap.add_argument("--tables", action="store_true")
     ap.add_argument("--data", action="store_true")
     ap.add_argument("--bsgsd", action="store_true")
+    ap.add_argument("--mapped", action="store_true")
     ap.add_argument("--only", nargs="*")
     a = ap.parse_args()
-    if not a.vectors and not a.e2e and not a.tables and not a.data and not a.bsgsd:
-        a.vectors = a.e2e = a.tables = a.data = a.bsgsd = True
+    if not (a.vectors or a.e2e or a.tables or a.data or a.bsgsd or a.mapped):
+        a.vectors = a.e2e = a.tables = a.data = a.bsgsd = a.mapped = True
     if a.vectors:
         gen_vectors()
     if a.e2e:
@@ -380,3 +454,5 @@ if __name__ == "__main__":
         gen_data()
     if a.bsgsd:
         gen_bsgsd()
+    if a.mapped:
+        gen_mapped()

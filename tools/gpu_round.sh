@@ -10,9 +10,12 @@ R=$(pwd)
 O=$R/gpurun_out/$TAG
 mkdir -p $O
 has() { [[ ",$PARTS," == *",$1,"* ]]; }
+TESTS_RC=0
 if has tests; then
-  timeout -k 10 900 python -m pytest tests -q -m gpu > $O/tests.log 2>&1 || { echo "tests rc=$?"; tail -30 $O/tests.log; exit 1; }
-  tail -2 $O/tests.log
+  # a failing test does not stop the measurements; a crash or a time-out (rc > 1) does
+  timeout -k 10 900 python -u -m pytest tests -q -m gpu --timeout 600 --timeout-method thread > $O/tests.log 2>&1 || TESTS_RC=$?
+  tail -12 $O/tests.log
+  [ $TESTS_RC -gt 1 ] && { echo "tests rc=$TESTS_RC"; exit 1; }
 fi
 if has bench; then
   timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err || { echo "bench rc=$?"; tail -20 $O/bench.err; exit 1; }
@@ -43,3 +46,4 @@ if has config5; then
   timeout -k 10 600 python $R/bench.py --config 5 > $O/bench_c5.json 2> $O/bench_c5.err || { echo "bench c5 rc=$?"; tail -20 $O/bench_c5.err; exit 1; }
   cat $O/bench_c5.json
 fi
+exit $TESTS_RC
