@@ -24,8 +24,9 @@ achieved = VALU wave-instructions per launch (rocprofv3 SQ_INSTS_VALU per point,
 profiles/, x this run's points per launch) / mean launch time; peak = 1024 SIMDs x 2.4 GHz / 4
 cycles: one wave64 VALU instruction per SIMD per quad-cycle, the unit the SQ counters use and the
 measured issue cost of the 32-bit multiply-accumulate and carry ops the field math is made of
-(4.1-5.5 cycles at 4 waves/SIMD; only add/xor/mov issue in 2).  frac_at_measured_clock divides by
-the same peak at the clock the counters saw (GRBM_GUI_ACTIVE / 8 / kernel time: DVFS).  The HBM
+(4.1-5.5 cycles at 4 waves/SIMD; only add/xor/mov issue in 2).  pmc_valu_issue_frac is the
+profiled dispatch's own occupancy of those issue slots, SQ_INSTS_VALU x 4 / (1024 x GRBM_GUI_ACTIVE
+/ 8), clock-free (the chip's clock under this load sits below 2.4 GHz: pmc_clock_ghz).  The HBM
 side is reported too ("hbm"): algorithmic bytes (BSGS: 64 B per giant point, one random line of the
 blocked layer 1; the reference layout's is 128 B) / launch time against 8 TB/s, and
 traffic = HBM bytes per launch from the PMC counters with the guide's gfx950 corrections
@@ -225,9 +226,10 @@ def walk_roofline(kname: str, pts_launch: float, ms_launch: float, algo_bytes_pe
         a = wipp * pts_launch / secs / 1e9
         roof.update(achieved=a, frac=a / VALU_PEAK_GIPS, valu_wave_instructions_per_point=wipp,
                     valu_lane_instructions_per_point=wipp * 64)
-        if d.get("effective_clock_ghz"):
-            clk = d["effective_clock_ghz"]
-            roof.update(effective_clock_ghz=clk, frac_at_measured_clock=a / (SIMDS * clk / VALU_ISSUE_CYCLES))
+        if d.get("valu_issue_frac"):
+            # the profiled dispatch's issue-slot occupancy, in cycles (clock-free; DVFS moves the
+            # clock between runs, so frac above is at the nominal 2.4 GHz)
+            roof.update(pmc_valu_issue_frac=d["valu_issue_frac"], pmc_clock_ghz=d["effective_clock_ghz"])
     hbm = {"achieved": pts_launch * algo_bytes_per_point / secs / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "algorithmic_bytes_per_point": algo_bytes_per_point}
     hbm["frac"] = hbm["achieved"] / HBM_PEAK_GBS

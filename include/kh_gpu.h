@@ -200,6 +200,10 @@ int kh_field_ops(kh_ctx *ctx, const uint8_t *a, const uint8_t *b, uint32_t n, ui
 int kh_bloom_check(kh_ctx *ctx, uint32_t layer, const uint8_t *items, uint32_t n, uint32_t len, uint8_t *out);
 /* copy a bloom back: layer 0 = target bloom, 1..3 = BSGS layers (256 shards concatenated, unpadded) */
 int kh_get_bloom(kh_ctx *ctx, uint32_t layer, uint8_t *buf, uint64_t cap, uint64_t *bytes);
+/* The context's own sorted bP rows (16 B each, the reference's bsgs_xvalue layout), valid until the
+ * next kh_bsgs_build / _load / _set_table / kh_close: --ptable writes them to its file without a copy. */
+int kh_bsgs_table_rows(kh_ctx *ctx, const uint8_t **rows, uint64_t *n_rows);
+
 /* Memory-mapped bloom files (--mapped, keyhunt.cpp:724-806, 7630-7706; bloom/bloom.cpp:491-747): the
  * file is the raw bit array of a filter whose geometry the reference derives from the entry count or,
  * when it reloads an existing file, from the file size (bits = bytes * 8).

@@ -2137,6 +2137,14 @@ int kh_bsgs_layer_bits(kh_ctx *ctx, uint32_t layer, uint64_t bits, uint32_t hash
   return r;
 }
 
+int kh_bsgs_table_rows(kh_ctx *ctx, const uint8_t **rows, uint64_t *n_rows) {
+  if (!ctx || !rows || !n_rows) return KH_E_ARG;
+  if (!ctx->bsgs_built) return KH_E_STATE;
+  *rows = ctx->h_rows.data();
+  *n_rows = ctx->h_rows.size() / 16;
+  return KH_OK;
+}
+
 int kh_bsgs_set_base_check(kh_ctx *ctx, int enable) {
   if (!ctx) return KH_E_ARG;
   ctx->base_check = enable != 0;

@@ -19,6 +19,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
 #include <time.h>
 #include <unistd.h>
@@ -883,7 +884,7 @@ bool take_bases(const U &twoN, uint64_t want, std::vector<U> &out) {
 // With --load-ptable an existing FILE.md5 is trusted (1958-1981); otherwise the MD5 is computed
 // from the file and written.  A cache file of another MD5 or size is rebuilt (2655-2700).  Only
 // the files are produced: the engine's third check does not need the buckets.
-void ptable_cache(const std::vector<uint8_t> &rows, uint64_t m3, bool loaded) {
+void ptable_cache(const uint8_t *rows, uint64_t m3, bool loaded) {
   if (!opt.ptable_cache) return;
   const std::string md5_path = std::string(opt.ptable) + ".md5", cache_path = std::string(opt.ptable) + ".cache";
   uint8_t md5[16];
@@ -911,7 +912,7 @@ void ptable_cache(const std::vector<uint8_t> &rows, uint64_t m3, bool loaded) {
     printf("[W] bP table cache mismatch (%s); rebuilding\n", cache_path.c_str());
   else
     printf("[I] bP table cache not found (%s); creating\n", cache_path.c_str());
-  if (bptable_cache_write(cache_path.c_str(), md5, rows.data(), m3))
+  if (bptable_cache_write(cache_path.c_str(), md5, rows, m3))
     printf("[+] bP table cache refreshed (%s)\n", cache_path.c_str());
   else
     printf("[W] Unable to write bP table cache to %s\n", cache_path.c_str());
@@ -924,41 +925,47 @@ void ptable_cache(const std::vector<uint8_t> &rows, uint64_t m3, bool loaded) {
 int bsgs_ptable(kh_ctx *ctx, const kh_bsgs_info &info, bool first) {
   if (!opt.ptable) return KH_OK;
   const uint64_t bytes = info.m3 * 16;
-  std::vector<uint8_t> rows(bytes);
   if (opt.load_ptable) {
-    FILE *f = fopen(opt.ptable, "rb");
-    if (!f) {
+    // the file is mapped read-only, as the reference maps it (keyhunt.cpp:1880-1900), and its first
+    // M3 rows go straight from the mapping into the context's table
+    int fd = open(opt.ptable, O_RDONLY);
+    if (fd < 0) {
       fprintf(stderr, "[E] Cannot open bP table file\n");
       return KH_E_IO;
     }
     struct stat st;
-    if (fstat(fileno(f), &st) != 0) {
-      fclose(f);
+    if (fstat(fd, &st) != 0) {
+      close(fd);
       fprintf(stderr, "[E] Cannot stat bP table file\n");
       return KH_E_IO;
     }
     if ((uint64_t)st.st_size < bytes) {
-      fclose(f);
+      close(fd);
       fprintf(stderr, "[E] Existing bP table file too small\n");
       return KH_E_IO;
     }
-    bool ok = bytes == 0 || fread(rows.data(), bytes, 1, f) == 1;
-    fclose(f);
-    if (!ok) {
-      fprintf(stderr, "[E] Cannot read bP table file\n");
-      return KH_E_IO;
+    const uint8_t *map = nullptr;
+    if (bytes) {
+      void *m = mmap(nullptr, bytes, PROT_READ, MAP_SHARED, fd, 0);
+      if (m == MAP_FAILED) {
+        close(fd);
+        fprintf(stderr, "[E] mmap failed for bP table\n");
+        return KH_E_IO;
+      }
+      map = (const uint8_t *)m;
     }
-    int r = kh_bsgs_set_table(ctx, rows.data(), info.m3);
-    if (r) {
-      fprintf(stderr, "[E] %s\n", kh_last_error(ctx));
-      return r;
-    }
-    if (first) ptable_cache(rows, info.m3, true);
-    return KH_OK;
+    close(fd);
+    int r = kh_bsgs_set_table(ctx, map, info.m3);
+    if (!r && first) ptable_cache(map, info.m3, true);
+    if (map) munmap((void *)map, bytes);
+    if (r) fprintf(stderr, "[E] %s\n", kh_last_error(ctx));
+    return r;
   }
   if (!first) return KH_OK;
-  uint64_t got = 0;
-  int r = kh_get_bsgs_table(ctx, rows.data(), info.m3, &got);
+  // the context's own sorted rows, written without another host copy
+  const uint8_t *rows = nullptr;
+  uint64_t nrows = 0;
+  int r = kh_bsgs_table_rows(ctx, &rows, &nrows);
   if (r) return r;
   const uint64_t map_bytes = std::max(bytes, opt.ptable_size);
   int fd = open(opt.ptable, O_RDWR | O_CREAT, 0600);
@@ -980,7 +987,7 @@ int bsgs_ptable(kh_ctx *ctx, const kh_bsgs_info &info, bool first) {
     ok = pwrite(fd, zero.data(), map_bytes, 0) == (ssize_t)map_bytes;
   }
   for (uint64_t o = 0; ok && o < bytes;) {
-    ssize_t w = pwrite(fd, rows.data() + o, bytes - o, (off_t)o);
+    ssize_t w = pwrite(fd, rows + o, bytes - o, (off_t)o);
     ok = w > 0;
     if (ok) o += (uint64_t)w;
   }
@@ -1003,6 +1010,19 @@ int bsgs_tables(kh_ctx *ctx, const kh_bsgs_info &info, bool first) {
   }
   if (!opt.save_read) return kh_bsgs_build(ctx);
   char f4[96], f6[96], f7[96], f2[96];
+  if (opt.load_ptable) {
+    // -S with --load-ptable (keyhunt.cpp:2153-2186): the reference reads the .tbl into its
+    // read-only mapping of the --ptable file, which fails, or reports the .tbl missing; it never
+    // writes the .tbl (2588)
+    snprintf(f2, sizeof f2, "keyhunt_bsgs_2_%llu.tbl", (unsigned long long)info.m3);
+    if (access(f2, F_OK) == 0) {
+      fprintf(stderr, "[E] Error reading the file %s\n", f2);
+    } else {
+      fprintf(stderr, "[E] Missing bP table file %s\n", f2);
+      fprintf(stderr, "    Remove --loadptable or generate the table first.\n");
+    }
+    return KH_E_IO;
+  }
   snprintf(f4, sizeof f4, "keyhunt_bsgs_4_%llu.blm", (unsigned long long)info.m);
   snprintf(f6, sizeof f6, "keyhunt_bsgs_6_%llu.blm", (unsigned long long)info.m2);
   snprintf(f7, sizeof f7, "keyhunt_bsgs_7_%llu.blm", (unsigned long long)info.m3);

@@ -91,6 +91,13 @@ def test_load_ptable_errors(work):
     (work / "short.tbl").write_bytes(bytes(100))
     p, _ = _run(work, ["--ptable", "short.tbl", "--load-ptable"])
     assert p.returncode == 1 and "[E] Existing bP table file too small" in p.stderr
+    # -S with --load-ptable and no .tbl (keyhunt.cpp:2180-2186; the reference CLI prints exactly this)
+    p, _ = _run(work, ["--ptable", "bp.tbl"])
+    p, _ = _run(work, ["-S", "--ptable", "bp.tbl", "--load-ptable"])
+    assert p.returncode == 1
+    assert ("[E] Missing bP table file keyhunt_bsgs_2_8.tbl\n    Remove --loadptable or generate the table first.\n"
+            in p.stderr)
+    assert not (work / "keyhunt_bsgs_2_8.tbl").exists()
 
 
 @pytest.mark.skipif(not os.path.exists(REF_BIN), reason="oracle/_ref/keyhunt not built")

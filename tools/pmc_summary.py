@@ -11,7 +11,10 @@ written once and read back once per group, so its read bytes equal the dispatch'
   other_read    = TCC_EA0_RDREQ x 64 B - pad_read / 2    (the probes' random 16-B loads: 64 B each)
   hbm_bytes     = other_read + pad_read + pad_write.
 VALU: SQ_INSTS_VALU counts wave-instructions; lane-instructions per point = x 64 / points (each
-lane walks its own points).  Clock: GRBM_GUI_ACTIVE / 8 (summed over the 8 XCDs) / kernel time."""
+lane walks its own points); issue fraction = SQ_INSTS_VALU x 4 cycles / (1024 SIMDs x
+GRBM_GUI_ACTIVE / 8).  Clock: GRBM_GUI_ACTIVE / 8 (summed over the 8 XCDs) / the same
+dispatch's End-Start timestamps in the GRBM pass (a kernel-trace duration from another run can
+differ: the PMC program's first dispatch is cold)."""
 import csv
 import glob
 import json
@@ -27,6 +30,8 @@ for f in glob.glob(f"{src}/*/run_counter_collection.csv") + glob.glob(f"{src}/*/
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"].split("(")[0].replace("void ", "").strip()
         agg[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        if r["Counter_Name"] == "GRBM_GUI_ACTIVE":
+            agg[k]["_grbm_dispatch_ns"].append(float(r["End_Timestamp"]) - float(r["Start_Timestamp"]))
 res = {}
 for k, d in agg.items():
     if k not in points:
@@ -46,9 +51,15 @@ for k, d in agg.items():
     if "SQ_INSTS_VALU" in per:
         e["valu_wave_instructions_per_dispatch"] = per["SQ_INSTS_VALU"]
         e["valu_lane_instructions_per_point"] = per["SQ_INSTS_VALU"] * 64 / p
-    if "GRBM_GUI_ACTIVE" in per and k in durations:
-        e["kernel_ns"] = durations[k]
-        e["effective_clock_ghz"] = per["GRBM_GUI_ACTIVE"] / 8 / durations[k]
+    if k in durations:
+        e["kernel_trace_ns"] = durations[k]
+    if "GRBM_GUI_ACTIVE" in per:
+        e["grbm_dispatch_ns"] = per.pop("_grbm_dispatch_ns")
+        e["effective_clock_ghz"] = per["GRBM_GUI_ACTIVE"] / 8 / e["grbm_dispatch_ns"]
+        if "SQ_INSTS_VALU" in per:
+            # share of the dispatch's VALU issue slots used: one wave64 instruction per SIMD per 4
+            # cycles, 1024 SIMDs, GRBM_GUI_ACTIVE / 8 cycles (clock-free: both sides in cycles)
+            e["valu_issue_frac"] = per["SQ_INSTS_VALU"] * 4 / (1024 * per["GRBM_GUI_ACTIVE"] / 8)
     res[k] = e
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps(res, indent=1))
