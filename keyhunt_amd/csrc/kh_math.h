@@ -173,7 +173,7 @@ KH_HD void fe_neg(fe &r, const fe &a) {
 }
 
 // 512-bit t (16 limbs) -> canonical r.  t = lo + hi*2^256 == lo + hi*(2^32 + 977) (mod p).
-KH_HD void fe_reduce512(fe &r, const uint32_t t[16]) {
+KH_HD void fe_reduce512_gen(fe &r, const uint32_t t[16]) {
   uint32_t u[10];
   uint64_t c = 0;
 #pragma unroll
@@ -239,6 +239,89 @@ __device__ __forceinline__ uint64_t mad_nc(uint32_t a, uint32_t b, uint64_t acc)
 #ifndef KH_SAFE_ADDC
 #define KH_SAFE_ADDC 1
 #endif
+#ifndef KH_RED2
+#define KH_RED2 1
+#endif
+
+#if defined(__HIP_DEVICE_COMPILE__)
+// a*b + c with b wave-uniform (an SGPR); m = the lane mask of the sum's 65th bit
+__device__ __forceinline__ uint64_t mad_co(uint32_t a, uint32_t b, uint64_t c, uint64_t &m) {
+  uint64_t d;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(d), "=s"(m) : "v"(a), "s"(b), "v"(c));
+  return d;
+}
+__device__ __forceinline__ uint64_t pack64(uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; }
+#endif
+
+// The fold with 64-bit multiply-adds only (device): with h = t[8..15], l = t[0..7],
+//   t == sum_{j even} V_j 2^(32j) + sum_{i odd} W_i 2^(32i)  (mod p),
+//   V_j = h_j*977 + l_j + l_{j+1} 2^32,   W_i = h_i*977 + h_{i-1} + h_i 2^32,
+// since h_j (2^32 + 977) 2^(32j) is h_j*977 at limb j (in V_j) plus h_j at limb j+1 (in W_{j+1}
+// for even j, in W_j's own 2^32 term for odd j).  The V_j are disjoint 64-bit slices (A) and so are
+// the W_i one limb up (B): R = A + B 2^32 is one 8-limb carry chain, and its limb 8 folds again.
+// Each V_j / W_i exceeds 64 bits with probability ~2^-22; the mad's carry-out lane mask keeps the
+// lost bit.  A wave with such a lane, or whose second fold overflows, ripples past limb 2 or lands
+// in [p, 2^256), puts the lost bits back into R and redoes the second fold the long way -- from R
+// and the masks only, so t is dead after the mads.  Replaces the 64-bit adds and zero-extension
+// moves of the long form (fe_reduce512_gen) by multiply-adds.
+KH_HD void fe_reduce512(fe &r, const uint32_t t[16]) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (KH_RED2) {
+    const uint32_t K = 977u;
+    uint64_t m0, m1, m2, m3, m4, m5, m6, m7, m8;
+    const uint64_t V0 = mad_co(t[8], K, pack64(t[0], t[1]), m0);
+    const uint64_t W1 = mad_co(t[9], K, pack64(t[8], t[9]), m1);
+    const uint64_t V2 = mad_co(t[10], K, pack64(t[2], t[3]), m2);
+    const uint64_t W3 = mad_co(t[11], K, pack64(t[10], t[11]), m3);
+    const uint64_t V4 = mad_co(t[12], K, pack64(t[4], t[5]), m4);
+    const uint64_t W5 = mad_co(t[13], K, pack64(t[12], t[13]), m5);
+    const uint64_t V6 = mad_co(t[14], K, pack64(t[6], t[7]), m6);
+    const uint64_t W7 = mad_co(t[15], K, pack64(t[14], t[15]), m7);
+    uint32_t R[10], c;
+    R[0] = (uint32_t)V0;
+    R[1] = addc((uint32_t)(V0 >> 32), (uint32_t)W1, 0, c);
+    R[2] = addc((uint32_t)V2, (uint32_t)(W1 >> 32), c, c);
+    R[3] = addc((uint32_t)(V2 >> 32), (uint32_t)W3, c, c);
+    R[4] = addc((uint32_t)V4, (uint32_t)(W3 >> 32), c, c);
+    R[5] = addc((uint32_t)(V4 >> 32), (uint32_t)W5, c, c);
+    R[6] = addc((uint32_t)V6, (uint32_t)(W5 >> 32), c, c);
+    R[7] = addc((uint32_t)(V6 >> 32), (uint32_t)W7, c, c);
+    uint32_t c1, c2;
+    R[8] = addc((uint32_t)(W7 >> 32), 0, c, R[9]);
+    // second fold: R8 (2^32 + 977) at limb 0
+    const uint64_t X = mad_co(R[8], K, pack64(R[0], R[1]), m8);
+    r.d[0] = (uint32_t)X;
+    r.d[1] = addc((uint32_t)(X >> 32), R[8], 0, c1);
+    r.d[2] = addc(R[2], 0, c1, c2);
+#pragma unroll
+    for (int i = 3; i < 8; i++) r.d[i] = R[i];
+    if ((m0 | m1 | m2 | m3 | m4 | m5 | m6 | m7 | m8) != 0 || kh_any((R[9] | c2) != 0 || r.d[7] == 0xFFFFFFFFu)) {
+      // rare: put back the 2^64 each overflowing V_j / W_i lost (limb j+2 / i+2; lane bits of
+      // the masks), then the second fold the long way from R: h = R8 + R9 2^32 < 2^34
+      const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+      const uint64_t ms[8] = {m0, m1, m2, m3, m4, m5, m6, m7};
+      uint32_t cc = 0;
+#pragma unroll
+      for (int q = 2; q < 9; q++) R[q] = addc(R[q], (uint32_t)(ms[q - 2] >> lane) & 1u, cc, cc);
+      R[9] += cc + ((uint32_t)(m7 >> lane) & 1u);
+      const uint64_t h = (uint64_t)R[8] + ((uint64_t)R[9] << 32);
+      uint64_t v = h * 977u + R[0];
+      r.d[0] = (uint32_t)v;
+      v = (v >> 32) + R[1] + (h & 0xFFFFFFFFu);
+      r.d[1] = (uint32_t)v;
+      v = (v >> 32) + R[2] + (h >> 32);
+      r.d[2] = (uint32_t)v;
+      cc = (uint32_t)(v >> 32);
+#pragma unroll
+      for (int i = 3; i < 8; i++) r.d[i] = addc(R[i], 0, cc, cc);
+      if (cc) fe_sub_p(r);  // wrapped past 2^256 once: + 0x1000003D1 cannot wrap again
+      fe_canon(r);
+    }
+    return;
+  }
+#endif
+  fe_reduce512_gen(r, t);
+}
 
 KH_HD void fe_mul(fe &r, const fe &a, const fe &b) {
   uint32_t t[16];

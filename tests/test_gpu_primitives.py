@@ -46,6 +46,24 @@ def test_field_ops_random(engine):
         assert sub == (x - y) % P
 
 
+def test_field_mul_reduction_rare_block(engine):
+    """Products that overflow each V_j / W_i slice of the device reduction (tests/_reduce_model.py),
+    spread over waves whose other lanes take the fast path, and whole waves of them."""
+    from _reduce_model import overflow_pairs
+    rng = random.Random(99)
+    pairs = overflow_pairs()
+    a, b = [], []
+    for k, (x, y) in enumerate(pairs):     # one rare lane per 64-lane wave, then all-rare waves
+        a += [rng.randrange(P) for _ in range(63)] + [x]
+        b += [rng.randrange(P) for _ in range(63)] + [y]
+    a += [x for x, _ in pairs]
+    b += [y for _, y in pairs]
+    got = engine.field_ops(a, b)
+    for x, y, (mul, sqr, _inv, _add, _sub) in zip(a, b, got):
+        assert mul == x * y % P
+        assert sqr == x * x % P
+
+
 def test_pubkeys_vs_reference(engine):
     ks = [h(v["k"]) for v in VEC["pubkeys"]]
     got = engine.pubkeys(ks)
