@@ -50,6 +50,7 @@ static_assert(KH_WALK_H >= 64 && KH_WALK_H <= 512 && (512 % KH_WALK_H) == 0,
 //                operand and a carry-in reads two scalars, over gfx9's constant-bus limit of one, so
 //                the compiler copies the SGPR in every such instruction)
 //   KH_REC32     the probe's block index in 32-bit arithmetic (mul_hi + mad_u24)
+//   KH_SPARSE_ALL the half-size inversion pad (even prefix products only) in every mode, not only BSGS
 #ifndef KH_TAB_LDS
 #define KH_TAB_LDS 0
 #endif
@@ -58,6 +59,9 @@ static_assert(KH_WALK_H >= 64 && KH_WALK_H <= 512 && (512 % KH_WALK_H) == 0,
 #endif
 #ifndef KH_REC32
 #define KH_REC32 0
+#endif
+#ifndef KH_SPARSE_ALL
+#define KH_SPARSE_ALL 0
 #endif
 
 enum kh_walk_mode {
