@@ -103,3 +103,37 @@ def overflow_pairs(seed=7, per=24):
             if a < P:
                 pairs.append((a, b))
     return pairs
+
+
+def _sqrt_mod_2k(t, k=256):
+    """a with a*a == t (mod 2^k), t odd and t == 1 (mod 8): Hensel lifting bit by bit"""
+    a = 1
+    for b in range(3, k):
+        if (a * a - t) % (1 << (b + 1)):
+            a += 1 << (b - 1)
+    return a % (1 << k)
+
+
+def square_overflow_inputs(seed=8, per=6):
+    """a < p whose square overflows V_j (low limbs j, j+1 all ones: a square root mod 2^256, j >= 1)
+    or W_i (high limb i of a^2 all ones: a = isqrt(T))"""
+    import math
+    rng = random.Random(seed)
+    out = []
+    for j in range(1, 8):
+        for _ in range(per):
+            lo = rng.getrandbits(256) | M32 << (32 * j) | (M32 << (32 * (j + 1)) if j < 7 else 0)
+            lo = (lo & ~7) | 1   # a square mod 8
+            lo &= 2**256 - 1
+            a = _sqrt_mod_2k(lo)
+            for c in (a, 2**256 - a):
+                if c < P and (c * c) % 2**256 == lo:
+                    out.append(c)
+    for i in range(8):
+        for _ in range(per):
+            th = rng.getrandbits(224) | M32 << (32 * i)
+            th = min(th | M32 << 224 if i == 7 else th, P - 2**40)
+            a = math.isqrt((th << 256) | (2**256 - 1))
+            if a < P:
+                out.append(a)
+    return out

@@ -58,6 +58,14 @@ def test_field_mul_reduction_rare_block(engine):
         b += [rng.randrange(P) for _ in range(63)] + [y]
     a += [x for x, _ in pairs]
     b += [y for _, y in pairs]
+    # squarings that overflow the slices (fe_sqr shares the reduction)
+    from _reduce_model import square_overflow_inputs
+    sq = square_overflow_inputs()
+    for x in sq:
+        a += [rng.randrange(P) for _ in range(63)] + [x]
+        b += [rng.randrange(P) for _ in range(64)]
+    a += sq
+    b += sq
     got = engine.field_ops(a, b)
     for x, y, (mul, sqr, _inv, _add, _sub) in zip(a, b, got):
         assert mul == x * y % P

@@ -39,3 +39,13 @@ def test_overflow_pairs_cover_every_slice():
     c = Counter(h for a, b in overflow_pairs() for h in fast(a * b)[1])
     for k in ("V0", "V2", "V4", "V6", "W1", "W3", "W5", "W7"):
         assert c[k] >= 8, (k, c)
+
+
+def test_square_inputs_cover_slices():
+    from _reduce_model import square_overflow_inputs
+    xs = square_overflow_inputs()
+    c = Counter(h for a in xs for h in fast(a * a)[1])
+    for k in ("V2", "V4", "V6", "W1", "W3", "W5", "W7"):
+        assert c[k] >= 2, (k, c)
+    for a in xs:
+        assert reduce(a * a) == a * a % P
