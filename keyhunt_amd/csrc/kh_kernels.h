@@ -51,6 +51,7 @@ static_assert(KH_WALK_H >= 64 && KH_WALK_H <= 512 && (512 % KH_WALK_H) == 0,
 //                the compiler copies the SGPR in every such instruction)
 //   KH_REC32     the probe's block index in 32-bit arithmetic (mul_hi + mad_u24)
 //   KH_SPARSE_ALL the half-size inversion pad (even prefix products only) in every mode, not only BSGS
+//   KH_SPARSE_BSGS the half-size pad in the BSGS walks (default on)
 #ifndef KH_TAB_LDS
 #define KH_TAB_LDS 0
 #endif
@@ -59,6 +60,9 @@ static_assert(KH_WALK_H >= 64 && KH_WALK_H <= 512 && (512 % KH_WALK_H) == 0,
 #endif
 #ifndef KH_REC32
 #define KH_REC32 0
+#endif
+#ifndef KH_SPARSE_BSGS
+#define KH_SPARSE_BSGS 1
 #endif
 #ifndef KH_SPARSE_ALL
 #define KH_SPARSE_ALL 0

@@ -516,7 +516,7 @@ __global__ void __launch_bounds__((walk_threads<MODE, H>()), (walk_blocks_per_cu
 
   // BSGS walks keep only the even prefix products in the pad and rebuild each odd one with one
   // multiplication in the backward pass: half the pad traffic for +1/2 multiplication per pair
-  constexpr bool SPARSE = KH_SPARSE_ALL || MODE == KM_BSGSB || MODE == KM_BSGS;
+  constexpr bool SPARSE = KH_SPARSE_ALL || (KH_SPARSE_BSGS && (MODE == KM_BSGSB || MODE == KM_BSGS));
   auto slot = [&](int m) { return (size_t)(SPARSE ? (m >> 1) : m) * L + g; };
   for (uint32_t j = 0; j < A.groups; j++) {
     const uint64_t cidx = A.interleave ? ((A.group_base + j) * (uint64_t)A.L + g) * (2 * H) + H
