@@ -128,7 +128,12 @@ __device__ __forceinline__ void blk_masks(uint32_t s0, uint32_t s1, uint32_t s2,
 }
 __device__ __forceinline__ bool blk_match(const uint4 &v, uint32_t s0, uint32_t s1, uint32_t s2) {
   uint32_t m[4];
+#ifdef KH_TIMING_CHEAP_MASKS
+  // timing-only build: the probe without mask arithmetic (hits are wrong); prices the masks
+  m[0] = s0 | 0x80000001u; m[1] = s1 | 0x80000001u; m[2] = s2 | 0x80000001u; m[3] = (s0 ^ s1) | 0x80000001u;
+#else
   blk_masks(s0, s1, s2, m);
+#endif
   return ((v.x & m[0]) == m[0]) & ((v.y & m[1]) == m[1]) & ((v.z & m[2]) == m[2]) & ((v.w & m[3]) == m[3]);
 }
 __device__ __forceinline__ void blk_insert(uint8_t *__restrict__ bf_shard, const bloom_desc &bd, const fe &x) {
