@@ -71,7 +71,7 @@ def main():
     two_n = 2 * info.n
     base0 = 1 << 124
     # known answer: a key inside the 8th base's window
-    key = base0 + 7 * two_n + 0x123456789ABCD
+    key = base0 + 7 * two_n + two_n // 3 + 12345
     e.bsgs_set_targets([ec_mul(key)])
     found = e.bsgs_scan(base0, 16)
     assert [f[1] for f in found] == [key], (found, hex(key))
