@@ -1046,8 +1046,10 @@ int kh_bsgs_setup(kh_ctx *ctx, uint64_t n, uint64_t k, kh_bsgs_info *info) {
     if (l == 0 && ctx->l1_layout == KH_LAYER1_BLOCKED) {
       // 3x the reference's bits per shard in whole 128-bit blocks (kh_kernels.h); desc.bits = blocks
       uint64_t blocks = (ctx->bd[0].bits * KH_BLK_BITS_MUL + 127) / 128;
-      if (blocks >> 32) {  // block index is a 32-bit multiply-high
-        ctx->err = "blocked layer 1 needs < 2^32 blocks per shard; use KH_LAYER1_REFERENCE";
+      // the probe record carries the block index within a shard and the shard byte, and addresses a
+      // shard by a 32-bit stride (k_walk blk_record / blk_load): shards must stay below 4 GB
+      if (((blocks * 16 + 255) & ~255ULL) >> 32) {
+        ctx->err = "blocked layer 1 needs shards below 4 GB (M < ~2^36); use KH_LAYER1_REFERENCE";
         return KH_E_ARG;
       }
       ctx->bd[0].bits = blocks;
@@ -1055,6 +1057,10 @@ int kh_bsgs_setup(kh_ctx *ctx, uint64_t n, uint64_t k, kh_bsgs_info *info) {
       ctx->bd[0].bytes = blocks * 16;
     }
     ctx->bd[l].stride = (ctx->bd[l].bytes + 255) & ~255ULL;
+    if (ctx->bd[l].bits >> 32) {  // the probes' bit index reduction (mod_bits) assumes bits < 2^32
+      ctx->err = "a bloom shard of 2^32 bits or more is outside the probes' index range";
+      return KH_E_ARG;
+    }
     I.bloom_bits[l] = (l == 0 && ctx->l1_layout == KH_LAYER1_BLOCKED) ? ctx->bd[0].bits * 128 : ctx->bd[l].bits;
     I.bloom_bytes[l] = ctx->bd[l].bytes;
     I.bloom_hashes[l] = (l == 0 && ctx->l1_layout == KH_LAYER1_BLOCKED) ? 16u : ctx->bd[l].hashes;
@@ -1901,10 +1907,7 @@ static int bsgs_scan_impl(kh_ctx *ctx, const u256 &st, const std::vector<u256> *
       Aw.n_points = cont ? total_groups * 2 * H : rg * 2 * H;
       Aw.bloom = ctx->d_bl[0];
       Aw.bd = ctx->bd[0];
-      // blocked layer 1: shard stride in 16-B blocks when the whole layer's block index fits 32 bits
-      Aw.bstride16 = ctx->bd[0].stride % 16 == 0 && ctx->bd[0].stride / 16 < (1u << 24)
-                         ? (uint32_t)(ctx->bd[0].stride / 16)
-                         : 0xFFFFFFFFu;
+      Aw.bstride32 = (uint32_t)ctx->bd[0].stride;  // < 2^32: checked by kh_bsgs_setup
       Aw.hit_count = ctx->d_cnt2[slot];
       Aw.hits = ctx->d_hits2[slot];
       Aw.hit_cap = ctx->cand_cap;

@@ -49,7 +49,6 @@ static_assert(KH_WALK_H >= 64 && KH_WALK_H <= 512 && (512 % KH_WALK_H) == 0,
 //   KH_TAB_VCOPY the table values a step uses twice copied to VGPRs once (a carry chain with an SGPR
 //                operand and a carry-in reads two scalars, over gfx9's constant-bus limit of one, so
 //                the compiler copies the SGPR in every such instruction)
-//   KH_REC32     the probe's block index in 32-bit arithmetic (mul_hi + mad_u24)
 //   KH_SPARSE_ALL the half-size inversion pad (even prefix products only) in every mode, not only BSGS
 //   KH_SPARSE_BSGS the half-size pad in the BSGS walks (default on)
 #ifndef KH_TAB_LDS
@@ -57,9 +56,6 @@ static_assert(KH_WALK_H >= 64 && KH_WALK_H <= 512 && (512 % KH_WALK_H) == 0,
 #endif
 #ifndef KH_TAB_VCOPY
 #define KH_TAB_VCOPY 0
-#endif
-#ifndef KH_REC32
-#define KH_REC32 0
 #endif
 #ifndef KH_SPARSE_BSGS
 #define KH_SPARSE_BSGS 1
@@ -116,7 +112,7 @@ struct walk_args {
   // kh_kernels.hip tblk_probe); null for vanity prefixes
   const uint4 *tblk;
   uint32_t tblocks;
-  uint32_t bstride16;  // BSGS blocked layer 1: shard stride in 16-byte blocks (KH_REC32 when < 2^24)
+  uint32_t bstride32;  // BSGS blocked layer 1: shard stride in bytes (< 2^32, kh_bsgs_setup checks)
   // BSGS build
   uint8_t *bl1, *bl2, *bl3;
   kh::bloom_desc bd2, bd3;

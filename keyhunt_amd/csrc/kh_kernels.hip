@@ -365,23 +365,20 @@ __device__ __forceinline__ uint4 ld_nt16(const uint4 *p) {
   v4u32 v = __builtin_nontemporal_load(reinterpret_cast<const v4u32 *>(p));
   return make_uint4(v.x, v.y, v.z, v.w);
 }
-// {global block index (shard*stride + block*16)/16, limbs 4, 3, 2} of one point
+// {block index within the shard, limbs 4, 3, and limb 2 with the shard byte in its top 8 bits} of
+// one point.  The masks read only bits 0..19 of limb 2, so the shard rides there and the record
+// addresses any layer whose shards are < 4 GB (the whole layer < 1 TB; a global 16-B block index
+// in 32 bits would stop at 64 GB).
 __device__ __forceinline__ uint4 blk_record(const walk_args &A, const fe &x) {
-#if KH_REC32
-  if (A.bstride16 < (1u << 24)) {  // wave-uniform: the whole layer's block index fits 32 bits
-    const uint32_t idx = __umul24(x.d[7] >> 24, A.bstride16) + blk_index(x.d[5], A.bd);
-    return make_uint4(idx, x.d[4], x.d[3], x.d[2]);
-  }
-#endif
-  const uint64_t off = (uint64_t)(x.d[7] >> 24) * A.bd.stride + (uint64_t)blk_index(x.d[5], A.bd) * 16;
-  return make_uint4((uint32_t)(off >> 4), x.d[4], x.d[3], x.d[2]);
+  return make_uint4(blk_index(x.d[5], A.bd), x.d[4], x.d[3], (x.d[2] & 0x000FFFFFu) | (x.d[7] & 0xFF000000u));
 }
 __device__ __forceinline__ uint4 blk_load(const walk_args &A, const uint4 &r) {
 #ifdef KH_TIMING_NO_PROBE_LOADS
   // timing-only build: no HBM reads (outputs are wrong); isolates the probe's compute
   return make_uint4(r.x, r.x * 3u, r.x * 5u, r.x * 7u);
 #else
-  return ld_nt16(reinterpret_cast<const uint4 *>(A.bloom) + r.x);
+  const uint8_t *shard = A.bloom + (uint64_t)(r.w >> 24) * A.bstride32;
+  return ld_nt16(reinterpret_cast<const uint4 *>(shard) + r.x);
 #endif
 }
 __device__ __forceinline__ bool blk_match_rec(const uint4 &v, const uint4 &r) { return blk_match(v, r.y, r.z, r.w); }
