@@ -99,30 +99,6 @@ std::string b58enc(const uint8_t *d, int n) {
   for (auto it = buf.rbegin(); it != buf.rend(); ++it) s += B58[*it];
   return s;
 }
-// b58tobin into exactly 25 bytes (forceReadFileAddress, keyhunt.cpp:7283-7292)
-bool b58dec25(const char *s, uint8_t out[25]) {
-  std::vector<uint8_t> buf;
-  int zeros = 0;
-  while (s[zeros] == '1') zeros++;
-  for (const char *q = s + zeros; *q; q++) {
-    const char *pos = strchr(B58, *q);
-    if (!pos) return false;
-    int carry = (int)(pos - B58);
-    for (auto &b : buf) {
-      carry += b * 58;
-      b = carry & 0xff;
-      carry >>= 8;
-    }
-    while (carry) {
-      buf.push_back(carry & 0xff);
-      carry >>= 8;
-    }
-  }
-  if (zeros + (int)buf.size() != 25) return false;
-  memset(out, 0, zeros);
-  for (size_t i = 0; i < buf.size(); i++) out[zeros + i] = buf[buf.size() - 1 - i];
-  return true;
-}
 std::string rmd_to_address(const uint8_t h[20]) {
   uint8_t d[25], c1[32], c2[32];
   d[0] = 0;
@@ -345,6 +321,27 @@ bool read_targets_eth(const char *fn, std::vector<uint8_t> &rows, uint64_t &bloo
 }
 
 // forceReadFileAddress (keyhunt.cpp:7239-7310) / forceReadFileXPoint (7392-7490)
+// The reference's line reads: fgets(buf, cap) pieces of at most cap - 1 characters (a longer line
+// is read as several pieces), trimmed of " \t\n\r" (util.c:217).
+std::vector<std::string> fgets_pieces(FILE *f, size_t cap) {
+  std::vector<std::string> out;
+  std::vector<char> buf(cap);
+  while (fgets(buf.data(), (int)cap, f)) {
+    trim(buf.data());
+    out.emplace_back(buf.data());
+  }
+  return out;
+}
+
+// -m address / rmd160 / xpoint target files, with the reference's reading quirks.
+//  address, rmd160 (forceReadFileAddress, keyhunt.cpp:7239-7305): items = lines longer than 20
+//    characters; then lines are consumed in order while i < items, a line that is not a 25-byte
+//    base58 address or 40 hex digits printing "[I] Ommiting invalid line" and lowering items by one,
+//    so valid lines after short or blank ones can go unread.  The base58 decode is b58tobin into a
+//    25-byte buffer whose result length alone decides (its return value is ignored, as there).
+//  xpoint (forceReadFileXPoint, keyhunt.cpp:7392-7490): items = lines of 40+ characters; the first
+//    `items` lines are table rows in order, an unusable one a zero row; lines missing at the end of
+//    the file lower the count.  (A blank line among them crashes the reference: strlen(NULL).)
 bool read_targets(const char *fn, int mode, std::vector<uint8_t> &rows, uint64_t &bloom_items,
                   std::vector<uint8_t> *adds = nullptr) {
   FILE *f = fopen(fn, "r");
@@ -352,28 +349,28 @@ bool read_targets(const char *fn, int mode, std::vector<uint8_t> &rows, uint64_t
     fprintf(stderr, "[E] Error opening the file %s\n", fn);
     return false;
   }
-  char line[1024];
-  uint64_t counted = 0;
-  std::vector<std::string> lines;
-  while (fgets(line, sizeof line, f)) {
-    trim(line);
-    size_t r = strlen(line);
-    if ((mode == MODE_XPOINT && r >= 40) || (mode != MODE_XPOINT && r > 20)) counted++;
-    lines.push_back(line);
-  }
+  const bool xp = mode == MODE_XPOINT;
+  std::vector<std::string> lines = fgets_pieces(f, xp ? 1000 : 100);
   fclose(f);
+  uint64_t counted = 0;
+  for (auto &ln : lines)
+    if ((xp && ln.size() >= 40) || (!xp && ln.size() > 20)) counted++;
   bloom_items = counted;
   printf("[+] Allocating memory for %llu elements: %.2f MB\n", (unsigned long long)counted,
          (double)(counted * 20) / 1048576.0);
-  for (auto &ln : lines) {
-    size_t r = ln.size();
-    uint8_t raw[100];
-    if (mode == MODE_XPOINT) {
-      if (r < 40) continue;
-      std::string tok = ln.substr(0, ln.find_first_of(" \t"));
+  uint8_t raw[100] = {0};
+  size_t next = 0;
+  if (xp) {
+    for (uint64_t i = 0; i < counted; i++) {
+      if (next >= lines.size()) {  // fgets hit the end of the file: "Omiting line", N--
+        fprintf(stderr, "[E] Omiting line : \n");
+        continue;
+      }
+      const std::string &ln = lines[next++];
+      std::string tok = ln.substr(0, ln.find_first_of(" \t:"));
       if (!is_hex(tok.c_str())) {
-        fprintf(stderr, "[E] Ignoring invalid hexvalue %s\n", ln.c_str());
-        rows.insert(rows.end(), 20, 0);  // the reference leaves a zero row (keyhunt.cpp:7419-7486)
+        fprintf(stderr, "[E] Ignoring invalid hexvalue %s\n", tok.c_str());  // aux after strtok
+        rows.insert(rows.end(), 20, 0);  // the row stays zero (keyhunt.cpp:7433)
         continue;
       }
       // the bloom gets the first 20 bytes of what was decoded: 04||X[0..19) for an uncompressed key
@@ -382,21 +379,26 @@ bool read_targets(const char *fn, int mode, std::vector<uint8_t> &rows, uint64_t
       else if (tok.size() == 66 && hex2bin(tok.c_str() + 2, raw, 32)) rows.insert(rows.end(), raw, raw + 20);
       else if (tok.size() == 130 && hex2bin(tok.c_str(), raw, 65)) rows.insert(rows.end(), raw + 2, raw + 22);
       else {
-        fprintf(stderr, "[E] Omiting line unknow length size %zu: %s\n", tok.size(), ln.c_str());
+        fprintf(stderr, "[E] Omiting line unknow length size %zu: %s\n", tok.size(), tok.c_str());
         rows.insert(rows.end(), 20, 0);
         continue;
       }
       if (adds) adds->insert(adds->end(), raw, raw + 20);
-      continue;
     }
-    if (r <= 20) continue;
+    return true;
+  }
+  uint64_t items = counted, i = 0;
+  while (i < items) {
+    const std::string ln = next < lines.size() ? lines[next++] : std::string();
+    const size_t r = ln.size();
     bool ok = false;
     if (r > 0 && r <= 40) {
-      if (r < 40) {
-        uint8_t a[25];
-        if (b58dec25(ln.c_str(), a)) {
-          rows.insert(rows.end(), a + 1, a + 21);
-          if (adds) adds->insert(adds->end(), a + 1, a + 21);
+      if (r < 40 && is_base58(ln.c_str())) {
+        size_t len = 25;
+        b58tobin_ref(raw, &len, ln.c_str(), r);
+        if (len == 25) {
+          rows.insert(rows.end(), raw + 1, raw + 21);
+          if (adds) adds->insert(adds->end(), raw + 1, raw + 21);
           ok = true;
         }
       }
@@ -406,7 +408,12 @@ bool read_targets(const char *fn, int mode, std::vector<uint8_t> &rows, uint64_t
         ok = true;
       }
     }
-    if (!ok) fprintf(stderr, "[I] Ommiting invalid line %s\n", ln.c_str());
+    if (ok) {
+      i++;
+    } else {
+      fprintf(stderr, "[I] Ommiting invalid line %s\n", ln.c_str());
+      items--;
+    }
   }
   return true;
 }

@@ -42,6 +42,11 @@ REF_GOLDEN = os.path.join(HERE, "_ref", "ref_golden")
 # (name, argv after the binary, timeout s).  Windows from SURVEY.md 8c.
 E2E_RUNS = [
     ("address_1to32_2p20", ["-m", "address", "-f", "1to32.txt", "-r", "1:100000", "-n", "0x100000", "-t", "8"], 300),
+    # malformed lines among the targets (tests/golden/make_ragged_targets.py): the reference's
+    # line counting and reading order decide which targets are loaded; stderr lines recorded
+    ("ragged_address_2p20", ["-m", "address", "-f", "ragged_addr.txt", "-r", "1:100000", "-n", "0x100000", "-t", "8"], 300),
+    ("ragged_rmd160_2p20", ["-m", "rmd160", "-f", "ragged_addr.txt", "-l", "compress", "-r", "1:100000", "-n", "0x100000", "-t", "8"], 300),
+    ("ragged_xpoint_2p20", ["-m", "xpoint", "-f", "ragged_x.txt", "-r", "1:100000", "-n", "0x100000", "-t", "8"], 300),
     ("rmd160_1to32_compress_2p20", ["-m", "rmd160", "-f", "1to32.rmd", "-l", "compress", "-r", "1:100000", "-n", "0x100000", "-t", "8"], 300),
     ("xpoint_1to63_65_2p20", ["-m", "xpoint", "-f", "1to63_65.txt", "-r", "1:100000", "-n", "0x100000", "-t", "8"], 300),
     ("rmd160_66_window", ["-m", "rmd160", "-f", "66.rmd", "-l", "compress", "-r", "2832ed74f2b000000:2832ed74f2bffffff", "-n", "0x100000", "-t", "8"], 600),
@@ -223,6 +228,10 @@ def parse_keyfound(text: str) -> list[dict]:
     return hits
 
 
+# the reference's notes on target-file lines it skips (keyhunt.cpp:7299, 7433, 7468, 7479)
+STDERR_NOTE = re.compile(r"^\[[IE]\] (?:Ommiting|Omiting|Ignoring)[^\n]*$", re.M)
+
+
 def gen_e2e(only: list[str] | None = None) -> None:
     subprocess.run(["make", "-s", "-C", HERE, "-f", "Makefile.ref", "-j8"], check=True)
     path = os.path.join(REPO, "tests", "golden", "ref_e2e.json")
@@ -241,6 +250,8 @@ def gen_e2e(only: list[str] | None = None) -> None:
             hits = sorted(parse_keyfound(text), key=lambda h: int(h["key"], 16))
             blocks = stdout_blocks(p.stdout)
             results[name] = {"argv": argv, "exit": p.returncode, "hits": hits, "stdout_blocks": blocks}
+            if name.startswith("ragged"):
+                results[name]["stderr_lines"] = STDERR_NOTE.findall(p.stderr)
             if name in CMP_BELOW:
                 lim = CMP_BELOW[name]
                 results[name].update(cmp_below=hex(lim), killed_after=tmo,

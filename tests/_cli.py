@@ -17,6 +17,10 @@ STDOUT_BLOCK = re.compile(r"\nHit! Private Key: [^\n]*\npubkey: [^\n]*\nAddress 
                           r"|\[\+\] Thread Key found privkey [0-9a-f]+ *\n?|\[\+\] Publickey [^\n]*\n")
 
 
+# the reference's notes on target-file lines it skips (same pattern as oracle/make_golden.py's)
+STDERR_NOTE = re.compile(r"^\[[IE]\] (?:Ommiting|Omiting|Ignoring)[^\n]*$", re.M)
+
+
 def parse_keyfound(text: str) -> list[dict]:
     hits = []
     for m in re.finditer(r"(Vanity )?Private Key: ([0-9a-f]+)\npubkey: ([0-9a-f]+)\nAddress (\S+)\nrmd160 ([0-9a-f]+)", text):
@@ -78,4 +82,6 @@ def check_against_reference(ref: dict, argv: list[str], name: str):
             rest.remove(b)
     else:
         assert blocks == ref_blocks
+    if "stderr_lines" in ref:  # the reference's notes on target-file lines it skipped, in order
+        assert STDERR_NOTE.findall(p.stderr) == ref["stderr_lines"]
     return p
