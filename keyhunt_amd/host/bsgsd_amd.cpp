@@ -406,19 +406,10 @@ void handle(int fd) {
   fe qx, qy;
   bool compressed = false;
   U from, to;
-  if (!parse_pubkey(pub.c_str(), qx, qy, compressed)) {
-    // Secp256K1::ParsePublicKeyHex's own message first (SECP256K1.cpp:327-372); a 04 key of the
-    // wrong length makes the reference exit (361), here it is refused like the others
-    const size_t len = pub.size();
-    const std::string pfx = len >= 2 ? pub.substr(0, 2) : "";
-    if (len < 2)
-      printf("ParsePublicKeyHex: Error invalid public key specified (66 or 130 character length)\n");
-    else if ((pfx == "02" || pfx == "03") && len != 66)
-      printf("ParsePublicKeyHex: Error invalid public key specified (66 character length)\n");
-    else if (pfx == "04" && len != 130)
-      printf("ParsePublicKeyHex: Error invalid public key specified (130 character length)\n");
-    else if (pfx != "02" && pfx != "03" && pfx != "04")
-      printf("ParsePublicKeyHex: Error invalid public key specified (Unexpected prefix (only 02,03 or 04 allowed)\n");
+  // Secp256K1::ParsePublicKeyHex prints its own message first (SECP256K1.cpp:303-380); where the
+  // reference exits (a 04 key of the wrong length, an unreadable digit pair) the request is refused
+  // like the others instead
+  if (parse_pubkey_hex_ref(pub.c_str(), qx, qy, compressed) <= 0) {
     printf("Invalid publickey format from client %s\n", pub.c_str());
     send_all(fd, bad, strlen(bad));
     return;

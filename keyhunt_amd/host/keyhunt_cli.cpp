@@ -1536,22 +1536,36 @@ int main(int argc, char **argv) {
       return EXIT_FAILURE;
     }
     printf("[+] Opening file %s\n", opt.file);
-    char line[1024];
-    while (fgets(line, sizeof line, f)) {
-      trim(line);
-      if (strlen(line) < 66) continue;
-      char *tok = strtok(line, " \t");
+    // keyhunt.cpp:1369-1446: N = lines of 66+ characters; each such line's first token (separators
+    // " \t:") is a public key of 66 or 130 characters (ParsePublicKeyHex), else "Invalid length"
+    std::vector<std::string> lines = fgets_pieces(f, 1022);
+    fclose(f);
+    size_t counted = 0;
+    for (auto &ln : lines) counted += ln.size() >= 66;
+    if (!counted) {
+      fprintf(stderr, "[E] There is no valid data in the file\n");
+      return EXIT_FAILURE;
+    }
+    for (auto &ln : lines) {
+      if (ln.size() < 66) continue;
+      std::vector<char> buf(ln.begin(), ln.end());
+      buf.push_back(0);
+      char *tok = strtok(buf.data(), " \t:");
+      const size_t tl = tok ? strlen(tok) : 0;
       fe x, y;
-      bool cp;
-      if (tok && parse_pubkey(tok, x, y, cp)) {
-        tx.push_back(x);
-        ty.push_back(y);
-        comp.push_back(cp);
+      bool cp = false;
+      if (tl == 66 || tl == 130) {
+        const int r = parse_pubkey_hex_ref(tok, x, y, cp);
+        if (r < 0) return 255;  // the reference's exit(-1)
+        if (r > 0) {
+          tx.push_back(x);
+          ty.push_back(y);
+          comp.push_back(cp);
+        }
       } else {
         printf("Invalid length: %s\n", tok ? tok : "");
       }
     }
-    fclose(f);
     if (tx.empty()) {
       fprintf(stderr, "[E] The file don't have any valid publickeys\n");
       return EXIT_FAILURE;

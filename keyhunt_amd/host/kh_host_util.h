@@ -233,6 +233,77 @@ inline bool parse_pubkey(const char *s, fe &x, fe &y, bool &compressed) {
   return false;
 }
 
+// Secp256K1::ParsePublicKeyHex (secp256k1/SECP256K1.cpp:303-380) with its printed messages: bytes
+// read two characters at a time by sscanf("%X") (GetByte, 303-314), the prefix picks the form, and
+// the point must lie on the curve.  Returns 1 on success, 0 on a refused key, -1 where the reference
+// calls exit(-1) (a digit pair sscanf cannot read, a 04 key of the wrong length).
+inline int parse_pubkey_hex_ref(const char *s, fe &x, fe &y, bool &compressed) {
+  const size_t len = strlen(s);
+  if (len < 2) {
+    printf("ParsePublicKeyHex: Error invalid public key specified (66 or 130 character length)\n");
+    return 0;
+  }
+  bool bad = false;
+  auto byte = [&](size_t idx) -> uint8_t {
+    char tmp[3] = {idx * 2 < len ? s[2 * idx] : '\0', idx * 2 + 1 < len ? s[2 * idx + 1] : '\0', 0};
+    int val = 0;
+    if (sscanf(tmp, "%X", &val) != 1) bad = true;
+    return (uint8_t)val;
+  };
+  auto fail_digit = [&]() {
+    printf("ParsePublicKeyHex: Error invalid public key specified (unexpected hexadecimal digit)\n");
+    return -1;
+  };
+  const uint8_t type = byte(0);
+  if (bad) return fail_digit();
+  uint8_t raw[64];
+  if (type == 0x02 || type == 0x03) {
+    if (len != 66) {
+      printf("ParsePublicKeyHex: Error invalid public key specified (66 character length)\n");
+      return 0;
+    }
+    for (int i = 0; i < 32; i++) raw[i] = byte(i + 1);
+    if (bad) return fail_digit();
+    fe_from_be(x, raw);
+    fe t, s3, seven;
+    fe_sqr(t, x);
+    fe_mul(t, t, x);
+    fe_set_u32(seven, 7);
+    fe_add(s3, t, seven);
+    if (!fe_sqrt(y, s3)) {
+      printf("ParsePublicKeyHex: Error invalid public key specified (Not lie on elliptic curve)\n");
+      return 0;
+    }
+    if ((y.d[0] & 1) != (uint32_t)(type == 0x03)) fe_neg(y, y);
+    compressed = true;
+    return 1;
+  }
+  if (type == 0x04) {
+    if (len != 130) {
+      printf("ParsePublicKeyHex: Error invalid public key specified (130 character length)\n");
+      return -1;
+    }
+    for (int i = 0; i < 64; i++) raw[i] = byte(i + 1);
+    if (bad) return fail_digit();
+    fe_from_be(x, raw);
+    fe_from_be(y, raw + 32);
+    fe t, r, seven;
+    fe_sqr(t, x);
+    fe_mul(t, t, x);
+    fe_set_u32(seven, 7);
+    fe_add(r, t, seven);
+    fe_sqr(t, y);
+    if (!fe_eq(t, r)) {
+      printf("ParsePublicKeyHex: Error invalid public key specified (Not lie on elliptic curve)\n");
+      return 0;
+    }
+    compressed = false;
+    return 1;
+  }
+  printf("ParsePublicKeyHex: Error invalid public key specified (Unexpected prefix (only 02,03 or 04 allowed)\n");
+  return 0;
+}
+
 // ---------------------------------------------------------------------------------------------
 // vanity targets
 // ---------------------------------------------------------------------------------------------

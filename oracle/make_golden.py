@@ -47,6 +47,8 @@ E2E_RUNS = [
     ("ragged_address_2p20", ["-m", "address", "-f", "ragged_addr.txt", "-r", "1:100000", "-n", "0x100000", "-t", "8"], 300),
     ("ragged_rmd160_2p20", ["-m", "rmd160", "-f", "ragged_addr.txt", "-l", "compress", "-r", "1:100000", "-n", "0x100000", "-t", "8"], 300),
     ("ragged_xpoint_2p20", ["-m", "xpoint", "-f", "ragged_x.txt", "-r", "1:100000", "-n", "0x100000", "-t", "8"], 300),
+    ("ragged_bsgs_63_window", ["-m", "bsgs", "-f", "ragged_bsgs.txt", "-r", "7cce5a0000000000:7cce9a0000000000", "-t", "8"], 300),
+    ("ragged_bsgs_bad_digit", ["-m", "bsgs", "-f", "ragged_bsgs_bad.txt", "-r", "7cce5a0000000000:7cce9a0000000000", "-t", "8"], 60),
     ("rmd160_1to32_compress_2p20", ["-m", "rmd160", "-f", "1to32.rmd", "-l", "compress", "-r", "1:100000", "-n", "0x100000", "-t", "8"], 300),
     ("xpoint_1to63_65_2p20", ["-m", "xpoint", "-f", "1to63_65.txt", "-r", "1:100000", "-n", "0x100000", "-t", "8"], 300),
     ("rmd160_66_window", ["-m", "rmd160", "-f", "66.rmd", "-l", "compress", "-r", "2832ed74f2b000000:2832ed74f2bffffff", "-n", "0x100000", "-t", "8"], 600),
@@ -230,6 +232,8 @@ def parse_keyfound(text: str) -> list[dict]:
 
 # the reference's notes on target-file lines it skips (keyhunt.cpp:7299, 7433, 7468, 7479)
 STDERR_NOTE = re.compile(r"^\[[IE]\] (?:Ommiting|Omiting|Ignoring)[^\n]*$", re.M)
+# and on public keys it refuses (keyhunt.cpp:1433; SECP256K1.cpp:303-380)
+STDOUT_NOTE = re.compile(r"^(?:ParsePublicKeyHex: |Invalid length: )[^\n]*$", re.M)
 
 
 def gen_e2e(only: list[str] | None = None) -> None:
@@ -252,6 +256,7 @@ def gen_e2e(only: list[str] | None = None) -> None:
             results[name] = {"argv": argv, "exit": p.returncode, "hits": hits, "stdout_blocks": blocks}
             if name.startswith("ragged"):
                 results[name]["stderr_lines"] = STDERR_NOTE.findall(p.stderr)
+                results[name]["stdout_notes"] = STDOUT_NOTE.findall(p.stdout)
             if name in CMP_BELOW:
                 lim = CMP_BELOW[name]
                 results[name].update(cmp_below=hex(lim), killed_after=tmo,

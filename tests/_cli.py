@@ -19,6 +19,7 @@ STDOUT_BLOCK = re.compile(r"\nHit! Private Key: [^\n]*\npubkey: [^\n]*\nAddress 
 
 # the reference's notes on target-file lines it skips (same pattern as oracle/make_golden.py's)
 STDERR_NOTE = re.compile(r"^\[[IE]\] (?:Ommiting|Omiting|Ignoring)[^\n]*$", re.M)
+STDOUT_NOTE = re.compile(r"^(?:ParsePublicKeyHex: |Invalid length: )[^\n]*$", re.M)
 
 
 def parse_keyfound(text: str) -> list[dict]:
@@ -84,4 +85,6 @@ def check_against_reference(ref: dict, argv: list[str], name: str):
         assert blocks == ref_blocks
     if "stderr_lines" in ref:  # the reference's notes on target-file lines it skipped, in order
         assert STDERR_NOTE.findall(p.stderr) == ref["stderr_lines"]
+    if "stdout_notes" in ref:  # and on public keys it refused
+        assert STDOUT_NOTE.findall(p.stdout) == ref["stdout_notes"]
     return p

@@ -50,6 +50,16 @@ def main():
              f"04{u6[0]:064x}{u6[1]:064x}", comp(7), comp(8)]
     open(os.path.join(DATA, "ragged_x.txt"), "w").write("\n".join(lines) + "\n")
 
+    # BSGS public keys: first token of each 66+ character line; a wrong token length, a point off
+    # the curve and an unknown prefix are refused with ParsePublicKeyHex's messages
+    x_off = next(x for x in range(5, 100) if pow((x ** 3 + 7) % P, (P - 1) // 2, P) != 1)
+    u7 = mul(7)
+    lines = ["0365ec2994b8cc0a20d40dd69edfe55ca32a54bcbbaa6b0ddcff36049301a54579 puzzle63", "abc",
+             "ab" * 35, f"02{x_off:064x}", "05" + "11" * 32, f"04{u7[0]:064x}{u7[1]:064x}:seven"]
+    open(os.path.join(DATA, "ragged_bsgs.txt"), "w").write("\n".join(lines) + "\n")
+    # a digit pair sscanf("%X") cannot read: the reference exits (GetByte, SECP256K1.cpp:303-314)
+    open(os.path.join(DATA, "ragged_bsgs_bad.txt"), "w").write("02" + "zz" * 32 + "\n")
+
 
 if __name__ == "__main__":
     main()
