@@ -49,6 +49,18 @@ void u256_to_be(uint8_t b[32], const u256 &a) {
 }
 u256 u256_from_u128(u128 x) { return u256{{(uint64_t)x, (uint64_t)(x >> 64), 0, 0}}; }
 u256 u256_u64(uint64_t x) { return u256{{x, 0, 0, 0}}; }
+int u256_cmp(const u256 &a, const u256 &b);
+// st + count*stride >= n as plain integers (a key span that reaches the group order)
+bool reaches_order(const u256 &st, const u256 &stride, uint64_t count) {
+  u256 r;
+  unsigned __int128 c = 0;
+  for (int i = 0; i < 4; i++) {
+    c += (unsigned __int128)stride.v[i] * count + st.v[i];
+    r.v[i] = (uint64_t)c;
+    c >>= 64;
+  }
+  return c != 0 || u256_cmp(r, ORDER_N) >= 0;
+}
 int u256_cmp(const u256 &a, const u256 &b) {
   for (int i = 3; i >= 0; i--) {
     if (a.v[i] < b.v[i]) return -1;
@@ -783,15 +795,18 @@ int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride_be[32], u
          : search == KH_SEARCH_UNCOMPRESS ? KM_H160U
                                           : KM_H160B;
   if (endo) km |= KM_ENDO;
-  // xpoint and compressed rmd160/address (configs 2-3) walk 4096-point groups when the chunk holds
-  // whole ones (the default 2^32-key chunk does): one inversion per 4096 points
-  const int H = ((km == KM_XPOINT || km == KM_H160C) && n_keys % (2 * KH_WALK_HB) == 0 &&
-                 !getenv("KH_NO_BIG_GROUPS"))
-                    ? KH_WALK_HB
-                    : KH_WALK_H;
   u256 st = sc_reduce(u256_from_be(start));
   u256 stride = stride_be ? sc_reduce(u256_from_be(stride_be)) : u256_u64(1);
   if (u256_is_zero(stride)) return KH_E_ARG;
+  // xpoint and compressed rmd160/address (configs 2-3) walk 4096-point groups when the chunk holds
+  // whole ones (the default 2^32-key chunk does): one inversion per 4096 points.  A chunk that
+  // reaches the group order keeps the reference's 1024-key groups: there a centre can equal
+  // -(i+1)*stride*G, whose zero difference collapses the group's batch inversion (parity note 4),
+  // and only the reference's own geometry collapses the same groups (fixtures *_near_order)
+  const int H = ((km == KM_XPOINT || km == KM_H160C) && n_keys % (2 * KH_WALK_HB) == 0 &&
+                 !reaches_order(st, stride, n_keys + 4 * KH_WALK_HB) && !getenv("KH_NO_BIG_GROUPS"))
+                    ? KH_WALK_HB
+                    : KH_WALK_H;
   const uint32_t *tab = nullptr;
   int r;
 

@@ -47,6 +47,13 @@ E2E_RUNS = [
     ("ragged_address_2p20", ["-m", "address", "-f", "ragged_addr.txt", "-r", "1:100000", "-n", "0x100000", "-t", "8"], 300),
     ("ragged_rmd160_2p20", ["-m", "rmd160", "-f", "ragged_addr.txt", "-l", "compress", "-r", "1:100000", "-n", "0x100000", "-t", "8"], 300),
     ("ragged_xpoint_2p20", ["-m", "xpoint", "-f", "ragged_x.txt", "-r", "1:100000", "-n", "0x100000", "-t", "8"], 300),
+    # keys within 2^20 of the group order (tests/golden/make_near_order_targets.py)
+    ("address_near_order", ["-m", "address", "-f", "near_order_addr.txt", "-l", "compress", "-r",
+                            "fffffffffffffffffffffffffffffffebaaedce6af48a03bbfd25e8cd0264141:fffffffffffffffffffffffffffffffebaaedce6af48a03bbfd25e8cd0364140",
+                            "-n", "0x100000", "-t", "8"], 300),
+    ("xpoint_near_order", ["-m", "xpoint", "-f", "near_order_x.txt", "-r",
+                           "fffffffffffffffffffffffffffffffebaaedce6af48a03bbfd25e8cd0264141:fffffffffffffffffffffffffffffffebaaedce6af48a03bbfd25e8cd0364140",
+                           "-n", "0x100000", "-t", "8"], 300),
     ("ragged_bsgs_63_window", ["-m", "bsgs", "-f", "ragged_bsgs.txt", "-r", "7cce5a0000000000:7cce9a0000000000", "-t", "8"], 300),
     ("ragged_bsgs_bad_digit", ["-m", "bsgs", "-f", "ragged_bsgs_bad.txt", "-r", "7cce5a0000000000:7cce9a0000000000", "-t", "8"], 60),
     ("rmd160_1to32_compress_2p20", ["-m", "rmd160", "-f", "1to32.rmd", "-l", "compress", "-r", "1:100000", "-n", "0x100000", "-t", "8"], 300),
