@@ -31,10 +31,11 @@ side is reported too ("hbm"): algorithmic bytes (BSGS: 64 B per giant point, one
 blocked layer 1; the reference layout's is 128 B) / launch time against 8 TB/s, and
 traffic = HBM bytes per launch from the PMC counters with the guide's gfx950 corrections
 (tools/pmc_summary.py), or null.
-cpu_baseline: rank 0 at N=1 only.  BSGS: the oracle's restatement of the giant-step loop
-(oracle/kh_oracle.c, keyhunt.cpp:4644-4880) on all host threads against the same GPU-built bloom
-(kind "port").  rmd160: the reference binary built from its own sources (oracle/_ref/keyhunt, kind
-"reference") on all host threads for ~20 s.
+cpu_baseline: rank 0 at N=1 only, on every leg the reference binary built from its own sources
+(oracle/_ref/keyhunt, oracle/Makefile.ref; kind "reference") run for --cpu-seconds on the job's CPU
+share (cpu_threads), its own last stats line parsed.  BSGS skips the reference's baby-step build:
+the engine writes the -S table files in the reference's format (kh_bsgs_save, byte-identical) and the
+reference reads them (-S -6).
 """
 from __future__ import annotations
 
