@@ -18,7 +18,7 @@ reported.  torch.distributed (gloo, CPU tensors) provides the barrier and the ma
 engine owns the GPU through its own HIP stream, synchronised on both sides of the timed region.
 
 roofline: dominant kernel of each leg (the giant-step walk k_walk<7, 2048>; k_walk<0, 2048> and
-k_walk<3, 2048> for rmd160 / xpoint), from HIP events the engine records on its own stream around
+k_walk<10, 2048> for rmd160 / xpoint), from HIP events the engine records on its own stream around
 its launches.  The walks are bound by VALU issue, so "bound" is "valu":
 achieved = VALU wave-instructions per launch (rocprofv3 SQ_INSTS_VALU per point, committed under
 profiles/, x this run's points per launch) / mean launch time; peak = 1024 SIMDs x 2.4 GHz / 4
@@ -293,7 +293,7 @@ def xpoint_leg(D: Dist, eng, args):
     keys = D.world * args.steps_rmd * chunk
     return {"value": keys / T / 1e6, "ms_per_step": T / args.steps_rmd * 1e3,
             "points_per_s_in_kernel": pts / (ms / 1e3),
-            "roofline": walk_roofline("k_walk<3, 2048>", pts / la, ms / la, 0, la)}
+            "roofline": walk_roofline("k_walk<10, 2048>", pts / la, ms / la, 0, la)}
 
 
 def cpu_host() -> dict:

@@ -63,6 +63,12 @@ static_assert(KH_WALK_H >= 64 && KH_WALK_H <= 512 && (512 % KH_WALK_H) == 0,
 #ifndef KH_SPARSE_ALL
 #define KH_SPARSE_ALL 0
 #endif
+//   KH_XPOINT_DEFER -m xpoint against the blocked target filter walks like the BSGS giant walk: a
+//                pair's two 16-B filter loads are issued one step later and tested after that
+//                step's field math (k_walk<KM_XPOINTB>), and -(dy) = T.y + C.y replaces the negation
+#ifndef KH_XPOINT_DEFER
+#define KH_XPOINT_DEFER 1
+#endif
 
 enum kh_walk_mode {
   KM_H160C = 0,   // hash160(02||X), hash160(03||X)          -l compress
@@ -75,6 +81,7 @@ enum kh_walk_mode {
   KM_BSGSB = 7,   // giant steps against the blocked layer-1 bloom (one 16-B block per probe)
   KM_BUILDB = 8,  // baby-step build with the blocked layer-1 bloom
   KM_ETH = 9,     // Keccak-256(X||Y)[12..32): Ethereum address -> target bloom (-c eth)
+  KM_XPOINTB = 10,  // KM_XPOINT with the blocked target filter, deferred probes (launch_walk picks it)
   // flag on KM_H160C/U/B and KM_XPOINT: also probe the endomorphism images (beta*x, y) and
   // (beta^2*x, y), i.e. keys lambda*k and lambda^2*k (-e, keyhunt.cpp:3408-3440, 3476-3830)
   KM_ENDO = 16,

@@ -382,6 +382,12 @@ __device__ __forceinline__ uint4 blk_load(const walk_args &A, const uint4 &r) {
 #endif
 }
 __device__ __forceinline__ bool blk_match_rec(const uint4 &v, const uint4 &r) { return blk_match(v, r.y, r.z, r.w); }
+// {target-filter block, w1, w2, w3} of X[0..20), w_j = bswap32(limb 7 - j) as in probe_xpoint /
+// tblk_probe: the -m xpoint probe record that crosses the loop edge in k_walk<KM_XPOINTB>
+__device__ __forceinline__ uint4 tblk_record(const walk_args &A, const fe &x) {
+  return make_uint4((uint32_t)(((uint64_t)bswap32(x.d[7]) * A.tblocks) >> 32), bswap32(x.d[6]), bswap32(x.d[5]),
+                    bswap32(x.d[4]));
+}
 // one blocked probe, in place (the group centre)
 __device__ __forceinline__ void blk_probe(const walk_args &A, const fe &x, uint64_t idx) {
   const uint4 r = blk_record(A, x);
@@ -549,7 +555,9 @@ __global__ void __launch_bounds__((walk_threads<MODE, H>()), (walk_blocks_per_cu
     // the centre itself (offset 0)
     if constexpr (MODE == KM_BSGSB)
       blk_probe(A, cx, cidx);
-    else
+    else if constexpr (MODE == KM_XPOINTB) {
+      if (cidx < A.n_points) probe_xpoint(A, cx, cidx, 0);
+    } else
       probe_point<MODE>(A, cx, cy, cidx);
 
     // backward: recover 1/dx_i and emit C - T[i] (offset -(i+1)) and C + T[i] (offset i+1).
@@ -609,13 +617,33 @@ __global__ void __launch_bounds__((walk_threads<MODE, H>()), (walk_blocks_per_cu
         plive = (cidx - off < A.n_points ? 1u : 0u) | (i < H - 1 && cidx + off < A.n_points ? 2u : 0u);
         continue;
       }
-      fe nty;
-      fe_neg(nty, ty);
+      if constexpr (MODE == KM_XPOINTB) {
+        // -m xpoint against the blocked target filter (L2-resident): the same deferred-probe shape
+        const uint4 vm = A.tblk[pm.x], vp = A.tblk[pp.x];
+        fe xm, xp, s, dy, sx;
+        fe_add(sx, cx, tx);
+        fe_add(dy, ty, cy);  // -(dy) of C - T[i]: s^2 is the same
+        fe_mul(s, dy, di);
+        fe_sqr(xm, s);
+        fe_sub(xm, xm, sx);
+        fe_sub(dy, ty, cy);
+        fe_mul(s, dy, di);
+        fe_sqr(xp, s);
+        fe_sub(xp, xp, sx);
+        if ((plive & 1u) && blk_match_rec(vm, pm)) record_hit(A, cidx - poff, 3);
+        if ((plive & 2u) && blk_match_rec(vp, pp)) record_hit(A, cidx + poff, 3);
+        const uint64_t off = (uint64_t)(i + 1);
+        pm = tblk_record(A, xm);
+        pp = tblk_record(A, xp);
+        poff = off;
+        plive = (cidx - off < A.n_points ? 1u : 0u) | (i < H - 1 && cidx + off < A.n_points ? 2u : 0u);
+        continue;
+      }
       if constexpr (MODE == KM_BSGS) {
         // both points first, then one lockstep probe of the pair (two loads in flight per lane)
         fe xm, xp, s, dy, sx;
         fe_add(sx, cx, tx);
-        fe_sub(dy, nty, cy);
+        fe_add(dy, ty, cy);  // -(dy) of C - T[i]: only x is needed, s^2 is the same
         fe_mul(s, dy, di);
         fe_sqr(xm, s);
         fe_sub(xm, xm, sx);
@@ -629,6 +657,8 @@ __global__ void __launch_bounds__((walk_threads<MODE, H>()), (walk_blocks_per_cu
       }
       fe sx;
       fe_add(sx, cx, tx);  // x3 = s^2 - (C.x + T.x) on both sides
+      fe nty;
+      fe_neg(nty, ty);
 #pragma unroll 1
       for (int side = 0; side < 2; side++) {
         if (side == 1 && i == H - 1) break;
@@ -652,6 +682,10 @@ __global__ void __launch_bounds__((walk_threads<MODE, H>()), (walk_blocks_per_cu
     if constexpr (MODE == KM_BSGSB) {  // the last pair of the group
       if ((plive & 1u) && blk_match_rec(blk_load(A, pm), pm)) record_hit(A, cidx - poff, 4);
       if ((plive & 2u) && blk_match_rec(blk_load(A, pp), pp)) record_hit(A, cidx + poff, 4);
+    }
+    if constexpr (MODE == KM_XPOINTB) {
+      if ((plive & 1u) && blk_match_rec(A.tblk[pm.x], pm)) record_hit(A, cidx - poff, 3);
+      if ((plive & 2u) && blk_match_rec(A.tblk[pp.x], pp)) record_hit(A, cidx + poff, 3);
     }
     // next centre C += T[H]  (keyhunt.cpp:3840-3855)
     {
@@ -953,6 +987,7 @@ namespace kh {
 
 hipError_t launch_walk(int mode, const walk_args &A, hipStream_t st, int H) {
   dim3 block(256), grid((A.L + 255) / 256);
+  if (KH_XPOINT_DEFER && mode == KM_XPOINT && A.tblk) mode = KM_XPOINTB;
   if (H == KH_WALK_HB) {
     constexpr int TB = walk_threads<KM_BSGSB, KH_WALK_HB>();
     switch (mode) {
@@ -961,6 +996,7 @@ hipError_t launch_walk(int mode, const walk_args &A, hipStream_t st, int H) {
         hipLaunchKernelGGL((k_walk<KM_BSGSB, KH_WALK_HB>), dim3((A.L + TB - 1) / TB), dim3(TB), 0, st, A);
         break;
       case KM_XPOINT: hipLaunchKernelGGL((k_walk<KM_XPOINT, KH_WALK_HB>), grid, block, 0, st, A); break;
+      case KM_XPOINTB: hipLaunchKernelGGL((k_walk<KM_XPOINTB, KH_WALK_HB>), grid, block, 0, st, A); break;
       case KM_H160C: hipLaunchKernelGGL((k_walk<KM_H160C, KH_WALK_HB>), grid, block, 0, st, A); break;
       default: return hipErrorInvalidValue;
     }
@@ -977,6 +1013,7 @@ hipError_t launch_walk(int mode, const walk_args &A, hipStream_t st, int H) {
     case KM_H160U: hipLaunchKernelGGL(k_walk<KM_H160U>, grid, block, 0, st, A); break;
     case KM_H160B: hipLaunchKernelGGL(k_walk<KM_H160B>, grid, block, 0, st, A); break;
     case KM_XPOINT: hipLaunchKernelGGL(k_walk<KM_XPOINT>, grid, block, 0, st, A); break;
+    case KM_XPOINTB: hipLaunchKernelGGL(k_walk<KM_XPOINTB>, grid, block, 0, st, A); break;
     case KM_BSGS: hipLaunchKernelGGL(k_walk<KM_BSGS>, grid, block, 0, st, A); break;
     case KM_BUILD: hipLaunchKernelGGL(k_walk<KM_BUILD>, grid, block, 0, st, A); break;
     case KM_DUMP: hipLaunchKernelGGL(k_walk<KM_DUMP>, grid, block, 0, st, A); break;
