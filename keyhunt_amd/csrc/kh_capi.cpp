@@ -710,7 +710,7 @@ int kh_synchronize(kh_ctx *ctx) {
 // ---------------------------------------------------------------------------------------------
 // The blocked target filter the walk probes for exact targets (kh_kernels.hip tblk_probe): 16-byte
 // blocks, KH_BLK_BITS_MUL x the reference bloom's bits; row words w = little-endian u32s of the
-// 20 bytes: block (w0 * blocks) >> 32, bits from 5-bit fields of w1, w2, w3 as blk_masks.
+// 20 bytes: block (w0 * blocks) >> 32, bits from w1, w2 (, w3) as kh_blk_masks (kh_kernels.h).
 static int upload_tblk(kh_ctx *c) {
   const uint64_t blocks = (c->tbd.bits * KH_BLK_BITS_MUL + 127) / 128;
   std::vector<uint32_t> words(blocks * 4, 0);
@@ -721,10 +721,9 @@ static int upload_tblk(kh_ctx *c) {
       w[k] = (uint32_t)p[4 * k] | ((uint32_t)p[4 * k + 1] << 8) | ((uint32_t)p[4 * k + 2] << 16) |
              ((uint32_t)p[4 * k + 3] << 24);
     const uint64_t blk = ((uint64_t)w[0] * blocks) >> 32;
-    for (int t = 0; t < 16; t++) {
-      const uint32_t src = w[1 + t / 6];
-      words[blk * 4 + t / 4] |= 1u << ((src >> (5 * (t % 6))) & 31u);
-    }
+    uint32_t m[4];
+    kh_blk_masks(w[1], w[2], w[3], m);
+    for (int k = 0; k < 4; k++) words[blk * 4 + k] |= m[k];
   }
   (void)hipFree(c->d_tblk);
   c->d_tblk = nullptr;

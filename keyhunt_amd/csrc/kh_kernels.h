@@ -36,12 +36,51 @@ static_assert(KH_WALK_H >= 64 && KH_WALK_H <= 512 && (512 % KH_WALK_H) == 0,
 // Blocked layer-1 bloom (KH_LAYER1_BLOCKED), a split-block filter: per shard X[0], `blocks` 16-byte
 // blocks, blocks = ceil(KH_BLK_BITS_MUL x reference bits / 128).  An item X (an x-coordinate, so
 // already uniform) uses its own bits instead of a hash: with u = big-endian u32 of X[8..12), the
-// block is (u * blocks) >> 32.  The 16 bit positions are 5-bit fields of the next 96 bits, taken
-// as big-endian u32s s0 = X[12..16), s1 = X[16..20), s2 = X[20..24): field f (f < 16) is
-// (s_{f/6} >> 5*(f%6)) & 31; fields 4w..4w+3 are the bits set in little-endian u32 word w of the
-// block (w < 4).  An item is present iff every word covers its mask.  3x the reference's bits:
-// FP 5.6e-7 (Poisson block load) vs the reference's 1e-6; one 16-byte load per probe, no hashing.
+// block is (u * blocks) >> 32; its 16 bit positions come from X[12..20) (kh_blk_masks below).  An
+// item is present iff every little-endian u32 word of the block covers its mask.  3x the
+// reference's bits: FP 6.6e-7 (Poisson block load) vs the reference's 1e-6; one 16-byte load per
+// probe, no hashing.
 #define KH_BLK_BITS_MUL 3
+
+// Bit positions of the split-block filters (blocked layer 1 above, and the exact-target filter of
+// kh_kernels.hip tblk_probe), from an item's position words s0, s1 (layer 1: the big-endian u32s of
+// X[12..16), X[16..20); targets: w1, w2).  KH_PK_MASKS (default): block word w (< 4) gets 4 bits, 2 in
+// each 16-bit half: with s = s_{w/2}, a = s >> 8*(w%2) and b = a >> 4, the bits
+//   a & 15,  16 + ((a >> 16) & 15),  b & 15,  16 + ((b >> 16) & 15)
+// -- each pair is one v_pk_lshlrev_b16 of 0x00010001, so the 16 positions cost 6 shifts and 8 packed
+// shifts (the 5-bit-field form below, KH_PK_MASKS=0, costs two 32-bit shifts per position).  Every
+// bit of s0 and s1 is used once; per 16-bit half the FP model is the same as per 32-bit word.
+// KH_PK_MASKS=0: fields f < 16 of X[12..24) (s0, s1, s2 = X[20..24)), (s_{f/6} >> 5*(f%6)) & 31, bits
+// 4w..4w+3 in word w.
+#ifndef KH_PK_MASKS
+#define KH_PK_MASKS 1
+#endif
+// (1 << (a & 15)) | (1 << (16 + ((a >> 16) & 15)))
+KH_HD uint32_t kh_pk_bits(uint32_t a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t r;
+  asm("v_pk_lshlrev_b16 %0, %1, %2" : "=v"(r) : "v"(a), "s"(0x00010001u));
+  return r;
+#else
+  return (1u << (a & 15u)) | (1u << (16u + ((a >> 16) & 15u)));
+#endif
+}
+KH_HD void kh_blk_masks(uint32_t s0, uint32_t s1, uint32_t s2, uint32_t m[4]) {
+  if (KH_PK_MASKS) {
+    (void)s2;
+    m[0] = kh_pk_bits(s0) | kh_pk_bits(s0 >> 4);
+    m[1] = kh_pk_bits(s0 >> 8) | kh_pk_bits(s0 >> 12);
+    m[2] = kh_pk_bits(s1) | kh_pk_bits(s1 >> 4);
+    m[3] = kh_pk_bits(s1 >> 8) | kh_pk_bits(s1 >> 12);
+    return;
+  }
+  uint32_t f[16];
+  for (int t = 0; t < 16; t++) {
+    const uint32_t s = t < 6 ? s0 : t < 12 ? s1 : s2;
+    f[t] = 1u << ((s >> (5 * (t % 6))) & 31u);
+  }
+  for (int w = 0; w < 4; w++) m[w] = f[4 * w] | f[4 * w + 1] | f[4 * w + 2] | f[4 * w + 3];
+}
 
 // Variant switches of the BSGS giant walk (k_walk<KM_BSGSB, KH_WALK_HB>), A/B-measured:
 //   KH_TAB_LDS   the delta table staged in LDS (one 1024-thread workgroup per CU, ds_read_b128

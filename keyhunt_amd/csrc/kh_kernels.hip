@@ -109,22 +109,15 @@ __device__ __forceinline__ void bloom_insert(uint8_t *__restrict__ bf_base, uint
 
 // Blocked layer-1 (split-block) geometry, kh_kernels.h: desc.bits = blocks per shard.  The item
 // is an x-coordinate, already uniform, so the block and the bit positions are taken from its words
-// directly (no XXH64): block = (X[8..12) * blocks) >> 32 (limb 5); positions = 5-bit fields of
-// X[12..24) (limbs 4, 3, 2).
+// directly (no XXH64): block = (X[8..12) * blocks) >> 32 (limb 5); positions from X[12..20) (limbs
+// 4, 3) by kh_blk_masks (kh_kernels.h).
 __device__ __forceinline__ uint32_t blk_index(uint32_t w5, const bloom_desc &bd) {
   return (uint32_t)(((uint64_t)w5 * bd.bits) >> 32);
 }
-// masks of the four block words from s0 = limb 4, s1 = limb 3, s2 = limb 2.  `1u << (s >> k)`
-// is one v_lshrrev + one v_lshlrev: the hardware shift uses the low 5 bits of the amount.
+// masks of the four block words from s0 = limb 4, s1 = limb 3, s2 = limb 2 (kh_kernels.h
+// kh_blk_masks: packed 16-bit shifts, or `1u << (s >> k)` per 5-bit field with KH_PK_MASKS=0)
 __device__ __forceinline__ void blk_masks(uint32_t s0, uint32_t s1, uint32_t s2, uint32_t m[4]) {
-  uint32_t f[16];
-#pragma unroll
-  for (int t = 0; t < 16; t++) {
-    const uint32_t s = t < 6 ? s0 : t < 12 ? s1 : s2;
-    f[t] = 1u << ((s >> (5 * (t % 6))) & 31u);
-  }
-#pragma unroll
-  for (int w = 0; w < 4; w++) m[w] = f[4 * w] | f[4 * w + 1] | f[4 * w + 2] | f[4 * w + 3];
+  kh_blk_masks(s0, s1, s2, m);
 }
 __device__ __forceinline__ bool blk_match(const uint4 &v, uint32_t s0, uint32_t s1, uint32_t s2) {
   uint32_t m[4];
@@ -162,8 +155,8 @@ __device__ __forceinline__ void x_bytes_u64(const fe &x, uint64_t in[4]) {
 
 // Exact 20-byte targets (hash160, X[0..20), eth address) are uniform, so they go to a split-block
 // filter keyed on their own words, like the blocked BSGS layer 1: with w = the little-endian u32s
-// of the 20 bytes, the 16-byte block is (w0 * blocks) >> 32 and the bit positions are 5-bit fields
-// of w1, w2, w3 (blk_masks).  One 16-B load, no XXH64.  Every filter hit is still confirmed by the
+// of the 20 bytes, the 16-byte block is (w0 * blocks) >> 32 and the bit positions come from w1, w2
+// (kh_blk_masks).  One 16-B load, no XXH64.  Every filter hit is still confirmed by the
 // host's exact table search (searchbinary), so the reported hits are the reference's.
 __device__ __forceinline__ bool tblk_probe(const walk_args &A, const uint32_t w[5]) {
   const uint32_t blk = (uint32_t)(((uint64_t)w[0] * A.tblocks) >> 32);
@@ -365,11 +358,13 @@ __device__ __forceinline__ uint4 ld_nt16(const uint4 *p) {
   v4u32 v = __builtin_nontemporal_load(reinterpret_cast<const v4u32 *>(p));
   return make_uint4(v.x, v.y, v.z, v.w);
 }
-// {block index within the shard, limbs 4, 3, and limb 2 with the shard byte in its top 8 bits} of
-// one point.  The masks read only bits 0..19 of limb 2, so the shard rides there and the record
-// addresses any layer whose shards are < 4 GB (the whole layer < 1 TB; a global 16-B block index
-// in 32 bits would stop at 64 GB).
+// {block index within the shard, limbs 4, 3, and the shard byte in the top 8 bits of the last word}
+// of one point (KH_PK_MASKS=0: limb 2, whose bits 0..19 are all its masks read).  The record
+// addresses any layer whose shards are < 4 GB (the whole layer < 1 TB; a global 16-B block index in
+// 32 bits would stop at 64 GB).
 __device__ __forceinline__ uint4 blk_record(const walk_args &A, const fe &x) {
+  // the packed-shift masks read limbs 4 and 3 only: the shard byte rides as limb 7 itself
+  if constexpr (KH_PK_MASKS) return make_uint4(blk_index(x.d[5], A.bd), x.d[4], x.d[3], x.d[7]);
   return make_uint4(blk_index(x.d[5], A.bd), x.d[4], x.d[3], (x.d[2] & 0x000FFFFFu) | (x.d[7] & 0xFF000000u));
 }
 __device__ __forceinline__ uint4 blk_load(const walk_args &A, const uint4 &r) {
@@ -386,7 +381,7 @@ __device__ __forceinline__ bool blk_match_rec(const uint4 &v, const uint4 &r) { 
 // tblk_probe: the -m xpoint probe record that crosses the loop edge in k_walk<KM_XPOINTB>
 __device__ __forceinline__ uint4 tblk_record(const walk_args &A, const fe &x) {
   return make_uint4((uint32_t)(((uint64_t)bswap32(x.d[7]) * A.tblocks) >> 32), bswap32(x.d[6]), bswap32(x.d[5]),
-                    bswap32(x.d[4]));
+                    KH_PK_MASKS ? 0u : bswap32(x.d[4]));  // w3 feeds only the 5-bit-field masks
 }
 // one blocked probe, in place (the group centre)
 __device__ __forceinline__ void blk_probe(const walk_args &A, const fe &x, uint64_t idx) {

@@ -144,7 +144,7 @@ def test_bsgs_multi_target_and_not_found(engine, oracle):
 @pytest.mark.parametrize("layer1", [0, 1], ids=["reference", "blocked"])
 def test_layer1_layouts_no_false_negative_and_fp_rate(engine, oracle, layer1):
     """Every baby X is in layer 1 (bloom has no false negatives) in both layouts; random X's pass at
-    a rate near the design error (reference 1e-6, blocked 5.6e-7)."""
+    a rate near the design error (reference 1e-6, blocked 6.6e-7)."""
     import random
     n, k = 1 << 30, 8                       # M = 2^18 babies
     info = engine.bsgs_setup(n, k, layer1=layer1)
@@ -155,7 +155,7 @@ def test_layer1_layouts_no_false_negative_and_fp_rate(engine, oracle, layer1):
     rng = random.Random(11)
     rnd = [rng.getrandbits(256).to_bytes(32, "big") for _ in range(200000)]
     fp = sum(engine.bloom_check(1, rnd))
-    assert fp <= 5   # expectation 0.2 (reference) / 0.11 (blocked) false positives
+    assert fp <= 5   # expectation 0.2 (reference) / 0.13 (blocked) false positives
 
 
 def test_blocked_and_reference_find_same_keys(engine, oracle):
@@ -173,10 +173,11 @@ def test_blocked_and_reference_find_same_keys(engine, oracle):
 
 
 def test_blocked_layer1_bytes_match_layout_spec(engine, oracle):
-    """The blocked (split-block) layer-1 bloom is bit-exact with its specification (kh_kernels.h):
-    shard X[0]; 16-byte block (u * blocks) >> 32 with u = X[8..12); four little-endian u32 words,
-    each with the 4 bits given by 5-bit fields of X[12..24) (big-endian u32s s0, s1, s2; field f is
-    (s_{f/6} >> 5*(f%6)) & 31)."""
+    """The blocked (split-block) layer-1 bloom is bit-exact with its specification (kh_kernels.h
+    kh_blk_masks): shard X[0]; 16-byte block (u * blocks) >> 32 with u = X[8..12); four little-endian
+    u32 words; word w gets, from s = s_{w/2} (big-endian u32s s0 = X[12..16), s1 = X[16..20)),
+    a = s >> 8*(w%2) and b = a >> 4, the bits a & 15, 16 + ((a >> 16) & 15), b & 15 and
+    16 + ((b >> 16) & 15) (two per 16-bit half: one v_pk_lshlrev_b16 per pair)."""
     info = engine.bsgs_setup(1 << 20, 1, layer1=1)       # M = 1024 babies
     engine.bsgs_build()
     blocks = info.bloom_bits[0] // 128
@@ -185,12 +186,13 @@ def test_blocked_layer1_bytes_match_layout_spec(engine, oracle):
     for i in range(1, info.m + 1):
         xb = oracle.pubkey(i)[0].to_bytes(32, "big")
         u = int.from_bytes(xb[8:12], "big")
-        s = [int.from_bytes(xb[12 + 4 * q:16 + 4 * q], "big") for q in range(3)]
+        s = [int.from_bytes(xb[12 + 4 * q:16 + 4 * q], "big") for q in range(2)]
         base = xb[0] * blocks * 16 + ((u * blocks) >> 32) * 16
-        fields = [(s[f // 6] >> (5 * (f % 6))) & 31 for f in range(16)]
         for w in range(4):
-            for f in fields[4 * w:4 * w + 4]:
-                model[base + 4 * w + (f >> 3)] |= 1 << (f & 7)
+            a = s[w // 2] >> (8 * (w % 2))
+            for v in (a, a >> 4):
+                for f in (v & 15, 16 + ((v >> 16) & 15)):
+                    model[base + 4 * w + (f >> 3)] |= 1 << (f & 7)
     assert engine.get_bloom(1) == bytes(model)
 
 

@@ -103,3 +103,41 @@ if __name__ == "__main__":
     for mult in (2.0, 3.0):
         print(f"split-block 128 (4 words x 4 bits), bits x{mult}: model {model_split(128 / (BPE * mult)):.3g}"
               f"  sim {simulate_split128(65536, mult):.3g}")
+
+
+def pk128_masks(s0: np.ndarray, s1: np.ndarray):
+    """Masks of the packed-shift layout (kh_kernels.h kh_blk_masks, KH_PK_MASKS): word w gets, from
+    s = s_{w/2}, a = s >> 8*(w%2) and b = a >> 4, bits a & 15, 16 + (a >> 16 & 15), b & 15, 16 + (b >> 16 & 15)."""
+    masks = []
+    for w in range(4):
+        a = (s0 if w < 2 else s1) >> np.uint64(8 * (w % 2))
+        m = np.zeros_like(a)
+        for v in (a, a >> np.uint64(4)):
+            m |= np.uint64(1) << (v & np.uint64(15))
+            m |= np.uint64(1) << (np.uint64(16) + ((v >> np.uint64(16)) & np.uint64(15)))
+        masks.append(m)
+    return masks
+
+
+def simulate_pk128(items: int, mult: float, queries: int = 4_000_000, seed: int = 3) -> float:
+    rng = np.random.default_rng(seed)
+    blocks = math.ceil(math.ceil(items * BPE) * mult / 128)
+    filt = np.zeros((blocks, 4), dtype=np.uint64)
+
+    def draw(n):
+        return (rng.integers(0, blocks, size=n), rng.integers(0, 2**32, size=n, dtype=np.uint64),
+                rng.integers(0, 2**32, size=n, dtype=np.uint64))
+    blk, s0, s1 = draw(items)
+    for w, m in enumerate(pk128_masks(s0, s1)):
+        np.bitwise_or.at(filt[:, w], blk, m)
+    blk, s0, s1 = draw(queries)
+    ok = np.ones(queries, dtype=bool)
+    for w, m in enumerate(pk128_masks(s0, s1)):
+        ok &= (filt[blk, w] & m) == m
+    return float(ok.mean())
+
+
+if __name__ == "__main__":
+    lam = 128 / (BPE * 3.0)
+    print(f"packed-shift split-block 128 (8 halves x 2 bits), bits x3.0: model "
+          f"{model_split(lam, words=8, wbits=16, per_word=2):.3g}  sim {simulate_pk128(65536, 3.0):.3g}")
