@@ -59,7 +59,7 @@ extern "C" {
 /* layer-1 (bloom_bP) layouts for kh_bsgs_set_layer1 */
 #define KH_LAYER1_REFERENCE 0  /* the reference's bit layout (bloom/bloom.cpp): bit-identical tables */
 #define KH_LAYER1_BLOCKED 1    /* default: split-block filter, an item's 16 bits in one 16-byte block chosen by
-                                  the x-coordinate's own words (3x the bits per shard, FP 5.6e-7 vs 1e-6); one
+                                  the x-coordinate's own words (3x the bits per shard, FP 6.6e-7 vs 1e-6); one
                                   16-B load per probe.  Layers 2/3 stay in the reference layout, so refinement
                                   and found keys are unchanged */
 
