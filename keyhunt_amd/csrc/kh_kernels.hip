@@ -521,6 +521,18 @@ __global__ void __launch_bounds__((walk_threads<MODE, H>()), (walk_blocks_per_cu
   // multiplication in the backward pass: half the pad traffic for +1/2 multiplication per pair
   constexpr bool SPARSE = KH_SPARSE_ALL || (KH_SPARSE_BSGS && (MODE == KM_BSGSB || MODE == KM_BSGS));
   auto slot = [&](int m) { return (size_t)(SPARSE ? (m >> 1) : m) * L + g; };
+  // Deferred-probe walks (one 16-B split-block load per point, issued a step ahead): the BSGS giant
+  // walk against the blocked layer 1 (kind 4) and -m xpoint against the blocked target filter (kind 3)
+  constexpr bool DEFER = MODE == KM_BSGSB || MODE == KM_XPOINTB;
+  constexpr uint32_t DKIND = MODE == KM_BSGSB ? 4u : 3u;
+  auto drec = [&](const fe &x) -> uint4 {
+    if constexpr (MODE == KM_BSGSB) return blk_record(A, x);
+    else return tblk_record(A, x);
+  };
+  auto dload = [&](const uint4 &r) -> uint4 {
+    if constexpr (MODE == KM_BSGSB) return blk_load(A, r);
+    else return A.tblk[r.x];
+  };
   for (uint32_t j = 0; j < A.groups; j++) {
     const uint64_t cidx = A.interleave ? ((A.group_base + j) * (uint64_t)A.L + g) * (2 * H) + H
                                        : (uint64_t)g * A.lane_stride + (uint64_t)(A.group_base + j) * (2 * H) + H;
@@ -558,7 +570,7 @@ __global__ void __launch_bounds__((walk_threads<MODE, H>()), (walk_blocks_per_cu
     // backward: recover 1/dx_i and emit C - T[i] (offset -(i+1)) and C + T[i] (offset i+1).
     // Both points use the second operand (T.x, +-T.y): x3 = s^2 - C.x - T.x, y3 = s(T.x - x3) -+ T.y.
     // prefix[i-1] is fetched one iteration ahead so its HBM latency overlaps the previous pair
-    uint4 pm = make_uint4(0u, 0u, 0u, 0u), pp = make_uint4(0u, 0u, 0u, 0u);  // KM_BSGSB: previous pair's probe records
+    uint4 pm = make_uint4(0u, 0u, 0u, 0u), pp = make_uint4(0u, 0u, 0u, 0u);  // DEFER: previous pair's probe records
     uint64_t poff = 0;
     uint32_t plive = 0;
     fe pre;
@@ -588,11 +600,11 @@ __global__ void __launch_bounds__((walk_threads<MODE, H>()), (walk_blocks_per_cu
       } else {
         di = inv;
       }
-      if constexpr (MODE == KM_BSGSB) {
+      if constexpr (DEFER) {
         // The previous pair's block loads are issued first and tested after this pair's field
         // math: the loads fly during it.  Only their addresses cross the loop edge (ALU values),
         // never an in-flight load destination.
-        const uint4 vm = blk_load(A, pm), vp = blk_load(A, pp);
+        const uint4 vm = dload(pm), vp = dload(pp);
         fe xm, xp, s, dy, sx;
         fe_add(sx, cx, tx);  // x3 = s^2 - (C.x + T.x) for both points
         fe_add(dy, ty, cy);  // -(dy of C - T[i]); only s^2 is needed, so the sign drops out
@@ -603,33 +615,11 @@ __global__ void __launch_bounds__((walk_threads<MODE, H>()), (walk_blocks_per_cu
         fe_mul(s, dy, di);
         fe_sqr(xp, s);
         fe_sub(xp, xp, sx);
-        if ((plive & 1u) && blk_match_rec(vm, pm)) record_hit(A, cidx - poff, 4);
-        if ((plive & 2u) && blk_match_rec(vp, pp)) record_hit(A, cidx + poff, 4);
+        if ((plive & 1u) && blk_match_rec(vm, pm)) record_hit(A, cidx - poff, DKIND);
+        if ((plive & 2u) && blk_match_rec(vp, pp)) record_hit(A, cidx + poff, DKIND);
         const uint64_t off = (uint64_t)(i + 1);
-        pm = blk_record(A, xm);
-        pp = blk_record(A, xp);
-        poff = off;
-        plive = (cidx - off < A.n_points ? 1u : 0u) | (i < H - 1 && cidx + off < A.n_points ? 2u : 0u);
-        continue;
-      }
-      if constexpr (MODE == KM_XPOINTB) {
-        // -m xpoint against the blocked target filter (L2-resident): the same deferred-probe shape
-        const uint4 vm = A.tblk[pm.x], vp = A.tblk[pp.x];
-        fe xm, xp, s, dy, sx;
-        fe_add(sx, cx, tx);
-        fe_add(dy, ty, cy);  // -(dy) of C - T[i]: s^2 is the same
-        fe_mul(s, dy, di);
-        fe_sqr(xm, s);
-        fe_sub(xm, xm, sx);
-        fe_sub(dy, ty, cy);
-        fe_mul(s, dy, di);
-        fe_sqr(xp, s);
-        fe_sub(xp, xp, sx);
-        if ((plive & 1u) && blk_match_rec(vm, pm)) record_hit(A, cidx - poff, 3);
-        if ((plive & 2u) && blk_match_rec(vp, pp)) record_hit(A, cidx + poff, 3);
-        const uint64_t off = (uint64_t)(i + 1);
-        pm = tblk_record(A, xm);
-        pp = tblk_record(A, xp);
+        pm = drec(xm);
+        pp = drec(xp);
         poff = off;
         plive = (cidx - off < A.n_points ? 1u : 0u) | (i < H - 1 && cidx + off < A.n_points ? 2u : 0u);
         continue;
@@ -674,13 +664,9 @@ __global__ void __launch_bounds__((walk_threads<MODE, H>()), (walk_blocks_per_cu
         probe_point<MODE>(A, x, y, side ? cidx + off : cidx - off);
       }
     }
-    if constexpr (MODE == KM_BSGSB) {  // the last pair of the group
-      if ((plive & 1u) && blk_match_rec(blk_load(A, pm), pm)) record_hit(A, cidx - poff, 4);
-      if ((plive & 2u) && blk_match_rec(blk_load(A, pp), pp)) record_hit(A, cidx + poff, 4);
-    }
-    if constexpr (MODE == KM_XPOINTB) {
-      if ((plive & 1u) && blk_match_rec(A.tblk[pm.x], pm)) record_hit(A, cidx - poff, 3);
-      if ((plive & 2u) && blk_match_rec(A.tblk[pp.x], pp)) record_hit(A, cidx + poff, 3);
+    if constexpr (DEFER) {  // the last pair of the group
+      if ((plive & 1u) && blk_match_rec(dload(pm), pm)) record_hit(A, cidx - poff, DKIND);
+      if ((plive & 2u) && blk_match_rec(dload(pp), pp)) record_hit(A, cidx + poff, DKIND);
     }
     // next centre C += T[H]  (keyhunt.cpp:3840-3855)
     {
