@@ -108,6 +108,11 @@ KH_HD void kh_blk_masks(uint32_t s0, uint32_t s1, uint32_t s2, uint32_t m[4]) {
 #ifndef KH_XPOINT_DEFER
 #define KH_XPOINT_DEFER 1
 #endif
+//   KH_FULL_GROUPS the xpoint deferred-probe walk skips the per-pair index-vs-job-end compares in
+//                groups that lie wholly inside the job for every lane of the wave (a uniform test)
+#ifndef KH_FULL_GROUPS
+#define KH_FULL_GROUPS 1
+#endif
 
 enum kh_walk_mode {
   KM_H160C = 0,   // hash160(02||X), hash160(03||X)          -l compress

@@ -573,6 +573,13 @@ __global__ void __launch_bounds__((walk_threads<MODE, H>()), (walk_blocks_per_cu
     uint4 pm = make_uint4(0u, 0u, 0u, 0u), pp = make_uint4(0u, 0u, 0u, 0u);  // DEFER: previous pair's probe records
     uint64_t poff = 0;
     uint32_t plive = 0;
+    // every point of this group, for every lane of the wave, lies inside the job (all but a job's
+    // last groups): the per-pair liveness test then needs no 64-bit compares (xpoint +0.9 %; the BSGS
+    // walk measured 0.2 % slower with it, so it keeps the compares)
+    bool wfull = false;
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (MODE == KM_XPOINTB && KH_FULL_GROUPS) wfull = !kh_any(cidx + H > A.n_points);
+#endif
     fe pre;
     scr_load(pre, scr, slot(H - 2));
 #pragma unroll 1
@@ -621,7 +628,10 @@ __global__ void __launch_bounds__((walk_threads<MODE, H>()), (walk_blocks_per_cu
         pm = drec(xm);
         pp = drec(xp);
         poff = off;
-        plive = (cidx - off < A.n_points ? 1u : 0u) | (i < H - 1 && cidx + off < A.n_points ? 2u : 0u);
+        if (wfull)
+          plive = i < H - 1 ? 3u : 1u;
+        else
+          plive = (cidx - off < A.n_points ? 1u : 0u) | (i < H - 1 && cidx + off < A.n_points ? 2u : 0u);
         continue;
       }
       if constexpr (MODE == KM_BSGS) {
