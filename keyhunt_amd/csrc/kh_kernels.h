@@ -113,6 +113,11 @@ KH_HD void kh_blk_masks(uint32_t s0, uint32_t s1, uint32_t s2, uint32_t m[4]) {
 #ifndef KH_FULL_GROUPS
 #define KH_FULL_GROUPS 1
 #endif
+//   KH_H160_BLK  -l compress hash160 scans with exact targets compile the blocked-filter probe alone
+//                (k_walk<KM_H160CB>), so the RIPEMD-160 steps that feed digest words 3..4 drop out
+#ifndef KH_H160_BLK
+#define KH_H160_BLK 1
+#endif
 
 enum kh_walk_mode {
   KM_H160C = 0,   // hash160(02||X), hash160(03||X)          -l compress
@@ -126,6 +131,7 @@ enum kh_walk_mode {
   KM_BUILDB = 8,  // baby-step build with the blocked layer-1 bloom
   KM_ETH = 9,     // Keccak-256(X||Y)[12..32): Ethereum address -> target bloom (-c eth)
   KM_XPOINTB = 10,  // KM_XPOINT with the blocked target filter, deferred probes (launch_walk picks it)
+  KM_H160CB = 11,   // KM_H160C with the blocked target filter only (launch_walk picks it)
   // flag on KM_H160C/U/B and KM_XPOINT: also probe the endomorphism images (beta*x, y) and
   // (beta^2*x, y), i.e. keys lambda*k and lambda^2*k (-e, keyhunt.cpp:3408-3440, 3476-3830)
   KM_ENDO = 16,

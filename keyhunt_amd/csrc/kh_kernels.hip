@@ -240,6 +240,20 @@ __device__ __forceinline__ void probe_eth(const walk_args &A, const fe &x, const
 template <int MODE>
 __device__ __forceinline__ void probe_point(const walk_args &A, const fe &x, const fe &y, uint64_t idx) {
   if (idx >= A.n_points) return;
+  if constexpr (MODE == KM_H160CB) {
+    // hash160(02||X), hash160(03||X) against the blocked target filter only: the filter reads digest
+    // words 0..2, so the RIPEMD-160 steps that feed only words 3..4 are dead code here
+    uint32_t hh[2][5];
+    hash160_comp2(x, hh[0], hh[1]);
+#pragma unroll 1
+    for (uint32_t k = 0; k < 2; k++) {
+      uint32_t h[5];
+#pragma unroll
+      for (int q = 0; q < 5; q++) h[q] = k ? hh[1][q] : hh[0][q];
+      if (tblk_probe(A, h)) record_hit(A, idx, k);
+    }
+    return;
+  }
   if constexpr (MODE == KM_ETH) {
     probe_eth(A, x, y, idx);
     return;
@@ -450,7 +464,8 @@ constexpr bool needs_y() {
 // 4 waves/SIMD even with a few spills; the hash160 modes prefer 3).
 template <int MODE>
 constexpr int walk_lb() {
-  return ((MODE & 15) == KM_H160C || (MODE & 15) == KM_H160U || (MODE & 15) == KM_H160B || (MODE & 15) == KM_ETH)
+  return ((MODE & 15) == KM_H160C || (MODE & 15) == KM_H160U || (MODE & 15) == KM_H160B || (MODE & 15) == KM_ETH ||
+          MODE == KM_H160CB)
              ? KH_WALK_LB_HASH
          : MODE == KM_DUMP                                          ? 2
                                                                     : KH_WALK_LB;
@@ -979,6 +994,7 @@ namespace kh {
 hipError_t launch_walk(int mode, const walk_args &A, hipStream_t st, int H) {
   dim3 block(256), grid((A.L + 255) / 256);
   if (KH_XPOINT_DEFER && mode == KM_XPOINT && A.tblk) mode = KM_XPOINTB;
+  if (KH_H160_BLK && mode == KM_H160C && A.tblk) mode = KM_H160CB;
   if (H == KH_WALK_HB) {
     constexpr int TB = walk_threads<KM_BSGSB, KH_WALK_HB>();
     switch (mode) {
@@ -989,6 +1005,7 @@ hipError_t launch_walk(int mode, const walk_args &A, hipStream_t st, int H) {
       case KM_XPOINT: hipLaunchKernelGGL((k_walk<KM_XPOINT, KH_WALK_HB>), grid, block, 0, st, A); break;
       case KM_XPOINTB: hipLaunchKernelGGL((k_walk<KM_XPOINTB, KH_WALK_HB>), grid, block, 0, st, A); break;
       case KM_H160C: hipLaunchKernelGGL((k_walk<KM_H160C, KH_WALK_HB>), grid, block, 0, st, A); break;
+      case KM_H160CB: hipLaunchKernelGGL((k_walk<KM_H160CB, KH_WALK_HB>), grid, block, 0, st, A); break;
       default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -1001,6 +1018,7 @@ hipError_t launch_walk(int mode, const walk_args &A, hipStream_t st, int H) {
 #endif
   switch (mode) {
     case KM_H160C: hipLaunchKernelGGL(k_walk<KM_H160C>, grid, block, 0, st, A); break;
+    case KM_H160CB: hipLaunchKernelGGL(k_walk<KM_H160CB>, grid, block, 0, st, A); break;
     case KM_H160U: hipLaunchKernelGGL(k_walk<KM_H160U>, grid, block, 0, st, A); break;
     case KM_H160B: hipLaunchKernelGGL(k_walk<KM_H160B>, grid, block, 0, st, A); break;
     case KM_XPOINT: hipLaunchKernelGGL(k_walk<KM_XPOINT>, grid, block, 0, st, A); break;
