@@ -17,7 +17,7 @@ continue the same lanes.  The table build (baby steps) is replicated per GPU and
 reported.  torch.distributed (gloo, CPU tensors) provides the barrier and the max over ranks; the
 engine owns the GPU through its own HIP stream, synchronised on both sides of the timed region.
 
-roofline: dominant kernel of each leg (the giant-step walk k_walk<7, 2048>; k_walk<0, 2048> and
+roofline: dominant kernel of each leg (the giant-step walk k_walk<7, 2048>; k_walk<11, 2048> and
 k_walk<10, 2048> for rmd160 / xpoint), from HIP events the engine records on its own stream around
 its launches.  The walks are bound by VALU issue, so "bound" is "valu":
 achieved = VALU wave-instructions per launch (rocprofv3 SQ_INSTS_VALU per point, committed under
@@ -273,7 +273,7 @@ def rmd160_leg(D: Dist, eng, args):
     # algorithmic HBM bytes ~0 per key: the 16-B target filter block is L2-resident
     return {"value": keys / T / 1e6, "ms_per_step": T / args.steps_rmd * 1e3,
             "points_per_s_in_kernel": pts / (ms / 1e3),
-            "roofline": walk_roofline("k_walk<0, 2048>", pts / la, ms / la, 0, la)}
+            "roofline": walk_roofline("k_walk<11, 2048>", pts / la, ms / la, 0, la)}
 
 
 def xpoint_leg(D: Dist, eng, args):
