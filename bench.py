@@ -3,17 +3,31 @@
 
 Metric (BASELINE.json): "Mkeys/s at 1/2/4/8 GPU (BSGS b125; addr b66); HBM GB/s fraction".
   primary   : -m bsgs -f tests/125.txt -b 125 -k 128  (configs[3]).  A step = one kh_bsgs_scan over
-              BASES consecutive bases of 2N keys (N = 2^44) for the puzzle-125 public key, i.e.
-              BASES x 32768 giant-step points probed against the 1.84 GB layer-1 bloom, plus the
-              host refinement of every first-level candidate.  Keys counted as the reference does
-              (2N per base, keyhunt.cpp:4883-4884 / 2871-2874).
-  secondary : -m rmd160 -f tests/66.rmd -b 66 -l compress (configs[1]).  A step = one 2^32-key
-              N_SEQUENTIAL_MAX chunk; keys counted x2 for -l compress (keyhunt.cpp:2889-2891).
+              B consecutive bases of 2N keys (N = 2^44) for the puzzle-125 public key, i.e.
+              B x 32768 giant-step points probed against the layer-1 filter, plus the second check of
+              every first-level candidate.  Keys counted as the reference does (2N per base,
+              keyhunt.cpp:4883-4884 / 2871-2874).
+  secondary : -m rmd160 -f tests/66.rmd -b 66 -l compress (configs[1]).  A step = C consecutive
+              2^32-key N_SEQUENTIAL_MAX chunks (one kh_scan each); keys counted x2 for -l compress
+              (keyhunt.cpp:2889-2891).
   tertiary  : -m xpoint -f tests/63.pub -b 63 (configs[2]), same chunks, one key per point.
   --config 5: the primary on -m bsgs -f tests/130.txt -b 130 -k 512 (configs[4]) instead.
+
+Sustained measurement (throughput runs of >= 60 s after warm-up): the batch of a step
+(B bases, C chunks) is sized from the last warm-up step so that the K timed steps last --seconds
+(primary, default 60) and --seconds-secondary (default 20) per address-family leg; the line reports
+the rate of the first and the last quarter of the timed steps, each with its kernel time per launch
+and the board's gfx clock sampled through amdsmi while they ran.
+
+Parity at full size: after each leg's timed loop (outside it), the same engine with the same tables
+scans the SURVEY.md 8c known-answer window of that workload and must find the reference's key
+("known_answer" per leg); bench.py exits 3 on a mismatch, after printing the line.
+
 Ranks split the keyspace (weak scaling, no collective on the data path): rank r walks its own
-contiguous run of BSGS base batches and of 2^32-key chunks (r*(W+K) + s), so consecutive calls
-continue the same lanes.  The table build (baby steps) is replicated per GPU and not timed; its time is
+contiguous region starting at r * span units (rank_origin), so consecutive steps continue the same
+lanes.  One process per GPU: more ranks than visible devices is refused unless --rehearse (ranks then
+share devices and the line says so); the line reports the distinct devices (PCI bus ids) the ranks
+used and every rank's own rate.  The table build is replicated per GPU and not timed; its time is
 reported.  torch.distributed (gloo, CPU tensors) provides the barrier and the max over ranks; the
 engine owns the GPU through its own HIP stream, synchronised on both sides of the timed region.
 
@@ -21,25 +35,30 @@ roofline: dominant kernel of each leg (the giant-step walk k_walk<7, 2048>; k_wa
 k_walk<10, 2048> for rmd160 / xpoint), from HIP events the engine records on its own stream around
 its launches.  The walks are bound by VALU issue, so "bound" is "valu":
 achieved = VALU wave-instructions per launch (rocprofv3 SQ_INSTS_VALU per point, committed under
-profiles/, x this run's points per launch) / mean launch time; peak = 1024 SIMDs x 2.4 GHz / 4
-cycles: one wave64 VALU instruction per SIMD per quad-cycle, the unit the SQ counters use and the
-measured issue cost of the 32-bit multiply-accumulate and carry ops the field math is made of
-(4.1-5.5 cycles at 4 waves/SIMD; only add/xor/mov issue in 2).  pmc_valu_issue_frac is the
-profiled dispatch's own occupancy of those issue slots, SQ_INSTS_VALU x 4 / (1024 x GRBM_GUI_ACTIVE
-/ 8), clock-free (the chip's clock under this load sits below 2.4 GHz: pmc_clock_ghz).  The HBM
-side is reported too ("hbm"): algorithmic bytes (BSGS: 64 B per giant point, one random line of the
-blocked layer 1; the reference layout's is 128 B) / launch time against 8 TB/s, and
-traffic = HBM bytes per launch from the PMC counters with the guide's gfx950 corrections
+profiles/, x this run's points per launch) / mean launch time.  Three ceilings:
+  peak / frac        1024 SIMDs x 2.4 GHz / 4 cycles: one wave64 VALU instruction per SIMD per
+                     quad-cycle (the SQ's issue unit and the cost of the multiply-add and carry ops);
+  peak_hw / frac_hw  1024 SIMDs x 2.4 GHz / 2 cycles: the guide's wave64 issue on a SIMD-32
+                     (MI355X_MICROARCH.md), which only full-rate ops reach;
+  frac_mix           the kernel's own class-weighted ceiling: sum over instruction classes of its
+                     dynamic count per point x the class's measured SIMD cycles (tools/ubench_cost.hip,
+                     in shader cycles), s_nop included (profiles/r03_valu_mix.json, tools/valu_mix.py),
+                     at 2.4 GHz; frac_mix_clock is the same at the profiled dispatch's own clock.
+The HBM side is reported too ("hbm"): algorithmic bytes (BSGS: 64 B per giant point, one random line
+of the blocked layer 1; the reference layout's is 128 B) / launch time against 8 TB/s,
+and traffic = HBM bytes per launch from the PMC counters with the guide's gfx950 corrections
 (tools/pmc_summary.py), or null.
-cpu_baseline: rank 0 at N=1 only, on every leg the reference binary built from its own sources
-(oracle/_ref/keyhunt, oracle/Makefile.ref; kind "reference") run for --cpu-seconds on the job's CPU
-share (cpu_threads), its own last stats line parsed.  BSGS skips the reference's baby-step build:
-the engine writes the -S table files in the reference's format (kh_bsgs_save, byte-identical) and the
-reference reads them (-S -6).
+cpu_baseline: rank 0 at N=1 only, on every leg the reference binary built from its own sources with
+its own optimisation flags (oracle/_ref/keyhunt, oracle/Makefile.ref; kind "reference") run for
+--cpu-seconds on the job's CPU share (cpu_threads), its own last stats line parsed; "all_cpus" scales
+its per-thread rate to every CPU of the host.  BSGS skips the reference's baby-step build: the engine
+writes the -S table files in the reference's format (kh_bsgs_save, byte-identical) and the reference
+reads them (-S -6).
 """
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import re
@@ -47,6 +66,7 @@ import shutil
 import subprocess
 import sys
 import tempfile
+import threading
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
@@ -56,23 +76,37 @@ METRIC = "Mkeys/s at 1/2/4/8 GPU (BSGS b125; addr b66); HBM GB/s fraction"
 HBM_PEAK_GBS = 8000.0
 ALGO_BYTES_PER_GIANT_POINT = {0: 128, 1: 64}      # by layer-1 layout (reference, blocked)
 WALK_KERNEL = {0: "k_walk<4, 2048>", 1: "k_walk<7, 2048>"}    # KM_BSGS, KM_BSGSB on 4096-point groups
-# 1024 SIMDs x 2.4 GHz / 4 cycles per wave64 VALU instruction (SQ quad-cycle; measured issue cost of
-# v_mad_u64_u32 / v_add_co / v_addc_co / v_bitop3 at 4 waves per SIMD: 4.1-5.5 cycles)
 SIMDS = 256 * 4
+NOMINAL_GHZ = 2.4
+# 1024 SIMDs x 2.4 GHz / 4 cycles per wave64 VALU instruction (SQ quad-cycle; measured issue cost of
+# v_mad_u64_u32 / v_add_co / v_addc_co / v_bitop3 at 4 waves per SIMD, profiles/r03_ubench_cost.txt)
 VALU_ISSUE_CYCLES = 4
-VALU_PEAK_GIPS = SIMDS * 2.4e9 / VALU_ISSUE_CYCLES / 1e9
+VALU_PEAK_GIPS = SIMDS * NOMINAL_GHZ / VALU_ISSUE_CYCLES
+VALU_PEAK_HW_GIPS = SIMDS * NOMINAL_GHZ / 2          # wave64 over 2 cycles on a SIMD-32 (guide)
 RANDOM16_CEILING_GPS = 51.36   # measured random 16-B nontemporal loads/s, 24 GB footprint (profiles/)
 PUZZLE125 = "0233709eb11e0d4439a729f21c2c443dedb727528229713f0065721ba8fa46f00e"
 PUZZLE130 = "03633cbe3ec02b9401c5effa144c5b4d22f87940259634858fc7e59b1c09937852"
-# BSGS workloads: --config 4 (the metric's, default) and 5 (BASELINE configs[4], k = 512)
+# BSGS workloads: --config 4 (the metric's, default) and 5 (BASELINE configs[4], k = 512), each with
+# the SURVEY.md 8c known-answer window (verified with the reference CLI) checked after the timed loop
 BSGS_CONFIGS = {
     4: {"pub": PUZZLE125, "bits": 125, "k": 128, "bases": 65536,
-        "workload": "-m bsgs -f tests/125.txt -b 125 -k 128", "data": "puzzle-125 public key (tests/125.txt)"},
+        "workload": "-m bsgs -f tests/125.txt -b 125 -k 128", "data": "puzzle-125 public key (tests/125.txt)",
+        "ka": (0x1c533b6bb7f0804e0995fe0000000000, 0x1c533b6bb7f0804e09963e0000000000,
+               0x1c533b6bb7f0804e09960225e44877ac)},
     5: {"pub": PUZZLE130, "bits": 130, "k": 512, "bases": 262144,
-        "workload": "-m bsgs -f tests/130.txt -b 130 -k 512", "data": "puzzle-130 public key (tests/130.txt)"},
+        "workload": "-m bsgs -f tests/130.txt -b 130 -k 512", "data": "puzzle-130 public key (tests/130.txt)",
+        "ka": (0x33e7665705359f04f28b8880000000000, 0x33e7665705359f04f28b8c80000000000,
+               0x33e7665705359f04f28b88cf897c603c9)},
 }
 PUZZLE66_RMD = "20d45a6a762535700ce9e0b216e31994335db8a5"
 PUZZLE63_X = 0x65ec2994b8cc0a20d40dd69edfe55ca32a54bcbbaa6b0ddcff36049301a54579  # tests/63.pub
+# known-answer windows of the address-family legs (reference CLI): (start, keys, key)
+KA_RMD160 = (0x2832ed74f2b000000, 1 << 24, 0x2832ed74f2b5e35ee)
+KA_XPOINT = (0x7cce5efdac000000, 1 << 24, 0x7cce5efdaccf6808)
+# per-rank regions (rank_origin): BSGS bases, address-family 2^32-key chunks
+RANK_SPAN_BASES = 1 << 40
+RANK_SPAN_CHUNKS = 1 << 24
+CHUNK = 1 << 32
 P = 2**256 - 2**32 - 977
 
 
@@ -89,6 +123,7 @@ class Dist:
         self.rank = int(os.environ.get("RANK", "0"))
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.local = int(os.environ.get("LOCAL_RANK", str(self.rank)))
+        self.local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(self.world)))
         self.pg = None
         if self.world > 1:
             import torch
@@ -115,17 +150,35 @@ class Dist:
         self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
         return float(t.item())
 
+    def gather(self, obj) -> list:
+        """Every rank's obj, in rank order (on every rank)."""
+        if self.world == 1:
+            return [obj]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj)
+        return out
+
     def close(self):
         if self.world > 1:
             self.dist.destroy_process_group()
 
 
-def rank_batch(rank: int, warmup: int, steps: int, s: int) -> int:
-    """Index of the batch rank `rank` walks at step s (warmup steps included, s < warmup + steps):
-    each rank owns one contiguous run of warmup + steps batches, so consecutive steps continue its
-    lanes (kh_bsgs_scan / kh_scan keep them across calls that follow on).  Runs of different ranks
-    are disjoint and together cover batches 0 .. world*(warmup+steps)-1 (tests/test_dist.py)."""
-    return rank * (warmup + steps) + s
+def rank_origin(rank: int, span: int) -> int:
+    """First unit (BSGS base / 2^32-key chunk, counted from the workload's start) of rank `rank`'s
+    region: each rank walks one contiguous run from there, warm-up and timed steps alike, so
+    consecutive calls continue its lanes (kh_bsgs_scan / kh_scan keep them across calls that follow
+    on).  Regions of different ranks are disjoint as long as a rank walks fewer than `span` units,
+    which the legs check (tests/test_dist.py)."""
+    return rank * span
+
+
+def batch_for(seconds: float, steps: int, unit_s: float, quantum: int, floor: int) -> int:
+    """Units per step so that `steps` steps of unit_s seconds per unit last about `seconds`: a
+    multiple of `quantum`, at least `floor`."""
+    if seconds <= 0 or unit_s <= 0 or steps <= 0:
+        return floor
+    want = seconds / steps / unit_s
+    return max(floor, int(-(-want // quantum)) * quantum)
 
 
 def launch_ranks(n: int, argv: list[str], script: str | None = None) -> int:
@@ -150,22 +203,149 @@ def launch_ranks(n: int, argv: list[str], script: str | None = None) -> int:
     return max(abs(rc) for rc in rcs)
 
 
-def timed(D: Dist, eng, warmup: int, steps: int, step_fn):
-    for s in range(warmup):
-        step_fn(s)
+def device_plan(world: int, local_rank: int, local_world: int, ndev: int, rehearse: bool) -> int:
+    """The device this rank uses: its local rank.  One process per GPU, so more local ranks than
+    visible devices is refused unless `rehearse` (ranks then share devices round-robin and the line
+    reports it: devices_used, rehearsal)."""
+    if ndev < 1:
+        raise SystemExit("bench.py: no GPU visible")
+    if local_world > ndev and not rehearse:
+        raise SystemExit(f"bench.py: {local_world} ranks on this node but only {ndev} visible GPU(s): one rank per "
+                         f"GPU (pass --rehearse to stack ranks on fewer devices; the line then says so)")
+    return local_rank % ndev
+
+
+def pci_bus_id(device: int) -> str | None:
+    """PCI bus id of HIP device `device`, from the HIP runtime the engine itself loaded."""
+    try:
+        path = None
+        with open("/proc/self/maps") as f:
+            for line in f:
+                if "libamdhip64" in line:
+                    path = line.split()[-1]
+                    break
+        hip = ctypes.CDLL(path or "libamdhip64.so")
+        buf = ctypes.create_string_buffer(64)
+        if hip.hipDeviceGetPCIBusId(buf, 64, device) != 0:
+            return None
+        return buf.value.decode().lower()
+    except Exception:
+        return None
+
+
+class ClockSampler:
+    """Samples the board's gfx clock (amdsmi, MHz) of the device with bus id `bdf` every `period`
+    seconds in a thread.  Board readings run a few % above the in-kernel clock (MI355X_MICROARCH.md,
+    DVFS give-back): a trend indicator beside the kernel times, not a cycle count."""
+
+    def __init__(self, bdf: str | None, period: float = 0.25):
+        self.samples: list[tuple[float, float]] = []
+        self.error = None
+        self._stop = threading.Event()
+        self._h = None
+        self._period = period
+        try:
+            import amdsmi
+            self._amdsmi = amdsmi
+            amdsmi.amdsmi_init()
+            for h in amdsmi.amdsmi_get_processor_handles():
+                b = str(amdsmi.amdsmi_get_gpu_device_bdf(h)).lower()
+                if bdf and (b == bdf or b.endswith(bdf.split(":", 1)[-1]) or bdf.endswith(b.split(":", 1)[-1])):
+                    self._h = h
+                    break
+            if self._h is None:
+                self.error = f"no amdsmi device with bus id {bdf}"
+        except Exception as e:  # amdsmi absent or not permitted: the line says why
+            self.error = f"amdsmi: {e!r}"[:200]
+        self._t = None
+
+    def _read(self) -> float | None:
+        a = self._amdsmi
+        try:
+            ci = a.amdsmi_get_clock_info(self._h, a.AmdSmiClkType.GFX)
+            v = ci.get("clk") if isinstance(ci, dict) else None
+            if v:
+                return float(v)
+        except Exception:
+            pass
+        m = a.amdsmi_get_gpu_metrics_info(self._h)
+        for key in ("current_gfxclk", "average_gfxclk_frequency"):
+            v = m.get(key)
+            if isinstance(v, (int, float)) and 0 < v < 10000:
+                return float(v)
+        v = m.get("current_gfxclks")
+        if isinstance(v, list):
+            vals = [x for x in v if isinstance(x, (int, float)) and 0 < x < 10000]
+            if vals:
+                return sum(vals) / len(vals)
+        return None
+
+    def _run(self):
+        while not self._stop.is_set():
+            try:
+                v = self._read()
+                if v:
+                    self.samples.append((time.perf_counter(), v))
+            except Exception as e:
+                self.error = f"amdsmi read: {e!r}"[:200]
+                return
+            self._stop.wait(self._period)
+
+    def start(self):
+        if self._h is not None:
+            self._t = threading.Thread(target=self._run, daemon=True)
+            self._t.start()
+        return self
+
+    def stop(self):
+        self._stop.set()
+        if self._t:
+            self._t.join(timeout=5)
+
+    def mean(self, t0: float, t1: float) -> float | None:
+        v = [c for t, c in self.samples if t0 <= t <= t1]
+        return sum(v) / len(v) if v else None
+
+
+def timed(D: Dist, eng, steps: int, step_fn, units_per_step: int, kind: int, clock: ClockSampler | None):
+    """K timed steps bracketed by barrier + synchronize; returns (max-over-ranks seconds, per-step
+    records (wall end, cumulative kernel ms and launches)) for the quarter analysis."""
     eng.synchronize()
     D.barrier()
     eng.kernel_time_reset()
+    recs = []
     t0 = time.perf_counter()
     for s in range(steps):
-        step_fn(warmup + s)
+        step_fn(s)
+        la, ms, _ = eng.kernel_time(kind)
+        recs.append((time.perf_counter(), ms, la))
     eng.synchronize()
     t1 = time.perf_counter()
     D.barrier()
-    return D.max(t1 - t0)
+    return D.max(t1 - t0), t0, t1, recs
 
 
-def bsgs_leg(D: Dist, eng, args):
+def quarters(t0: float, recs: list, units_per_step: int, keys_per_unit: float, clock: ClockSampler | None) -> dict | None:
+    """Rate of the first and the last quarter of the timed steps (keys/s from their wall time), their
+    kernel ms per launch, and the mean board clock while they ran."""
+    K = len(recs)
+    if K < 4:
+        return None
+    q = K // 4
+    out = {}
+    for name, a, b in (("first_quarter", 0, q), ("last_quarter", K - q, K)):
+        ts = t0 if a == 0 else recs[a - 1][0]
+        ms0, la0 = (0.0, 0) if a == 0 else (recs[a - 1][1], recs[a - 1][2])
+        te, ms1, la1 = recs[b - 1]
+        out[name] = {"steps": [a, b], "mkeys_per_s": (b - a) * units_per_step * keys_per_unit / (te - ts) / 1e6,
+                     "kernel_ms_per_launch": (ms1 - ms0) / max(1, la1 - la0),
+                     "board_gfxclk_mhz": clock.mean(ts, te) if clock else None}
+    f, l = out["first_quarter"], out["last_quarter"]
+    out["last_over_first"] = l["mkeys_per_s"] / f["mkeys_per_s"]
+    return out
+
+
+def bsgs_leg(D: Dist, eng, args, clock):
     import keyhunt_amd as K
     C = BSGS_CONFIGS[args.config]
     info = eng.bsgs_setup(1 << 44, C["k"], layer1=args.layer1)
@@ -176,19 +356,30 @@ def bsgs_leg(D: Dist, eng, args):
     q = decompress(C["pub"])
     eng.bsgs_set_targets([q])
     two_n = 2 * info.n
-    base0 = 1 << (C["bits"] - 1)
-    B = args.bases or C["bases"]
+    origin = (1 << (C["bits"] - 1)) + rank_origin(D.rank, RANK_SPAN_BASES) * two_n
+    B0 = args.bases or C["bases"]
+    walked = 0
 
-    # rank r walks its own contiguous run of batches, so consecutive steps continue its lanes
-    def step(s):
-        batch = rank_batch(D.rank, args.warmup, args.steps, s)
-        found = eng.bsgs_scan(base0 + batch * B * two_n, B)
-        assert not found  # puzzle 125's key lies far from the start of the range
+    def run(nb):
+        nonlocal walked
+        assert walked + nb <= RANK_SPAN_BASES, "rank region exhausted"
+        found = eng.bsgs_scan(origin + walked * two_n, nb)
+        walked += nb
+        assert not found  # puzzle 125's (130's) key lies far from the start of the range
 
-    T = timed(D, eng, args.warmup, args.steps, step)
+    last = 0.0
+    for s in range(args.warmup):
+        t = time.perf_counter()
+        run(B0)
+        last = time.perf_counter() - t
+    B = int(D.max(batch_for(args.seconds, args.steps, last / B0, B0, B0) if args.warmup else B0))
+    T, t0, _, recs = timed(D, eng, args.steps, lambda s: run(B), B, K.engine.TIME_BSGS, clock)
     la, ms, pts = eng.kernel_time(K.engine.TIME_BSGS)
+    my_pts_s = args.steps * B * info.cycles * 1024 / (recs[-1][0] - t0)
+    # known answer (outside the timed region, same engine and tables): SURVEY.md 8c
+    ka_lo, ka_hi, ka_key = C["ka"]
+    ka_found = eng.bsgs_scan(ka_lo, (ka_hi - ka_lo) // two_n)
     keys = D.world * args.steps * B * two_n
-    args.bases = B
     pts_launch = pts / la
     ms_launch = ms / la
     bpp = ALGO_BYTES_PER_GIANT_POINT[info.layer1_layout]
@@ -199,18 +390,32 @@ def bsgs_leg(D: Dist, eng, args):
     rand = {"achieved": pts_launch / (ms_launch / 1e3) / 1e9, "ceiling": RANDOM16_CEILING_GPS, "unit": "G loads/s",
             "frac": pts_launch / (ms_launch / 1e3) / 1e9 / RANDOM16_CEILING_GPS,
             "source": "profiles/r01l_random16B.txt"} if info.layer1_layout == 1 else None
-    res = {
+    return {
         "value": keys / T / 1e6,
         "random_access": rand,
         "ms_per_step": T / args.steps * 1e3,
+        "seconds_timed": T,
+        "bases_per_step": B,
         "giant_points_per_s": D.world * args.steps * B * info.cycles * 1024 / T,
+        "rank_giant_points_per_s": my_pts_s,
         "build_seconds": build_s,
         "candidates": eng.bsgs_candidates(),
         "info": info,
         "roofline": roof,
-        "q": q,
+        "sustained": quarters(t0, recs, B, two_n, clock),
+        "known_answer": {"window": f"{ka_lo:x}:{ka_hi:x}", "expected": f"{ka_key:x}",
+                         "found": [f"{k:x}" for _, k in ka_found], "match": [k for _, k in ka_found] == [ka_key]},
     }
-    return res
+
+
+def _valu_mix(kname: str) -> dict:
+    """The kernel's class-weighted VALU ceiling (profiles/r*_valu_mix.json, tools/valu_mix.py)."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "r*_valu_mix.json")), reverse=True):
+        d = json.load(open(f)).get(kname)
+        if d:
+            return dict(d, source=os.path.relpath(f, REPO))
+    return {}
 
 
 def walk_roofline(kname: str, pts_launch: float, ms_launch: float, algo_bytes_per_point: float, launches: int) -> dict:
@@ -220,17 +425,32 @@ def walk_roofline(kname: str, pts_launch: float, ms_launch: float, algo_bytes_pe
     d = pmc_entry(kname)
     secs = ms_launch / 1e3
     roof = {"bound": "valu", "achieved": None, "peak": VALU_PEAK_GIPS, "unit": "G VALU wave-instr/s", "frac": None,
+            "peak_hw": VALU_PEAK_HW_GIPS, "frac_hw": None, "frac_mix": None,
             "traffic": None, "kernel": kname, "launches": launches, "mean_launch_ms": ms_launch,
             "points_per_launch": pts_launch, "source": d.get("source")}
     if "valu_wave_instructions_per_dispatch" in d:
         wipp = d["valu_wave_instructions_per_dispatch"] / d["points_per_dispatch"]
         a = wipp * pts_launch / secs / 1e9
-        roof.update(achieved=a, frac=a / VALU_PEAK_GIPS, valu_wave_instructions_per_point=wipp,
-                    valu_lane_instructions_per_point=wipp * 64)
+        roof.update(achieved=a, frac=a / VALU_PEAK_GIPS, frac_hw=a / VALU_PEAK_HW_GIPS,
+                    valu_wave_instructions_per_point=wipp, valu_lane_instructions_per_point=wipp * 64)
         if d.get("valu_issue_frac"):
             # the profiled dispatch's issue-slot occupancy, in cycles (clock-free; DVFS moves the
             # clock between runs, so frac above is at the nominal 2.4 GHz)
             roof.update(pmc_valu_issue_frac=d["valu_issue_frac"], pmc_clock_ghz=d["effective_clock_ghz"])
+        for key in ("valu_dual_issue_frac", "wave_time_split", "valu_thread_cycles_per_instruction"):
+            if key in d:
+                roof["pmc_" + key] = d[key]
+    mix = _valu_mix(kname)
+    if mix.get("simd_cycles_per_point"):
+        # class-weighted ceiling: points/s if every SIMD issued this kernel's instruction mix back to
+        # back at the measured class costs (s_nop included), at 2.4 GHz and at the profiled clock
+        cyc = mix["simd_cycles_per_point"]
+        ceil_pts = SIMDS * NOMINAL_GHZ * 1e9 / cyc
+        got_pts = pts_launch / secs
+        roof.update(frac_mix=got_pts / ceil_pts, mix_simd_cycles_per_point=cyc,
+                    mix_ceiling_points_per_s=ceil_pts, mix_source=mix["source"])
+        if roof.get("pmc_clock_ghz"):
+            roof["frac_mix_clock"] = got_pts / (SIMDS * roof["pmc_clock_ghz"] * 1e9 / cyc)
     hbm = {"achieved": pts_launch * algo_bytes_per_point / secs / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "algorithmic_bytes_per_point": algo_bytes_per_point}
     hbm["frac"] = hbm["achieved"] / HBM_PEAK_GBS
@@ -256,44 +476,53 @@ def pmc_entry(kernel: str) -> dict:
     return {}
 
 
-def rmd160_leg(D: Dist, eng, args):
+def address_leg(D: Dist, eng, args, clock, mode: int, kname: str, keys_per_point: int, base0: int, ka):
+    """-m rmd160 -l compress / -m xpoint: steps of C chunks of 2^32 keys from the rank's region."""
+    import keyhunt_amd as K
+    kind = K.engine.TIME_ADDRESS if mode == K.KH_MODE_ADDRESS else K.engine.TIME_XPOINT
+    origin = base0 + rank_origin(D.rank, RANK_SPAN_CHUNKS) * CHUNK
+    walked = 0
+
+    def run(nc):
+        nonlocal walked
+        assert walked + nc <= RANK_SPAN_CHUNKS, "rank region exhausted"
+        for c in range(nc):
+            hits = eng.scan(origin + (walked + c) * CHUNK, CHUNK, mode, K.KH_SEARCH_COMPRESS)
+            assert not hits  # the puzzle keys lie far from the start of the range
+        walked += nc
+
+    last = 0.0
+    for s in range(args.warmup_rmd):
+        t = time.perf_counter()
+        run(1)
+        last = time.perf_counter() - t
+    C = int(D.max(batch_for(args.seconds_secondary, args.steps_rmd, last, 1, 1) if args.warmup_rmd else 1))
+    T, t0, _, recs = timed(D, eng, args.steps_rmd, lambda s: run(C), C, kind, clock)
+    la, ms, pts = eng.kernel_time(kind)
+    ka_lo, ka_n, ka_key = ka
+    ka_hits = eng.scan(ka_lo, ka_n, mode, K.KH_SEARCH_COMPRESS)
+    keys = D.world * args.steps_rmd * C * CHUNK * keys_per_point
+    return {"value": keys / T / 1e6, "ms_per_step": T / args.steps_rmd * 1e3, "seconds_timed": T,
+            "chunks_per_step": C, "steps": args.steps_rmd,
+            "points_per_s_in_kernel": pts / (ms / 1e3),
+            "roofline": walk_roofline(kname, pts / la, ms / la, 0, la),
+            "sustained": quarters(t0, recs, C, CHUNK * keys_per_point, clock),
+            "known_answer": {"window": f"{ka_lo:x}:{ka_lo + ka_n - 1:x}", "expected": f"{ka_key:x}",
+                             "found": [f"{h.key:x}" for h in ka_hits], "match": [h.key for h in ka_hits] == [ka_key]}}
+
+
+def rmd160_leg(D: Dist, eng, args, clock):
     import keyhunt_amd as K
     eng.set_targets([bytes.fromhex(PUZZLE66_RMD)], bloom_items=1)
-    chunk = 1 << 32
-    base0 = 1 << 65
-
-    def step(s):
-        c = rank_batch(D.rank, args.warmup_rmd, args.steps_rmd, s)
-        hits = eng.scan(base0 + c * chunk, chunk, K.KH_MODE_ADDRESS, K.KH_SEARCH_COMPRESS)
-        assert not hits
-
-    T = timed(D, eng, args.warmup_rmd, args.steps_rmd, step)
-    la, ms, pts = eng.kernel_time(K.engine.TIME_ADDRESS)
-    keys = D.world * args.steps_rmd * chunk * 2
     # algorithmic HBM bytes ~0 per key: the 16-B target filter block is L2-resident
-    return {"value": keys / T / 1e6, "ms_per_step": T / args.steps_rmd * 1e3,
-            "points_per_s_in_kernel": pts / (ms / 1e3),
-            "roofline": walk_roofline("k_walk<11, 2048>", pts / la, ms / la, 0, la)}
+    return address_leg(D, eng, args, clock, K.KH_MODE_ADDRESS, "k_walk<11, 2048>", 2, 1 << 65, KA_RMD160)
 
 
-def xpoint_leg(D: Dist, eng, args):
+def xpoint_leg(D: Dist, eng, args, clock):
     """-m xpoint -f tests/63.pub -b 63 (BASELINE configs[2]): X[0..20) probes, one key per point."""
     import keyhunt_amd as K
     eng.set_targets([PUZZLE63_X.to_bytes(32, "big")[:20]], bloom_items=1)
-    chunk = 1 << 32
-    base0 = 1 << 62
-
-    def step(s):
-        c = rank_batch(D.rank, args.warmup_rmd, args.steps_rmd, s)
-        hits = eng.scan(base0 + c * chunk, chunk, K.KH_MODE_XPOINT, K.KH_SEARCH_COMPRESS)
-        assert not hits
-
-    T = timed(D, eng, args.warmup_rmd, args.steps_rmd, step)
-    la, ms, pts = eng.kernel_time(K.engine.TIME_XPOINT)
-    keys = D.world * args.steps_rmd * chunk
-    return {"value": keys / T / 1e6, "ms_per_step": T / args.steps_rmd * 1e3,
-            "points_per_s_in_kernel": pts / (ms / 1e3),
-            "roofline": walk_roofline("k_walk<10, 2048>", pts / la, ms / la, 0, la)}
+    return address_leg(D, eng, args, clock, K.KH_MODE_XPOINT, "k_walk<10, 2048>", 1, 1 << 62, KA_XPOINT)
 
 
 def cpu_host() -> dict:
@@ -331,6 +560,7 @@ def cpu_threads() -> int:
 
 
 REF_BIN = os.path.join(REPO, "oracle", "_ref", "keyhunt")
+REF_FLAGS = os.path.join(REPO, "oracle", "_ref", "build_flags.txt")
 
 
 def run_reference(argv: list[str], files: list[str], seconds: float, setup=None):
@@ -377,8 +607,14 @@ def run_reference(argv: list[str], files: list[str], seconds: float, setup=None)
     if not last or last[1] == 0:
         return None
     keys, secs = last
+    host = cpu_host()
+    per_thread = keys / secs / 1e6 / thr
+    flags = open(REF_FLAGS).read().strip() if os.path.exists(REF_FLAGS) else None
     return {"value": keys / secs / 1e6, "unit": "Mkeys/s", "cores": thr, "kind": "reference",
-            "per_thread": keys / secs / 1e6 / thr, "host": cpu_host(),
+            "per_thread": per_thread, "host": host, "build_flags": flags,
+            "all_cpus": {"value": per_thread * (host.get("machine_cpus") or thr), "cpus": host.get("machine_cpus"),
+                         "how": "per-thread rate of this run x every CPU of the host (extrapolated: the job's share "
+                                "of the box is its GPU's 16 CPUs, so the other CPUs are not used)"},
             "sample": f"oracle/_ref/keyhunt {' '.join(argv)} -t {thr}: {keys} keys in {secs} s (the reference's "
                       f"own stats line, keys counted as it counts them)"}
 
@@ -419,12 +655,19 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", type=int, default=4, choices=sorted(BSGS_CONFIGS),
                     help="BSGS workload: 4 = b125 k128 (the metric's), 5 = b130 k512")
-    ap.add_argument("--bases", type=int, default=0, help="BSGS bases (of 2N keys) per step per GPU (0: per config)")
+    ap.add_argument("--bases", type=int, default=0,
+                    help="BSGS bases per warm-up step per GPU, and the quantum of the timed steps' batch (0: per config)")
+    ap.add_argument("--seconds", type=float, default=60.0,
+                    help="size the BSGS batch so that the timed steps last this long (0: --bases per step)")
+    ap.add_argument("--seconds-secondary", type=float, default=20.0,
+                    help="the same for each address-family leg (0: one 2^32-key chunk per step)")
     ap.add_argument("--steps-rmd", type=int, default=None)
     ap.add_argument("--warmup-rmd", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
+    ap.add_argument("--rehearse", action="store_true",
+                    help="allow more ranks than visible GPUs (ranks share devices; the line reports it)")
     ap.add_argument("--layer1", type=int, default=1, help="BSGS layer-1 layout: 1 blocked (default), 0 reference")
     args = ap.parse_args()
     args.steps_rmd = args.steps if args.steps_rmd is None else args.steps_rmd
@@ -434,12 +677,14 @@ def main():
     D = Dist()
     if args.gpus != D.world:
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={D.world}: launch one rank per GPU")
-    ndev = K.device_count()
-    # one process per GPU; on a box with fewer GPUs than ranks (rehearsal) ranks share devices
-    eng = K.Engine(D.local % max(1, ndev))
-    prim = bsgs_leg(D, eng, args)
-    sec = None if args.no_secondary else rmd160_leg(D, eng, args)
-    ter = None if args.no_secondary else xpoint_leg(D, eng, args)
+    dev = device_plan(D.world, D.local, D.local_world, K.device_count(), args.rehearse)
+    eng = K.Engine(dev)
+    bdf = pci_bus_id(dev)
+    clock = ClockSampler(bdf).start()
+    prim = bsgs_leg(D, eng, args, clock)
+    sec = None if args.no_secondary else rmd160_leg(D, eng, args, clock)
+    ter = None if args.no_secondary else xpoint_leg(D, eng, args, clock)
+    clock.stop()
     cpu_b = cpu_r = cpu_x = None
     if D.rank == 0 and D.world == 1 and not args.no_cpu_baseline:
         cpu_b = cpu_baseline_bsgs(eng, BSGS_CONFIGS[args.config], args.cpu_seconds)
@@ -447,9 +692,14 @@ def main():
             cpu_r = cpu_baseline_rmd160(args.cpu_seconds)
             cpu_x = cpu_baseline_xpoint(args.cpu_seconds)
     eng.close()
+    ranks = D.gather({"rank": D.rank, "host": os.uname().nodename, "device": dev, "pci_bus_id": bdf,
+                      "giant_points_per_s": prim["rank_giant_points_per_s"]})
+    kas = [prim["known_answer"]] + [x["known_answer"] for x in (sec, ter) if x]
+    ka_ok = D.sum(float(all(k["match"] for k in kas))) == D.world
     D.barrier()
     if D.rank == 0:
         info = prim["info"]
+        devices = sorted({(r["host"], r["pci_bus_id"] or f"hip{r['device']}") for r in ranks})
         line = {
             "metric": METRIC, "value": prim["value"], "unit": "Mkeys/s", "n_gpus": D.world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": prim["ms_per_step"], "higher_is_better": True, "scaling": "weak",
@@ -457,28 +707,40 @@ def main():
             "data": f"synthetic: {BSGS_CONFIGS[args.config]['data']}, sequential bases from 2^{BSGS_CONFIGS[args.config]['bits'] - 1}",
             "config": {"workload": BSGS_CONFIGS[args.config]["workload"], "n": info.n, "k": BSGS_CONFIGS[args.config]["k"], "m": info.m,
                        "layer1_layout": "blocked" if info.layer1_layout == 1 else "reference",
-                       "bases_per_step": args.bases, "giant_points_per_step": args.bases * info.cycles * 1024,
+                       "bases_per_step": prim["bases_per_step"],
+                       "giant_points_per_step": prim["bases_per_step"] * info.cycles * 1024,
                        "parallelism": f"keyspace split x{D.world} (no collective)"},
+            "devices_used": len(devices),
+            "rehearsal": len(devices) < D.world,
+            "ranks": ranks,
+            "seconds_timed": prim["seconds_timed"],
             "giant_points_per_s": prim["giant_points_per_s"],
             "build_seconds": prim["build_seconds"],
             "first_level_candidates": prim["candidates"],
+            "known_answer": prim["known_answer"],
+            "known_answers_all_ranks_match": ka_ok,
+            "sustained": prim["sustained"],
             "roofline": prim["roofline"],
             "random_access": prim["random_access"],
+            "clock_sampler": {"source": "amdsmi gfx clock of the rank-0 device", "samples": len(clock.samples),
+                              "error": clock.error},
             "cpu_baseline": cpu_b,
         }
-        if sec:
-            line["secondary"] = {"workload": "-m rmd160 -f tests/66.rmd -b 66 -l compress", "value": sec["value"],
-                                 "unit": "Mkeys/s", "ms_per_step": sec["ms_per_step"], "steps": args.steps_rmd,
-                                 "points_per_s_in_kernel": sec["points_per_s_in_kernel"],
-                                 "roofline": sec["roofline"], "cpu_baseline": cpu_r}
-        if ter:
-            line["tertiary"] = {"workload": "-m xpoint -f tests/63.pub -b 63", "value": ter["value"],
-                                "unit": "Mkeys/s", "ms_per_step": ter["ms_per_step"], "steps": args.steps_rmd,
-                                "points_per_s_in_kernel": ter["points_per_s_in_kernel"],
-                                "roofline": ter["roofline"], "cpu_baseline": cpu_x}
+        for key, leg, wl in (("secondary", sec, "-m rmd160 -f tests/66.rmd -b 66 -l compress"),
+                             ("tertiary", ter, "-m xpoint -f tests/63.pub -b 63")):
+            if leg:
+                line[key] = {"workload": wl, "value": leg["value"], "unit": "Mkeys/s", "ms_per_step": leg["ms_per_step"],
+                             "steps": leg["steps"], "chunks_per_step": leg["chunks_per_step"],
+                             "seconds_timed": leg["seconds_timed"],
+                             "points_per_s_in_kernel": leg["points_per_s_in_kernel"],
+                             "known_answer": leg["known_answer"], "sustained": leg["sustained"],
+                             "roofline": leg["roofline"],
+                             "cpu_baseline": cpu_r if key == "secondary" else cpu_x}
         json_out.write(json.dumps(line) + "\n")
         json_out.flush()
     D.close()
+    if not ka_ok:
+        sys.exit(3)
 
 
 if __name__ == "__main__":

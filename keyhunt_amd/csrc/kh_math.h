@@ -222,7 +222,12 @@ __device__ __forceinline__ uint64_t mad_acc(uint32_t a, uint32_t b, uint64_t acc
   uint64_t d, m, junk;
   asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(d), "=s"(m) : "v"(a), "v"(b), "v"(acc));
   uint32_t o;
+#ifdef KH_TIMING_EXTRA_NOPS
+  // timing-only build (same results): one more s_nop per carry count prices the hazard pads
+  asm("v_addc_co_u32 %0, %1, 0, %2, %3\n s_nop 1" : "=v"(o), "=s"(junk) : "v"(cnt), "s"(m));
+#else
   asm("v_addc_co_u32 %0, %1, 0, %2, %3" : "=v"(o), "=s"(junk) : "v"(cnt), "s"(m));
+#endif
   cnt = o;
   return d;
 }

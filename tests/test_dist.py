@@ -1,7 +1,8 @@
-"""The N>1 path of bench.py on CPU: world_size-2 gloo ranks agree on the barrier / max / sum, the
-partition bench.py actually uses (bench.rank_batch, called by all three legs) gives every rank a
-disjoint contiguous run of batches that together cover the keyspace prefix, and `bench.py --gpus N`
-started without WORLD_SIZE launches N ranks itself."""
+"""The N>1 path of bench.py on CPU: world_size-2 gloo ranks agree on the barrier / max / sum / gather,
+the partition bench.py actually uses (bench.rank_origin, called by all three legs) gives every rank a
+disjoint contiguous region, the step batch is sized for the sustained window, more ranks than GPUs
+is refused unless --rehearse, and `bench.py --gpus N` started without WORLD_SIZE launches N ranks
+itself."""
 import os
 import socket
 import subprocess
@@ -29,10 +30,11 @@ def _worker(rank, world, port, q):
     D.barrier()
     mx = D.max(float(rank + 1))
     sm = D.sum(float(rank + 1))
-    # the batches this rank walks for warmup 2 + steps 3, as bsgs_leg / rmd160_leg / xpoint_leg do
-    batches = [bench.rank_batch(D.rank, 2, 3, s) for s in range(5)]
+    # the region this rank walks (bsgs_leg / address_leg): units [origin, origin + span)
+    origin = bench.rank_origin(D.rank, bench.RANK_SPAN_BASES)
+    got = D.gather({"rank": D.rank, "origin": origin})
     D.close()
-    q.put((rank, mx, sm, batches))
+    q.put((rank, mx, sm, origin, got))
 
 
 @pytest.mark.parametrize("world", [2])
@@ -49,19 +51,48 @@ def test_gloo_barrier_max_and_partition(world):
     res.sort()
     assert all(r[1] == float(world) for r in res)
     assert all(r[2] == float(world * (world + 1) // 2) for r in res)
-    all_batches = [b for r in res for b in r[3]]
-    assert sorted(all_batches) == list(range(5 * world))  # disjoint and complete
+    origins = [r[3] for r in res]
+    assert origins == [r * (1 << 40) for r in range(world)]
+    assert all(r[4] == [{"rank": i, "origin": origins[i]} for i in range(world)] for r in res)  # gather, rank order
 
 
 @pytest.mark.parametrize("world", [1, 2, 8])
-@pytest.mark.parametrize("warmup,steps", [(0, 1), (2, 10), (5, 20)])
-def test_rank_batch_partition(world, warmup, steps):
+def test_rank_regions_disjoint_and_inside_the_range(world):
+    """Rank regions [origin, origin + span) of BSGS bases and 2^32-key chunks never overlap, and the
+    8-rank job stays inside each workload's -b range and short of its puzzle key (the legs assert
+    that nothing is found while timing)."""
     import bench
-    runs = [[bench.rank_batch(r, warmup, steps, s) for s in range(warmup + steps)] for r in range(world)]
-    for run in runs:  # contiguous, so consecutive steps continue the rank's lanes
-        assert run == list(range(run[0], run[0] + warmup + steps))
-    flat = sorted(b for run in runs for b in run)
-    assert flat == list(range(world * (warmup + steps)))  # disjoint and complete, warmup included
+    for span, unit_keys, lo, key in ((bench.RANK_SPAN_BASES, 2 << 44, 1 << 124, 0x1c533b6bb7f0804e09960225e44877ac),
+                                     (bench.RANK_SPAN_BASES, 2 << 44, 1 << 129, 0x33e7665705359f04f28b88cf897c603c9),
+                                     (bench.RANK_SPAN_CHUNKS, 1 << 32, 1 << 65, 0x2832ed74f2b5e35ee),
+                                     (bench.RANK_SPAN_CHUNKS, 1 << 32, 1 << 62, 0x7cce5efdaccf6808)):
+        regions = sorted((bench.rank_origin(r, span), bench.rank_origin(r, span) + span) for r in range(world))
+        assert all(a[1] <= b[0] for a, b in zip(regions, regions[1:]))
+        assert lo + regions[-1][1] * unit_keys <= key < 2 * lo
+
+
+@pytest.mark.parametrize("seconds,steps,unit_s,quantum,expect", [
+    (60, 10, 56.5e-3 / 65536, 65536, 65536 * 107),   # BSGS: 10 steps of ~6 s
+    (60, 20, 56.5e-3 / 65536, 65536, 65536 * 54),    # the driver's --steps 20
+    (20, 10, 0.57, 1, 4), (20, 10, 0.089, 1, 23),    # rmd160 / xpoint chunks
+    (0, 10, 0.57, 1, 1), (60, 10, 0.0, 65536, 65536)])
+def test_batch_for_sizes_the_sustained_window(seconds, steps, unit_s, quantum, expect):
+    import bench
+    b = bench.batch_for(seconds, steps, unit_s, quantum, quantum)
+    assert b == expect and b % quantum == 0
+    if seconds and unit_s:
+        assert b * steps * unit_s >= seconds * 0.999
+
+
+def test_more_ranks_than_gpus_is_refused_unless_rehearsal():
+    import bench
+    assert [bench.device_plan(8, r, 8, 8, False) for r in range(8)] == list(range(8))
+    with pytest.raises(SystemExit, match="only 1 visible GPU"):
+        bench.device_plan(8, 3, 8, 1, False)
+    assert bench.device_plan(8, 3, 8, 1, True) == 0
+    assert bench.device_plan(4, 3, 4, 2, True) == 1
+    with pytest.raises(SystemExit, match="no GPU visible"):
+        bench.device_plan(1, 0, 1, 0, True)
 
 
 def test_bench_gpus_flag_must_match_world_size():

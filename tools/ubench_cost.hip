@@ -1,0 +1,198 @@
+// ubench_cost.hip -- gfx950 VALU issue cost per instruction class in SHADER CYCLES (development
+// tool for the class-weighted roofline, bench.py "frac_mix").  tools/ubench_lat.hip priced the
+// classes from wall time at a nominal 2.4 GHz, which folds the chip's clock into every figure; here
+// every wave stamps s_memtime (shader clock) around its loop, and the host also derives the clock
+// from s_memtime / s_memrealtime (100 MHz), so the table is clock-free.
+//
+// Each pattern is one asm statement of 32 wave-instructions (s_nop included where the pattern has
+// them) per loop trip.  Printed per pattern and waves/SIMD (1, 2, 4, 8): SIMD cycles per
+// wave-instruction = median over waves of (delta s_memtime) / (trips x 32) / (waves per SIMD),
+// i.e. the per-SIMD cost when W waves share it, and the in-kernel clock.
+//
+// build: hipcc --offload-arch=gfx950 -O3 tools/ubench_cost.hip -o tools/ubench_cost
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include <algorithm>
+#include <vector>
+
+#define TRIPS 1024
+#define R2(x) x x
+#define R4(x) R2(x) R2(x)
+#define R8(x) R4(x) R4(x)
+
+struct stamp {
+  uint64_t t0, t1, r0, r1;
+};
+
+template <int P>
+__global__ __launch_bounds__(256) void k_pat(stamp *out, uint32_t seed) {
+  const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+  uint64_t x0 = t * 3 + seed, x1 = t * 5, x2 = t * 7, x3 = t * 11;
+  uint32_t a = t * 2654435761u + seed, b = a ^ 0x5bd1e995u, u0 = t, u1 = t + 1, u2 = t + 2, u3 = t + 3;
+  uint64_t s0 = seed, s1 = seed + 1, s2 = seed + 2, s3 = seed + 3;
+  __syncthreads();
+  const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+  for (int it = 0; it < TRIPS; it++) {
+    // --- 64-bit multiply-add and the product-scanning carry count
+    if (P == 0)  // 4 independent accumulate chains, carry-outs into one SGPR pair
+      asm volatile(R8("v_mad_u64_u32 %0, %4, %5, %6, %0\n v_mad_u64_u32 %1, %4, %5, %6, %1\n"
+                      "v_mad_u64_u32 %2, %4, %5, %6, %2\n v_mad_u64_u32 %3, %4, %5, %6, %3\n")
+                   : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3), "=s"(s0)
+                   : "v"(a), "v"(b));
+    if (P == 1)  // column as hipcc emits it around single-instruction asm: mad, s_nop 0, addc, s_nop 0
+      asm volatile(R8("v_mad_u64_u32 %0, %2, %4, %5, %0\n s_nop 0\n v_addc_co_u32 %1, %3, 0, %1, %2\n s_nop 0\n")
+                   : "+v"(x0), "+v"(u0), "=s"(s0), "=s"(s1)
+                   : "v"(a), "v"(b));
+    if (P == 2)  // the same 16 mad + 16 addc with the hazards covered by scheduling (no s_nop):
+                 // each count reads a mask written two instructions earlier
+      asm volatile(R4("v_mad_u64_u32 %0, %2, %6, %7, %0\n v_mad_u64_u32 %0, %3, %6, %7, %0\n"
+                      "v_addc_co_u32 %1, %5, 0, %1, %2\n v_mad_u64_u32 %0, %4, %6, %7, %0\n"
+                      "v_addc_co_u32 %1, %5, 0, %1, %3\n v_mad_u64_u32 %0, %2, %6, %7, %0\n"
+                      "v_addc_co_u32 %1, %5, 0, %1, %4\n v_addc_co_u32 %1, %5, 0, %1, %2\n")
+                   : "+v"(x0), "+v"(u0), "=s"(s0), "=s"(s1), "=s"(s2), "=s"(s3)
+                   : "v"(a), "v"(b));
+    if (P == 3)  // VCC carry chain as emitted: v_addc_co_u32_e32, s_nop 1, ... (16 + 16 nops)
+      asm volatile(R8("v_add_co_u32_e32 %0, vcc, %4, %0\n s_nop 1\n v_addc_co_u32_e32 %1, vcc, %4, %1, vcc\n s_nop 1\n")
+                   : "+v"(u0), "+v"(u1), "+v"(u2), "+v"(u3) : "v"(a) : "vcc");
+    if (P == 4)  // add/addc pairs of 4 independent chains through 4 SGPR pairs, no s_nop needed
+      asm volatile(R4("v_add_co_u32 %0, %4, %0, %8\n v_add_co_u32 %1, %5, %1, %8\n"
+                      "v_add_co_u32 %2, %6, %2, %8\n v_addc_co_u32 %0, %4, %0, %8, %4\n"
+                      "v_add_co_u32 %3, %7, %3, %8\n v_addc_co_u32 %1, %5, %1, %8, %5\n"
+                      "v_addc_co_u32 %2, %6, %2, %8, %6\n v_addc_co_u32 %3, %7, %3, %8, %7\n")
+                   : "+v"(u0), "+v"(u1), "+v"(u2), "+v"(u3), "=s"(s0), "=s"(s1), "=s"(s2), "=s"(s3)
+                   : "v"(a));
+    // --- full-rate candidates
+    if (P == 5)
+      asm volatile(R8("v_mov_b32 %0, %4\n v_mov_b32 %1, %4\n v_mov_b32 %2, %4\n v_mov_b32 %3, %4\n")
+                   : "=v"(u0), "=v"(u1), "=v"(u2), "=v"(u3) : "v"(a));
+    if (P == 6)
+      asm volatile(R8("v_add_u32 %0, %0, %4\n v_add_u32 %1, %1, %4\n v_add_u32 %2, %2, %4\n v_add_u32 %3, %3, %4\n")
+                   : "+v"(u0), "+v"(u1), "+v"(u2), "+v"(u3) : "v"(a));
+    if (P == 7)
+      asm volatile(R8("v_and_b32 %0, %4, %0\n v_and_b32 %1, %4, %1\n v_and_b32 %2, %4, %2\n v_and_b32 %3, %4, %3\n")
+                   : "+v"(u0), "+v"(u1), "+v"(u2), "+v"(u3) : "v"(a));
+    if (P == 8)
+      asm volatile(R8("v_bitop3_b32 %0, %0, %4, %1 bitop3:0x96\n v_bitop3_b32 %1, %1, %4, %2 bitop3:0x96\n"
+                      "v_bitop3_b32 %2, %2, %4, %3 bitop3:0x96\n v_bitop3_b32 %3, %3, %4, %0 bitop3:0x96\n")
+                   : "+v"(u0), "+v"(u1), "+v"(u2), "+v"(u3) : "v"(a));
+    if (P == 9)
+      asm volatile(R8("v_alignbit_b32 %0, %0, %0, 7\n v_alignbit_b32 %1, %1, %1, 7\n v_alignbit_b32 %2, %2, %2, 7\n"
+                      "v_alignbit_b32 %3, %3, %3, 7\n")
+                   : "+v"(u0), "+v"(u1), "+v"(u2), "+v"(u3));
+    if (P == 10)
+      asm volatile(R8("v_add3_u32 %0, %0, %4, %1\n v_add3_u32 %1, %1, %4, %2\n v_add3_u32 %2, %2, %4, %3\n"
+                      "v_add3_u32 %3, %3, %4, %0\n")
+                   : "+v"(u0), "+v"(u1), "+v"(u2), "+v"(u3) : "v"(a));
+    if (P == 11)
+      asm volatile(R8("v_lshrrev_b32 %0, 3, %0\n v_lshrrev_b32 %1, 3, %1\n v_lshrrev_b32 %2, 3, %2\n v_lshrrev_b32 %3, 3, %3\n")
+                   : "+v"(u0), "+v"(u1), "+v"(u2), "+v"(u3));
+    if (P == 12)
+      asm volatile(R8("v_pk_lshlrev_b16 %0, %4, %0\n v_pk_lshlrev_b16 %1, %4, %1\n v_pk_lshlrev_b16 %2, %4, %2\n"
+                      "v_pk_lshlrev_b16 %3, %4, %3\n")
+                   : "+v"(u0), "+v"(u1), "+v"(u2), "+v"(u3) : "v"(a));
+    if (P == 13)
+      asm volatile(R8("v_perm_b32 %0, %0, %4, %1\n v_perm_b32 %1, %1, %4, %2\n v_perm_b32 %2, %2, %4, %3\n"
+                      "v_perm_b32 %3, %3, %4, %0\n")
+                   : "+v"(u0), "+v"(u1), "+v"(u2), "+v"(u3) : "v"(a));
+    // --- compares, selects, carries to VCC
+    if (P == 14)
+      asm volatile(R8("v_cmp_eq_u32_e32 vcc, %0, %4\n v_cmp_eq_u32_e32 vcc, %1, %4\n v_cmp_eq_u32_e32 vcc, %2, %4\n"
+                      "v_cmp_eq_u32_e32 vcc, %3, %4\n")
+                   : "+v"(u0), "+v"(u1), "+v"(u2), "+v"(u3) : "v"(a) : "vcc");
+    if (P == 15)
+      asm volatile(R8("v_cndmask_b32_e64 %0, 0, 1, %4\n v_cndmask_b32_e64 %1, 0, 1, %4\n v_cndmask_b32_e64 %2, 0, 1, %4\n"
+                      "v_cndmask_b32_e64 %3, 0, 1, %4\n")
+                   : "=v"(u0), "=v"(u1), "=v"(u2), "=v"(u3) : "s"(s0));
+    if (P == 16)  // independent adds writing VCC
+      asm volatile(R8("v_add_co_u32_e32 %0, vcc, %4, %0\n v_add_co_u32_e32 %1, vcc, %4, %1\n"
+                      "v_add_co_u32_e32 %2, vcc, %4, %2\n v_add_co_u32_e32 %3, vcc, %4, %3\n")
+                   : "+v"(u0), "+v"(u1), "+v"(u2), "+v"(u3) : "v"(a) : "vcc");
+    // --- 64-bit ALU
+    if (P == 17)
+      asm volatile(R8("v_lshrrev_b64 %0, 1, %0\n v_lshrrev_b64 %1, 1, %1\n v_lshrrev_b64 %2, 1, %2\n v_lshrrev_b64 %3, 1, %3\n")
+                   : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3));
+    if (P == 18)
+      asm volatile(R8("v_lshl_add_u64 %0, %0, 0, %1\n v_lshl_add_u64 %1, %1, 0, %2\n v_lshl_add_u64 %2, %2, 0, %3\n"
+                      "v_lshl_add_u64 %3, %3, 0, %0\n")
+                   : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3));
+    if (P == 19)
+      asm volatile(R8("v_mov_b64 %0, %1\n v_mov_b64 %1, %2\n v_mov_b64 %2, %3\n v_mov_b64 %3, %0\n")
+                   : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3));
+    if (P == 20)
+      asm volatile(R8("v_mul_lo_u32 %0, %0, %4\n v_mul_hi_u32 %1, %1, %4\n v_mul_lo_u32 %2, %2, %4\n v_mul_hi_u32 %3, %3, %4\n")
+                   : "+v"(u0), "+v"(u1), "+v"(u2), "+v"(u3) : "v"(a));
+    // --- s_nop and mixes
+    if (P == 21)  // s_nop 0 only
+      asm volatile(R8(R4("s_nop 0\n")));
+    if (P == 22)  // 16 v_add_u32 + 16 s_nop 0
+      asm volatile(R8("v_add_u32 %0, %0, %4\n s_nop 0\n v_add_u32 %1, %1, %4\n s_nop 0\n")
+                   : "+v"(u0), "+v"(u1), "+v"(u2), "+v"(u3) : "v"(a));
+    if (P == 23)  // 16 independent mads + 16 s_nop 0 (nops that cover no hazard)
+      asm volatile(R8("v_mad_u64_u32 %0, %4, %5, %6, %0\n s_nop 0\n v_mad_u64_u32 %1, %4, %5, %6, %1\n s_nop 0\n")
+                   : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3), "=s"(s0)
+                   : "v"(a), "v"(b));
+    if (P == 24)  // 16 mads + 16 v_mov (the product-scanning column shift), interleaved
+      asm volatile(R8("v_mad_u64_u32 %0, %4, %5, %6, %0\n v_mov_b32 %7, %5\n v_mad_u64_u32 %1, %4, %5, %6, %1\n"
+                      "v_mov_b32 %8, %6\n")
+                   : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3), "=s"(s0), "+v"(a), "+v"(b), "=v"(u0), "=v"(u1));
+  }
+  const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+  if ((threadIdx.x & 63) == 0) {
+    stamp s;
+    s.t0 = t0;
+    s.t1 = t1 + (x0 ^ x1 ^ x2 ^ x3 ^ u0 ^ u1 ^ u2 ^ u3 ^ s0 ^ s1 ^ s2 ^ s3 ^ a ^ b) * 0;  // keep results live
+    s.r0 = r0;
+    s.r1 = r1;
+    out[t >> 6] = s;
+  }
+}
+
+typedef void (*kfn)(stamp *, uint32_t);
+#define K(n) k_pat<n>
+static const kfn kernels[] = {K(0),  K(1),  K(2),  K(3),  K(4),  K(5),  K(6),  K(7),  K(8),  K(9),  K(10), K(11), K(12),
+                              K(13), K(14), K(15), K(16), K(17), K(18), K(19), K(20), K(21), K(22), K(23), K(24)};
+static const char *names[] = {
+    "mad_u64_u32 acc, 4 chains",      "mad,nop,addc,nop (as hipcc)",  "mad+addc, hazards scheduled", "addc_e32 vcc chain + s_nop 1",
+    "add_co/addc, 4 sgpr chains",     "v_mov_b32",                    "v_add_u32",                   "v_and_b32",
+    "v_bitop3_b32",                   "v_alignbit_b32",               "v_add3_u32",                  "v_lshrrev_b32",
+    "v_pk_lshlrev_b16",               "v_perm_b32",                   "v_cmp_eq_u32 (vcc)",          "v_cndmask_b32_e64 (sgpr)",
+    "v_add_co_u32_e32 (vcc) indep",   "v_lshrrev_b64",                "v_lshl_add_u64",              "v_mov_b64",
+    "v_mul_lo/hi_u32",                "s_nop 0 only",                 "v_add_u32 + s_nop 0",         "mad + s_nop 0 (no hazard)",
+    "mad + v_mov interleaved"};
+
+int main() {
+  const int NP = sizeof(kernels) / sizeof(kernels[0]);
+  const int waves_per_simd[] = {1, 2, 4, 8};
+  stamp *d;
+  const int max_blocks = 256 * 8;
+  (void)hipMalloc(&d, sizeof(stamp) * max_blocks * 4);
+  std::vector<stamp> h(max_blocks * 4);
+  printf("%-32s %s\n", "pattern (32 instr per trip)", "SIMD cycles per wave-instruction at W waves/SIMD [in-kernel GHz]");
+  for (int p = 0; p < NP; p++) {
+    printf("%-32s", names[p]);
+    for (int w : waves_per_simd) {
+      const int blocks = 256 * w;  // 256 CUs x w blocks of 4 waves: w waves per SIMD
+      double cyc = 0, ghz = 0;
+      for (int rep = 0; rep < 2; rep++) {  // the first launch warms the clock
+        hipLaunchKernelGGL(kernels[p], dim3(blocks), dim3(256), 0, 0, d, 1u);
+        (void)hipDeviceSynchronize();
+        (void)hipMemcpy(h.data(), d, sizeof(stamp) * blocks * 4, hipMemcpyDeviceToHost);
+        std::vector<double> c, g;
+        for (int i = 0; i < blocks * 4; i++) {
+          const double dt = (double)(h[i].t1 - h[i].t0), dr = (double)(h[i].r1 - h[i].r0);
+          c.push_back(dt / (TRIPS * 32.0) / w);
+          if (dr > 0) g.push_back(dt / dr * 0.1);  // s_memrealtime ticks at 100 MHz
+        }
+        std::sort(c.begin(), c.end());
+        std::sort(g.begin(), g.end());
+        cyc = c[c.size() / 2];
+        ghz = g.empty() ? 0 : g[g.size() / 2];
+      }
+      printf("  W%d %5.2f [%.2f]", w, cyc, ghz);
+    }
+    printf("\n");
+  }
+  return 0;
+}
