@@ -49,7 +49,7 @@ of the blocked layer 1; the reference layout's is 128 B) / launch 
 and traffic = HBM bytes per launch from the PMC counters with the guide's gfx950 corrections
 (tools/pmc_summary.py), or null.
 cpu_baseline: rank 0 at N=1 only, on every leg the reference binary built from its own sources with
-its own optimisation flags (oracle/_ref/keyhunt, oracle/Makefile.ref; kind "reference") run for
+its own optimisation flags (oracle/_ref/keyhunt_fast, oracle/Makefile.ref; kind "reference") run for
 --cpu-seconds on the job's CPU share (cpu_threads), its own last stats line parsed; "all_cpus" scales
 its per-thread rate to every CPU of the host.  BSGS skips the reference's baby-step build: the engine
 writes the -S table files in the reference's format (kh_bsgs_save, byte-identical) and the reference
@@ -559,7 +559,10 @@ def cpu_threads() -> int:
     return max(1, min(aff, int(share))) if share.isdigit() and int(share) > 0 else max(1, aff)
 
 
-REF_BIN = os.path.join(REPO, "oracle", "_ref", "keyhunt")
+# the reference CLI at its own optimisation level (oracle/Makefile.ref keyhunt_fast); the -O3 build the
+# fixtures come from is the fallback
+REF_BIN = next((p for p in (os.path.join(REPO, "oracle", "_ref", b) for b in ("keyhunt_fast", "keyhunt"))
+                if os.path.exists(p)), os.path.join(REPO, "oracle", "_ref", "keyhunt"))
 REF_FLAGS = os.path.join(REPO, "oracle", "_ref", "build_flags.txt")
 
 
@@ -609,13 +612,14 @@ def run_reference(argv: list[str], files: list[str], seconds: float, setup=None)
     keys, secs = last
     host = cpu_host()
     per_thread = keys / secs / 1e6 / thr
-    flags = open(REF_FLAGS).read().strip() if os.path.exists(REF_FLAGS) else None
+    flags = (open(REF_FLAGS).read().strip() if os.path.exists(REF_FLAGS) and REF_BIN.endswith("_fast")
+             else "oracle/_ref/keyhunt: g++ -m64 -march=x86-64-v3 -mssse3 -O3 (the fixtures' build)")
     return {"value": keys / secs / 1e6, "unit": "Mkeys/s", "cores": thr, "kind": "reference",
             "per_thread": per_thread, "host": host, "build_flags": flags,
             "all_cpus": {"value": per_thread * (host.get("machine_cpus") or thr), "cpus": host.get("machine_cpus"),
                          "how": "per-thread rate of this run x every CPU of the host (extrapolated: the job's share "
                                 "of the box is its GPU's 16 CPUs, so the other CPUs are not used)"},
-            "sample": f"oracle/_ref/keyhunt {' '.join(argv)} -t {thr}: {keys} keys in {secs} s (the reference's "
+            "sample": f"oracle/_ref/{os.path.basename(REF_BIN)} {' '.join(argv)} -t {thr}: {keys} keys in {secs} s (the reference's "
                       f"own stats line, keys counted as it counts them)"}
 
 

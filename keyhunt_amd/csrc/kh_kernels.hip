@@ -138,6 +138,7 @@ __device__ __forceinline__ void blk_insert(uint8_t *__restrict__ bf_shard, const
 }
 
 __device__ __forceinline__ void record_hit(const walk_args &A, uint64_t idx, uint32_t kind) {
+  KH_RARE_MARK();
   uint32_t slot = atomicAdd(A.hit_count, 1u);
   if (slot < A.hit_cap) {
     A.hits[slot].idx = idx;

@@ -103,6 +103,14 @@ KH_HD void fe_canon(fe &r) {
   if (fe_geq_p(r)) fe_sub_p(r);
 }
 
+// KH_ISA_MARKS (analysis builds only, tools/valu_mix.py): every rarely executed fix-up block carries
+// an empty asm statement whose comment marks it in the ISA listing
+#if defined(__HIP_DEVICE_COMPILE__) && defined(KH_ISA_MARKS)
+#define KH_RARE_MARK() asm volatile(";@kh_rare")
+#else
+#define KH_RARE_MARK() ((void)0)
+#endif
+
 #if defined(__HIP_DEVICE_COMPILE__)
 // true iff `v` holds on any lane of the wave: a wave-uniform branch around a rarely needed fix-up
 // (a carry rippling past limb 1, a value in [p, 2^256)).  When no lane needs it the wave jumps
@@ -122,6 +130,7 @@ KH_HD void fe_add(fe &r, const fe &a, const fe &b) {
   r.d[0] = addc(r.d[0], c ? 0x3D1u : 0u, 0, c1);
   r.d[1] = addc(r.d[1], c, c1, c1);
   if (kh_any(c1 != 0 || r.d[7] == 0xFFFFFFFFu)) {
+    KH_RARE_MARK();
 #pragma unroll
     for (int i = 2; i < 8; i++) r.d[i] = addc(r.d[i], 0, c1, c1);
     fe_canon(r);
@@ -153,6 +162,7 @@ KH_HD void fe_sub(fe &r, const fe &a, const fe &b) {
     r.d[0] = subb(r.d[0], br ? 0x3D1u : 0u, 0, b2);
     r.d[1] = subb(r.d[1], br, b2, b2);
     if (kh_any(b2 != 0)) {
+      KH_RARE_MARK();
 #pragma unroll
       for (int i = 2; i < 8; i++) r.d[i] = subb(r.d[i], 0, b2, b2);
     }
@@ -202,6 +212,7 @@ KH_HD void fe_reduce512_gen(fe &r, const uint32_t t[16]) {
 #pragma unroll
   for (int i = 3; i < 8; i++) r.d[i] = u[i];
   if (kh_any(cc != 0 || r.d[7] == 0xFFFFFFFFu)) {
+    KH_RARE_MARK();
 #pragma unroll
     for (int i = 3; i < 8; i++) r.d[i] = addc(r.d[i], 0, cc, cc);
     if (cc) fe_sub_p(r);
@@ -247,6 +258,11 @@ __device__ __forceinline__ uint64_t mad_nc(uint32_t a, uint32_t b, uint64_t acc)
 #ifndef KH_RED2
 #define KH_RED2 1
 #endif
+// KH_COLS: fe_mul / fe_sqr columns as one scheduled asm statement each (kh_cols.h, tools/gen_cols.py)
+#ifndef KH_COLS
+#define KH_COLS 1
+#endif
+#include "kh_cols.h"
 
 #if defined(__HIP_DEVICE_COMPILE__)
 // a*b + c with b wave-uniform (an SGPR); m = the lane mask of the sum's 65th bit
@@ -303,6 +319,7 @@ KH_HD void fe_reduce512(fe &r, const uint32_t t[16]) {
     if ((m0 | m1 | m2 | m3 | m4 | m5 | m6 | m7 | m8) != 0 || kh_any((R[9] | c2) != 0 || r.d[7] == 0xFFFFFFFFu)) {
       // rare: put back the 2^64 each overflowing V_j / W_i lost (limb j+2 / i+2; lane bits of
       // the masks), then the second fold the long way from R: h = R8 + R9 2^32 < 2^34
+      KH_RARE_MARK();
       const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
       const uint64_t ms[8] = {m0, m1, m2, m3, m4, m5, m6, m7};
       uint32_t cc = 0;
@@ -331,6 +348,11 @@ KH_HD void fe_reduce512(fe &r, const uint32_t t[16]) {
 KH_HD void fe_mul(fe &r, const fe &a, const fe &b) {
   uint32_t t[16];
 #if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (KH_COLS) {
+    mul_cols(a.d, b.d, t);  // the same columns, one scheduled asm statement each (kh_cols.h)
+    fe_reduce512(r, t);
+    return;
+  }
   // product scanning: column k = sum_{i+j=k} a_i*b_j in a 64-bit accumulator + carry count
   uint64_t acc = 0;
   uint32_t cnt = 0;
@@ -378,6 +400,9 @@ KH_HD void fe_sqr(fe &r, const fe &a) {
   uint32_t t[16];
 #if defined(__HIP_DEVICE_COMPILE__)
   // cross products a_i*a_j (i<j) by product scanning, doubled, plus the squares a_i^2
+  if constexpr (KH_COLS) {
+    sqr_cross_cols(a.d, t);  // one scheduled asm statement per column (kh_cols.h)
+  } else {
   uint64_t acc = 0;
   uint32_t cnt = 0;
   t[0] = 0;
@@ -400,6 +425,7 @@ KH_HD void fe_sqr(fe &r, const fe &a) {
   }
   t[14] = (uint32_t)acc;
   t[15] = (uint32_t)(acc >> 32);
+  }
   // double
 #pragma unroll
   for (int i = 15; i > 0; i--) t[i] = __builtin_amdgcn_alignbit(t[i], t[i - 1], 31);

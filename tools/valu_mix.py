@@ -1,0 +1,227 @@
+#!/usr/bin/env python3
+"""Class-weighted VALU ceiling of the walk kernels (bench.py "frac_mix").
+
+For each kernel: the dynamic instruction mix per point, priced at the measured SIMD cost of each
+instruction class, gives the SIMD cycles per point the kernel needs when every SIMD issues its mix
+back to back (s_nop pads included); bench.py compares the measured rate with
+1024 SIMDs x clock / that figure.
+
+Dynamic mix.  The hot loops are read from the ISA listing of an analysis build compiled with
+-DKH_ISA_MARKS, which only adds an empty asm comment ";@kh_rare" to every rarely executed fix-up
+block (kh_math.h KH_RARE_MARK: carries rippling past limb 1, reductions with an overflowing slice,
+recorded hits).  A rare region runs from a marked block to the label its guarding branch jumps to;
+everything else in the loop is the common path, executed once per trip.  Per point:
+    (forward-loop trip + backward-loop trip) / 2
+since both loops of a 2H-point group run H trips (one prefix product / one symmetric pair each);
+the inversion and the centre step (once per group) are left out (< 1 %: they are checked against the
+PMC count below).  The sparse BSGS pad rebuilds every other prefix product in the backward loop
+(SPARSE, kh_kernels.hip), a block taken on half the trips: the tool counts it at 1/2 when it finds
+it (a branch on the loop counter's parity, s_bitcmp).  The resulting VALU per point is printed beside
+the PMC SQ_INSTS_VALU per point of the shipped build; they agree within a few %.
+
+Class costs (SIMD cycles per wave-instruction at 4 waves/SIMD, in shader cycles):
+profiles/r03b_ubench_cost.txt (tools/ubench_cost.hip).
+
+usage: python tools/valu_mix.py LISTING.s PMC_SUMMARY.json OUT.json [COST.txt]
+"""
+import json
+import re
+import sys
+
+KERNELS = {"k_walk<7, 2048>": "_Z6k_walkILi7ELi2048EEv9walk_args",
+           "k_walk<10, 2048>": "_Z6k_walkILi10ELi2048EEv9walk_args",
+           "k_walk<11, 2048>": "_Z6k_walkILi11ELi2048EEv9walk_args"}
+
+# ubench_cost.txt pattern name -> class
+PATTERN = {"mad_u64_u32 acc, 4 chains": "mad64", "add_co/addc, 4 sgpr chains": "carry", "v_mov_b32": "mov",
+           "v_add_u32": "full", "v_bitop3_b32": "bitop3", "v_alignbit_b32": "alignbit", "v_add3_u32": "add3",
+           "v_pk_lshlrev_b16": "pk16", "v_perm_b32": "perm", "v_cmp_eq_u32 (vcc)": "cmp",
+           "v_cndmask_b32_e64 (sgpr)": "cndmask", "v_add_co_u32_e32 (vcc) indep": "carry_vcc",
+           "v_lshrrev_b64": "alu64", "v_mov_b64": "mov64", "v_mul_lo/hi_u32": "mul32", "s_nop 0 only": "s_nop"}
+
+
+def klass(op: str) -> str | None:
+    """Cost class of one opcode (None: not a VALU / s_nop instruction)."""
+    if op == "s_nop":
+        return "s_nop"
+    if not op.startswith("v_"):
+        return None
+    if op.startswith("v_mad_u64_u32"):
+        return "mad64"
+    if op.startswith(("v_add_co_u32", "v_sub_co_u32", "v_subrev_co_u32")):
+        return "carry_vcc" if op.endswith("_e32") else "carry"
+    if op.startswith(("v_addc_co_u32", "v_subb_co_u32", "v_subbrev_co_u32")):
+        return "carry_vcc" if op.endswith("_e32") else "carry"
+    if op.startswith(("v_mov_b64", "v_pk_mov_b32")):
+        return "mov64"
+    if op.startswith("v_mov_b32"):
+        return "mov"
+    if op.startswith("v_bitop3"):
+        return "bitop3"
+    if op.startswith(("v_alignbit", "v_alignbyte")):
+        return "alignbit"
+    if op.startswith(("v_add3_u32", "v_lshl_add_u32", "v_add_lshl_u32", "v_lshl_or_b32", "v_and_or_b32",
+                      "v_or3_b32", "v_xor3_b32", "v_xad_u32", "v_bfi_b32", "v_bfe_u32")):
+        return "add3"
+    if op.startswith("v_pk_"):
+        return "pk16"
+    if op.startswith("v_perm"):
+        return "perm"
+    if op.startswith(("v_cmp", "v_cmpx")):
+        return "cmp"
+    if op.startswith("v_cndmask"):
+        return "cndmask"
+    if op.startswith(("v_lshrrev_b64", "v_lshlrev_b64", "v_ashrrev_i64", "v_lshl_add_u64")):
+        return "alu64"
+    if op.startswith(("v_mul_lo", "v_mul_hi", "v_mad_u32", "v_mul_u32")):
+        return "mul32"
+    if op.startswith(("v_add_u32", "v_sub_u32", "v_subrev_u32", "v_and_b32", "v_or_b32", "v_xor_b32", "v_not_b32",
+                      "v_lshlrev_b32", "v_lshrrev_b32", "v_ashrrev_i32", "v_max_u32", "v_min_u32")):
+        return "full"
+    return "other"  # priced as the half-rate median
+
+
+def costs(path: str) -> dict:
+    """{class: SIMD cycles per wave-instruction at 4 waves/SIMD} from ubench_cost.txt."""
+    c = {}
+    for line in open(path):
+        m = re.match(r"^(.*?)\s+W1\s+([\d.]+).*W4\s+([\d.]+)", line)
+        if m and m.group(1).strip() in PATTERN:
+            c[PATTERN[m.group(1).strip()]] = float(m.group(3))
+    half = sorted(v for k, v in c.items() if k in ("mad64", "carry", "cmp", "alignbit", "add3", "perm", "alu64"))
+    c["other"] = half[len(half) // 2]
+    return c
+
+
+def function(lines, sym):
+    s = next(i for i, l in enumerate(lines) if l.startswith(sym + ":"))
+    e = next(i for i in range(s, len(lines)) if lines[i].startswith(".Lfunc_end"))
+    return lines[s:e]
+
+
+def blocks(body):
+    """[(label, [instruction lines], marked)] in listing order; label None for fall-through blocks."""
+    out, cur, lab, mark = [], [], None, False
+    for l in body:
+        t = l.strip()
+        m = re.match(r"^(\.LBB\d+_\d+):", l)
+        if m or t.startswith("; %bb."):
+            if cur or lab:
+                out.append((lab, cur, mark))
+            cur, lab, mark = [], (m.group(1) if m else None), False
+            continue
+        if ";@kh_rare" in t:
+            mark = True
+            continue
+        if t and not t.startswith(";") and not t.startswith(".") and not t.endswith(":"):
+            cur.append(t)
+    out.append((lab, cur, mark))
+    return out
+
+
+def loops(bl):
+    """(start, end) block indices of each loop (a backward branch to a label), largest first."""
+    idx = {b[0]: i for i, b in enumerate(bl) if b[0]}
+    res = []
+    for i, (_, ins, _) in enumerate(bl):
+        for t in ins:
+            m = re.match(r"s_(cbranch_\w+|branch)\s+(\.LBB\d+_\d+)", t)
+            if m and m.group(2) in idx and idx[m.group(2)] <= i:
+                res.append((idx[m.group(2)], i))
+    # keep outermost-distinct loops by size
+    res = sorted(set(res), key=lambda x: -(sum(len(bl[k][1]) for k in range(x[0], x[1] + 1))))
+    return res
+
+
+def common_path(bl, a, b):
+    """Per-trip weight of each block of the loop [a, b]: 0 for rare regions, 1/2 for the parity
+    block, else 1."""
+    w = [1.0] * len(bl)
+    idx = {x[0]: i for i, x in enumerate(bl) if x[0]}
+    # the sparse pad's odd-trip block: entered through a branch on the counter's parity (s_bitcmp)
+    for j in range(a, b + 1):
+        ins = bl[j][1]
+        if ins and any(t.startswith("s_bitcmp") for t in ins):
+            m = re.match(r"s_cbranch_scc[01]\s+(\.LBB\d+_\d+)", ins[-1])
+            if m and idx.get(m.group(1), -1) > j:
+                for k in range(j + 1, min(idx[m.group(1)], b + 1)):
+                    w[k] = 0.5
+    i = a
+    while i <= b:
+        if bl[i][2]:
+            # the guarding branch: last instruction of the previous block with a forward target
+            j = i - 1
+            while j >= a and not bl[j][1]:
+                j -= 1
+            tgt = None
+            if j >= a:
+                m = re.match(r"s_cbranch_\w+\s+(\.LBB\d+_\d+)", bl[j][1][-1])
+                if m and idx.get(m.group(1), -1) > i:
+                    tgt = idx[m.group(1)]
+            end = tgt if tgt is not None else i + 1
+            for k in range(i, min(end, b + 1)):
+                w[k] = 0.0
+            i = max(end, i + 1)
+            continue
+        i += 1
+    return w
+
+
+def mix(listing: str, sym: str):
+    lines = open(listing).read().split("\n")
+    bl = blocks(function(lines, sym))
+    ls = loops(bl)
+    # the backward loop (largest) and the forward loop (largest one not overlapping it)
+    bwd = ls[0]
+    fwd = next(x for x in ls[1:] if x[1] < bwd[0] or x[0] > bwd[1])
+    per_point = {}
+    for (a, b) in (bwd, fwd):
+        w = common_path(bl, a, b)
+        for k in range(a, b + 1):
+            for t in bl[k][1]:
+                op = t.split()[0]
+                c = klass(op)
+                if c is None:
+                    continue
+                n = w[k] / 2.0  # one trip = one pair per lane (backward) / one prefix (forward)
+                if c == "s_nop":
+                    n *= int(t.split()[1]) + 1 if len(t.split()) > 1 else 1  # s_nop N = N + 1 states
+                per_point[c] = per_point.get(c, 0.0) + n
+    return per_point
+
+
+def main():
+    listing, pmc, out = sys.argv[1:4]
+    cost = costs(sys.argv[4] if len(sys.argv) > 4 else "profiles/r03b_ubench_cost.txt")
+    pm = json.load(open(pmc))
+    res = {}
+    for name, sym in KERNELS.items():
+        pp = mix(listing, sym)
+        # pp: lane-instructions per point (every lane walks its own points); a wave-instruction
+        # serves 64 points, so SIMD cycles per point = sum(count x class cost) / 64
+        valu = sum(v for k, v in pp.items() if k != "s_nop")
+        cyc = sum(v * cost[k] for k, v in pp.items()) / 64
+        e = {"valu_per_point_static": valu, "s_nop_states_per_point": pp.get("s_nop", 0.0),
+             "lane_instructions_per_point": {k: round(v, 2) for k, v in sorted(pp.items())},
+             "class_cost_simd_cycles": {k: cost[k] for k in sorted(pp)},
+             "simd_cycles_per_point": cyc,
+             "simd_cycles_by_class": {k: round(v * cost[k] / 64, 4)
+                                      for k, v in sorted(pp.items(), key=lambda x: -x[1] * cost[x[0]])},
+             "listing": listing, "costs": "profiles/r03b_ubench_cost.txt"}
+        if name in pm and "valu_lane_instructions_per_point" in pm[name]:
+            e["valu_per_point_pmc"] = pm[name]["valu_lane_instructions_per_point"]
+            # scale the static mix to the measured dynamic VALU count (inversion, centre step)
+            f = pm[name]["valu_lane_instructions_per_point"] / valu
+            e["pmc_over_static"] = f
+            e["simd_cycles_per_point"] = cyc * f
+        res[name] = e
+    json.dump(res, open(out, "w"), indent=1)
+    for k, e in res.items():
+        print(k, "static VALU/pt %.1f  PMC %.1f  s_nop states/pt %.1f  SIMD cycles/pt %.3f" % (
+            e["valu_per_point_static"], e.get("valu_per_point_pmc", 0), e["s_nop_states_per_point"],
+            e["simd_cycles_per_point"]))
+        print("   ", e["simd_cycles_by_class"])
+
+
+if __name__ == "__main__":
+    main()
