@@ -106,6 +106,9 @@ typedef struct {
 
 /* ---- context ------------------------------------------------------------------------------ */
 int kh_device_count(int *count);
+/* free and total device memory of `device` (hipMemGetInfo): hosts that stack several contexts on
+ * one device check kh_bsgs_memory against it before building their tables */
+int kh_device_memory(int device, uint64_t *free_bytes, uint64_t *total_bytes);
 int kh_open(int device, kh_ctx **out);
 int kh_close(kh_ctx *ctx);
 const char *kh_strerror(int code);
@@ -138,6 +141,10 @@ int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride[32], uint
 /* layer-1 layout for the next kh_bsgs_setup (KH_LAYER1_BLOCKED unless changed) */
 int kh_bsgs_set_layer1(kh_ctx *ctx, uint32_t layout);
 int kh_bsgs_setup(kh_ctx *ctx, uint64_t n, uint64_t k, kh_bsgs_info *info);
+/* after kh_bsgs_setup: the device bytes this context holds once its tables are built and it scans
+ * (the three layers, the bP rows, the inversion pad of the giant walk, lane state), and how many of
+ * them it holds already */
+int kh_bsgs_memory(kh_ctx *ctx, uint64_t *needed_bytes, uint64_t *held_bytes);
 int kh_bsgs_build(kh_ctx *ctx);                  /* baby-step blooms + sorted bP table on the GPU */
 /* -S table files in the reference's formats (keyhunt.cpp:2504-2652 write, 1983-2230 read), in dir
  * (NULL -> "."): keyhunt_bsgs_4_<M>.blm, keyhunt_bsgs_6_<M2>.blm, keyhunt_bsgs_7_<M3>.blm (256 x

@@ -647,6 +647,17 @@ int kh_device_count(int *count) {
   return KH_OK;
 }
 
+int kh_device_memory(int device, uint64_t *free_bytes, uint64_t *total_bytes) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return KH_E_HIP;
+  if (hipSetDevice(device) != hipSuccess) return KH_E_HIP;
+  size_t f = 0, t = 0;
+  if (hipMemGetInfo(&f, &t) != hipSuccess) return KH_E_HIP;
+  if (free_bytes) *free_bytes = f;
+  if (total_bytes) *total_bytes = t;
+  return KH_OK;
+}
+
 int kh_open(int device, kh_ctx **out) {
   if (!out) return KH_E_ARG;
   *out = nullptr;
@@ -929,6 +940,18 @@ int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride_be[32], u
     return base < 2 ? 2 * e + base : base == 2 || base == KH_KIND_ETH ? 6 + 2 * e + neg : 12 + e;
   };
   std::vector<kh_dev_hit> dh(ctx->h_hits.begin(), ctx->h_hits.begin() + nd);
+  // -e -c eth: a hit on (beta X, Y) is also the reference's slot-4 hit (keyhunt.cpp:3533), whose key
+  // it derives as lambda^2 k, checks against the image, and so negates (3736-3744): added as kind
+  // ETH | ENDO2 (an image the GPU never probes in this mode) before the sort, whose order puts it
+  // between the point's slot-3 eth(-beta P) and slot-5 eth(-beta^2 P) hits (3706-3745)
+  if (endo && mode == KH_MODE_ETH) {
+    for (size_t i = 0, n = dh.size(); i < n; i++)
+      if (dh[i].kind == (KH_KIND_ETH | (1u << KH_DKIND_ENDO_SHIFT))) {
+        kh_dev_hit t = dh[i];
+        t.kind = KH_KIND_ETH | (2u << KH_DKIND_ENDO_SHIFT);
+        dh.push_back(t);
+      }
+  }
   std::sort(dh.begin(), dh.end(), [&](const kh_dev_hit &a, const kh_dev_hit &b) {
     return a.idx != b.idx ? a.idx < b.idx : order(a.kind) < order(b.kind);
   });
@@ -940,21 +963,6 @@ int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride_be[32], u
       fe{{1, 0, 0, 0, 0, 0, 0, 0}},
       fe{{0x719501eeu, 0xc1396c28u, 0x12f58995u, 0x9cf04975u, 0xac3434e9u, 0x6e64479eu, 0x657c0710u, 0x7ae96a2bu}},
       fe{{0x8e6afa40u, 0x3ec693d6u, 0xed0a766au, 0x630fb68au, 0x53cbcb16u, 0x919bb861u, 0x9a83f8efu, 0x851695d4u}}};
-  // -e -c eth: a hit on (beta X, Y) is also the reference's slot-4 hit (keyhunt.cpp:3533), whose key
-  // it derives as lambda^2 k, checks against the image, and so negates (3736-3744): appended as
-  // kind ETH | ENDO2 (an image the GPU never probes in this mode) right after its slot-2 twin
-  if (endo && mode == KH_MODE_ETH) {
-    std::vector<kh_dev_hit> d2;
-    for (auto &h : dh) {
-      d2.push_back(h);
-      if (h.kind == (KH_KIND_ETH | (1u << KH_DKIND_ENDO_SHIFT))) {
-        kh_dev_hit t = h;
-        t.kind = KH_KIND_ETH | (2u << KH_DKIND_ENDO_SHIFT);
-        d2.push_back(t);
-      }
-    }
-    dh.swap(d2);
-  }
   std::vector<kh_hit> out;
   for (auto &h : dh) {
     u256 k = sc_add(st, sc_reduce(u256_from_u128((u128)h.idx)));
@@ -1063,7 +1071,8 @@ int kh_bsgs_setup(kh_ctx *ctx, uint64_t n, uint64_t k, kh_bsgs_info *info) {
       // the probe record carries the block index within a shard and the shard byte, and addresses a
       // shard by a 32-bit stride (k_walk blk_record / blk_load): shards must stay below 4 GB
       if (((blocks * 16 + 255) & ~255ULL) >> 32) {
-        ctx->err = "blocked layer 1 needs shards below 4 GB (M < ~2^36); use KH_LAYER1_REFERENCE";
+        ctx->err = "blocked layer 1 needs shards below 4 GB (M < ~2^36.6; the reference layout's shards reach the "
+                   "2^32-bit probe limit below that, at M ~2^35.1)";
         return KH_E_ARG;
       }
       ctx->bd[0].bits = blocks;
@@ -1071,8 +1080,8 @@ int kh_bsgs_setup(kh_ctx *ctx, uint64_t n, uint64_t k, kh_bsgs_info *info) {
       ctx->bd[0].bytes = blocks * 16;
     }
     ctx->bd[l].stride = (ctx->bd[l].bytes + 255) & ~255ULL;
-    if (ctx->bd[l].bits >> 32) {  // the probes' bit index reduction (mod_bits) assumes bits < 2^32
-      ctx->err = "a bloom shard of 2^32 bits or more is outside the probes' index range";
+    if (ctx->bd[l].bits >> 32) {  // shards of 2^32 bits or more (M >= ~2^35.1 in layer 1) are refused
+      ctx->err = "a bloom shard of 2^32 bits or more (M >= ~2^35.1) is outside the engine's tested probe range";
       return KH_E_ARG;
     }
     I.bloom_bits[l] = (l == 0 && ctx->l1_layout == KH_LAYER1_BLOCKED) ? ctx->bd[0].bits * 128 : ctx->bd[l].bits;
@@ -1166,6 +1175,22 @@ int build_walk(kh_ctx *ctx, int mode, uint8_t *bl1, const bloom_desc &bd1, uint6
   return run_walk(ctx, mode, 3, A, jg.gpl, 4);
 }
 }  // namespace
+
+int kh_bsgs_memory(kh_ctx *ctx, uint64_t *needed_bytes, uint64_t *held_bytes) {
+  if (!ctx) return KH_E_ARG;
+  if (!ctx->bsgs_ready) return KH_E_STATE;
+  uint64_t layers = 0;
+  for (int l = 0; l < 3; l++) layers += 256 * ctx->bd[l].stride + 4;
+  const uint64_t L = ctx->lanes_max;
+  // the giant walk's pad (L x KH_WALK_HB entries of 32 B), lane centres and scalars, the comb,
+  // candidate buffers, and the build's transient row keys (m3 x 12 B)
+  const uint64_t walk = L * (uint64_t)KH_WALK_HB * 32 + L * 32 * 3 + (512u << 10) + 4ull * ctx->cand_cap * 16 +
+                        ctx->info.m3 * 12;
+  if (needed_bytes) *needed_bytes = layers + walk;
+  if (held_bytes)
+    *held_bytes = layers + (uint64_t)ctx->lanes_alloc * ctx->scratch_h * 32 + (uint64_t)ctx->lanes_alloc * 32 * 3;
+  return KH_OK;
+}
 
 int kh_bsgs_build(kh_ctx *ctx) {
   if (!ctx) return KH_E_ARG;

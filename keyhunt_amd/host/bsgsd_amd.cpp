@@ -526,12 +526,29 @@ int main(int argc, char **argv) {
   g_gpus.resize(opt.gpus);
   bool present = false;
   std::vector<uint8_t> ptable_rows;
+  // every context holds its own tables and walk pad: before any table is built, the contexts each
+  // device will carry must fit its free memory (measured before the first context allocates)
+  std::vector<uint64_t> dev_free(ndev, 0);
+  for (int d = 0; d < ndev && d < opt.gpus; d++) kh_device_memory(d, &dev_free[d], nullptr);
   for (int d = 0; d < opt.gpus; d++) {
     gpu &g = g_gpus[d];
     int r = kh_open(d % ndev, &g.ctx);
     if (!r) r = kh_bsgs_set_layer1(g.ctx, opt.layer1);
     if (!r) r = kh_bsgs_set_base_check(g.ctx, 1);  // bsgsd.cpp:2544-2561
     if (!r) r = kh_bsgs_setup(g.ctx, opt.n, opt.k, &g.info);
+    if (!r && d == 0) {
+      uint64_t need = 0;
+      kh_bsgs_memory(g.ctx, &need, nullptr);
+      for (int dev = 0; dev < ndev && dev < opt.gpus; dev++) {
+        const uint64_t per = (uint64_t)(opt.gpus / ndev + (dev < opt.gpus % ndev ? 1 : 0));
+        if (dev_free[dev] && per * need > dev_free[dev]) {
+          fprintf(stderr, "[E] -g %d: %llu context(s) on GPU %d need %.1f GB of device memory (%.1f GB each), "
+                          "%.1f GB are free; use fewer contexts (-g) or a smaller -n / -k\n",
+                  opt.gpus, (unsigned long long)per, dev, per * need / 1e9, need / 1e9, dev_free[dev] / 1e9);
+          return EXIT_FAILURE;
+        }
+      }
+    }
     if (!r && d == 0) {
       r = first_tables(g, ptable_rows, present);
     } else if (!r) {  // the first context left the four files (or the --ptable rows) for the others

@@ -98,6 +98,8 @@ E2E_RUNS = [
     # (keyhunt.cpp:3524-3536, 3703-3760; tests/golden/make_eth_endo_targets.py)
     ("address_eth_endo_2p20", ["-m", "address", "-c", "eth", "-e", "-f", "eth_endo.txt", "-r", "1:100000", "-n", "0x100000", "-t", "8"], 300),
     ("address_eth_2p20_endo", ["-m", "address", "-c", "eth", "-e", "-f", "eth_targets.txt", "-r", "1:100000", "-n", "0x100000", "-t", "8"], 300),
+    # one thread, so the file's record order is the reference's per-point slot order (ORDERED)
+    ("address_eth_endo_pair_t1", ["-m", "address", "-c", "eth", "-e", "-f", "eth_endo_pair.txt", "-r", "1:100000", "-n", "0x100000", "-t", "1"], 300),
     # -r START without END runs to the group order (keyhunt.cpp:1028-1033): BSGS ends at "All points
     # were found"; the address family never ends, so it is stopped after `tmo` s and only hits
     # below the "cmp_below" key are compared
@@ -243,6 +245,10 @@ STDERR_NOTE = re.compile(r"^\[[IE]\] (?:Ommiting|Omiting|Ignoring)[^\n]*$", re.M
 STDOUT_NOTE = re.compile(r"^(?:ParsePublicKeyHex: |Invalid length: )[^\n]*$", re.M)
 
 
+# single-thread runs whose KEYFOUNDKEYFOUND.txt record order is pinned too ("hits_in_order")
+ORDERED = {"address_eth_endo_pair_t1"}
+
+
 def gen_e2e(only: list[str] | None = None) -> None:
     subprocess.run(["make", "-s", "-C", HERE, "-f", "Makefile.ref", "-j8"], check=True)
     path = os.path.join(REPO, "tests", "golden", "ref_e2e.json")
@@ -261,6 +267,8 @@ def gen_e2e(only: list[str] | None = None) -> None:
             hits = sorted(parse_keyfound(text), key=lambda h: int(h["key"], 16))
             blocks = stdout_blocks(p.stdout)
             results[name] = {"argv": argv, "exit": p.returncode, "hits": hits, "stdout_blocks": blocks}
+            if name in ORDERED:
+                results[name]["hits_in_order"] = parse_keyfound(text)
             if name.startswith("ragged"):
                 results[name]["stderr_lines"] = STDERR_NOTE.findall(p.stderr)
                 results[name]["stdout_notes"] = STDOUT_NOTE.findall(p.stdout)

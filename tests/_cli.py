@@ -22,7 +22,9 @@ STDERR_NOTE = re.compile(r"^\[[IE]\] (?:Ommiting|Omiting|Ignoring)[^\n]*$", re.M
 STDOUT_NOTE = re.compile(r"^(?:ParsePublicKeyHex: |Invalid length: )[^\n]*$", re.M)
 
 
-def parse_keyfound(text: str) -> list[dict]:
+def parse_keyfound(text: str, ordered: bool = False) -> list[dict]:
+    """The records of KEYFOUNDKEYFOUND.txt / VANITYKEYFOUND.txt, sorted by key (or, with ordered, in
+    file order per record kind, as oracle/make_golden.py stores "hits_in_order")."""
     hits = []
     for m in re.finditer(r"(Vanity )?Private Key: ([0-9a-f]+)\npubkey: ([0-9a-f]+)\nAddress (\S+)\nrmd160 ([0-9a-f]+)", text):
         h = {"key": m.group(2), "pubkey": m.group(3), "address": m.group(4), "rmd160": m.group(5)}
@@ -33,7 +35,7 @@ def parse_keyfound(text: str) -> list[dict]:
         hits.append({"key": m.group(1), "pubkey": m.group(2)})
     for m in re.finditer(r"Private Key: ([0-9a-f]+)\naddress: (0x[0-9a-f]+)\n", text):  # writekeyeth
         hits.append({"key": m.group(1), "address": m.group(2)})
-    return sorted(hits, key=lambda h: int(h["key"], 16))
+    return hits if ordered else sorted(hits, key=lambda h: int(h["key"], 16))
 
 
 def run_cli(argv: list[str], timeout: int = 600, kill_after: int | None = None):
@@ -51,6 +53,7 @@ def run_cli(argv: list[str], timeout: int = 600, kill_after: int | None = None):
         for fn in ("KEYFOUNDKEYFOUND.txt", "VANITYKEYFOUND.txt"):
             kf = os.path.join(td, fn)
             text += open(kf).read() if os.path.exists(kf) else ""
+        p.hits_in_order = parse_keyfound(text, ordered=True)
         return p, parse_keyfound(text)
 
 
@@ -83,6 +86,8 @@ def check_against_reference(ref: dict, argv: list[str], name: str):
             rest.remove(b)
     else:
         assert blocks == ref_blocks
+    if "hits_in_order" in ref:  # single-thread fixtures: the records in the reference's print order
+        assert p.hits_in_order == ref["hits_in_order"]
     if "stderr_lines" in ref:  # the reference's notes on target-file lines it skipped, in order
         assert STDERR_NOTE.findall(p.stderr) == ref["stderr_lines"]
     if "stdout_notes" in ref:  # and on public keys it refused

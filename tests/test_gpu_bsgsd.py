@@ -3,6 +3,7 @@ to a transcript of the reference daemon itself (tests/golden/ref_bsgsd.json): on
 connection, line mode and HTTP POST/JSON mode, the same reply bytes and printed lines; the same
 table files (-S, .tbl.md5, --ptable / --ptable-cache / --load-ptable) on start and restart."""
 import json
+import re
 import os
 import socket
 import subprocess
@@ -130,3 +131,16 @@ def test_tables_written_then_read(workdir):
         assert d.line(f"{PUB63} 7cce5efdac000000:7cce5efdad000000\n".encode()) == (KEY63 + "\n").encode()
     finally:
         d.stop()
+
+
+def test_contexts_beyond_device_memory_are_refused(tmp_path):
+    """-g stacks contexts on a device, each with its own tables and walk pad: a count that cannot
+    fit the device's free memory is refused before any table is built (the old daemon ran
+    out of memory after the first context's build)."""
+    t0 = time.time()
+    p = subprocess.run([DAEMON, "-n", "0x100000000000", "-k", "512", "-g", "64", "-p", str(free_port())],
+                       cwd=str(tmp_path), capture_output=True, text=True, timeout=300)
+    assert p.returncode != 0
+    assert re.search(r"-g 64: \d+ context\(s\) on GPU 0 need [\d.]+ GB of device memory", p.stderr), p.stderr
+    assert not any(f.startswith("keyhunt_bsgs_") for f in os.listdir(tmp_path))  # nothing built or written
+    assert time.time() - t0 < 120
