@@ -1609,12 +1609,14 @@ int main(int argc, char **argv) {
       bj[d].comp = &comp;
       bj[d].n = n;
       bj[d].k = opt.kfactor;
-      // ~2^31 giant points per engine call: enough lanes to fill the GPU, ~0.1 s per call; a range
-      // of fewer bases than that is dealt out evenly over the contexts (the reference's threads
-      // take one base each, keyhunt.cpp:4600-4617)
+      // ~2^35 giant points per engine call (16 pipelined rounds, ~1 s): the end of a call drains
+      // the pipeline (the last round's second check, the hit copies), which at 2^31 points per call
+      // cost 7 % of the rate (profiles/r03f_cli_rate_bsgs.json); a call returns as soon as every
+      // target is found.  A range of fewer bases than that is dealt out evenly over the contexts (the
+      // reference's threads take one base each, keyhunt.cpp:4600-4617)
       {
         uint64_t aux = Nr / M, pts = ((aux + 1023) / 1024) * 1024;
-        bj[d].bases_per_call = std::max<uint64_t>(1, (1ULL << 31) / pts);
+        bj[d].bases_per_call = std::max<uint64_t>(1, (1ULL << 35) / pts);
         const U span = u_sub(opt.end, opt.start);
         if (g_step.v[1] == 0 && g_step.v[2] == 0 && g_step.v[3] == 0 && g_step.v[4] == 0) {
           uint64_t rem = 0;

@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU session: GPU tests, bench, rocprofv3 kernel-trace stats of the bench, PMC counter passes.
 # Usage (on the box, from the repo root): bash tools/gpu_round.sh TAG [parts]
-#   parts: any of tests,bench,prof,pmc (default all).  Every GPU step has its own time limit and
+#   parts: any of tests,bench,prof,pmc,ubench,config5 (default tests,bench,prof,pmc).  Every GPU step has its own time limit and
 #   the script stops at the first failure.
 set -o pipefail
 TAG=${1:-r01}
@@ -32,7 +32,8 @@ if has pmc; then
   i=0
   for c in "TCC_EA0_RDREQ_sum TCC_HIT_sum TCC_MISS_sum" "WRITE_SIZE" "FETCH_SIZE" \
            "SQ_INSTS_VALU SQ_WAVES SQ_INSTS_SALU SQ_INSTS_SMEM GRBM_GUI_ACTIVE" \
-           "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU"; do
+           "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU" \
+           "SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU2 SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_CYCLES GRBM_GUI_ACTIVE"; do
     i=$((i + 1))
     timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d $O/pmc/p$i -o run -- \
       python3 $R/tools/pmc_run.py > $O/pmc_p$i.log 2>&1 || { echo "pmc pass $i rc=$?"; tail -20 $O/pmc_p$i.log; exit 1; }
@@ -41,6 +42,10 @@ if has pmc; then
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/pmc/trace -o run -- \
     python3 $R/tools/pmc_run.py > $O/pmc_trace.log 2>&1 || { echo "pmc trace rc=$?"; tail -20 $O/pmc_trace.log; exit 1; }
   echo "pmc ok"
+fi
+if has ubench; then
+  timeout -k 10 120 $R/tools/ubench_cost > $O/ubench_cost.txt 2>&1 || { echo "ubench rc=$?"; tail -5 $O/ubench_cost.txt; exit 1; }
+  cat $O/ubench_cost.txt
 fi
 if has config5; then
   timeout -k 10 600 python $R/bench.py --config 5 > $O/bench_c5.json 2> $O/bench_c5.err || { echo "bench c5 rc=$?"; tail -20 $O/bench_c5.err; exit 1; }

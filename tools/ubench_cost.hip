@@ -5,14 +5,19 @@
 // from s_memtime / s_memrealtime (100 MHz), so the table is clock-free.
 //
 // Each pattern is one asm statement of 32 wave-instructions (s_nop included where the pattern has
-// them) per loop trip.  Printed per pattern and waves/SIMD (1, 2, 4, 8): SIMD cycles per
-// wave-instruction = median over waves of (delta s_memtime) / (trips x 32) / (waves per SIMD),
-// i.e. the per-SIMD cost when W waves share it, and the in-kernel clock.
+// them) per loop trip.  Printed per pattern and waves/SIMD (1, 2, 4, 8), two figures:
+//   span  SIMD cycles per wave-instruction from the whole launch: (last wave's end - first wave's
+//         start, s_memrealtime) x the in-kernel clock / (wave-instructions / 1024 SIMDs) -- the
+//         SIMD's throughput whether or not the waves all overlap;
+//   wave  the median wave's own (delta s_memtime) / (trips x 32): its issue interval per
+//         instruction while sharing the SIMD (4.2 alone for most classes),
+// and the in-kernel clock (delta s_memtime / delta s_memrealtime x 100 MHz).
 //
 // build: hipcc --offload-arch=gfx950 -O3 tools/ubench_cost.hip -o tools/ubench_cost
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 #include <algorithm>
 #include <vector>
@@ -133,6 +138,52 @@ __global__ __launch_bounds__(256) void k_pat(stamp *out, uint32_t seed) {
       asm volatile(R8("v_mad_u64_u32 %0, %4, %5, %6, %0\n s_nop 0\n v_mad_u64_u32 %1, %4, %5, %6, %1\n s_nop 0\n")
                    : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3), "=s"(s0)
                    : "v"(a), "v"(b));
+    if (P == 25)  // 16 mads (4 chains) + 16 independent SALU ops on 64-bit masks, interleaved
+      asm volatile(R4("v_mad_u64_u32 %0, %4, %5, %6, %0\n s_xor_b64 %7, %7, %8\n v_mad_u64_u32 %1, %4, %5, %6, %1\n"
+                      "s_and_b64 %8, %8, %7\n v_mad_u64_u32 %2, %4, %5, %6, %2\n s_or_b64 %7, %7, %8\n"
+                      "v_mad_u64_u32 %3, %4, %5, %6, %3\n s_xor_b64 %8, %8, %7\n")
+                   : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3), "=s"(s0), "+v"(a), "+v"(b), "+s"(s1), "+s"(s2)
+                   :
+                   : "scc");  // SALU ops write SCC: the loop's own compare-and-branch must not see it
+    if (P == 26)  // SALU only: 32 s_xor_b64 / s_and_b64 on 4 independent mask pairs
+      asm volatile(R8("s_xor_b64 %0, %0, %1\n s_and_b64 %1, %1, %2\n s_or_b64 %2, %2, %3\n s_xor_b64 %3, %3, %0\n")
+                   : "+s"(s0), "+s"(s1), "+s"(s2), "+s"(s3)
+                   :
+                   : "scc");
+    if (P == 27)  // a 7-product column counted by 7 v_addc (masks 3 apart) -- 14 VALU; x2 + 4 filler adds
+      asm volatile(R2("v_mad_u64_u32 %0, %2, %9, %10, %0\n v_mad_u64_u32 %0, %3, %9, %10, %0\n v_mad_u64_u32 %0, %4, %9, %10, %0\n"
+                      "v_addc_co_u32 %1, %2, 0, %1, %2\n v_mad_u64_u32 %0, %2, %9, %10, %0\n v_addc_co_u32 %1, %3, 0, %1, %3\n"
+                      "v_mad_u64_u32 %0, %3, %9, %10, %0\n v_addc_co_u32 %1, %4, 0, %1, %4\n v_mad_u64_u32 %0, %4, %9, %10, %0\n"
+                      "v_addc_co_u32 %1, %2, 0, %1, %2\n v_mad_u64_u32 %0, %2, %9, %10, %0\n v_addc_co_u32 %1, %3, 0, %1, %3\n"
+                      "v_addc_co_u32 %1, %4, 0, %1, %4\n v_addc_co_u32 %1, %2, 0, %1, %2\n"
+                      "v_add_u32 %5, %5, %9\n v_add_u32 %6, %6, %9\n")
+                   : "+v"(x0), "+v"(u0), "=&s"(s0), "=&s"(s1), "=&s"(s2), "+v"(u1), "+v"(u2), "+v"(u3), "+v"(x1)
+                   : "v"(a), "v"(b));
+    if (P == 28)  // the same column counted on the SALU: 7 masks -> bit-sliced full adders (20 SALU) ->
+                  // 3 VALU to materialize cnt = b0 + 2 b1 + 4 b2 -- 10 VALU + 20 SALU; x2 + 12 filler
+      asm volatile(R2("v_mad_u64_u32 %0, s[40:41], %9, %10, %0\n v_mad_u64_u32 %0, s[42:43], %9, %10, %0\n"
+                      "v_mad_u64_u32 %0, s[44:45], %9, %10, %0\n v_mad_u64_u32 %0, s[46:47], %9, %10, %0\n"
+                      "s_xor_b64 s[60:61], s[40:41], s[42:43]\n v_mad_u64_u32 %0, s[48:49], %9, %10, %0\n"
+                      "s_xor_b64 s[62:63], s[60:61], s[44:45]\n s_and_b64 s[64:65], s[40:41], s[42:43]\n"
+                      "v_mad_u64_u32 %0, s[50:51], %9, %10, %0\n s_and_b64 s[60:61], s[60:61], s[44:45]\n"
+                      "s_or_b64 s[64:65], s[64:65], s[60:61]\n v_mad_u64_u32 %0, s[52:53], %9, %10, %0\n"
+                      "s_xor_b64 s[66:67], s[46:47], s[48:49]\n s_xor_b64 s[68:69], s[66:67], s[50:51]\n"
+                      "s_and_b64 s[70:71], s[46:47], s[48:49]\n s_and_b64 s[66:67], s[66:67], s[50:51]\n"
+                      "s_or_b64 s[70:71], s[70:71], s[66:67]\n"
+                      "s_xor_b64 s[72:73], s[62:63], s[68:69]\n s_xor_b64 s[74:75], s[72:73], s[52:53]\n"
+                      "s_and_b64 s[76:77], s[62:63], s[68:69]\n s_and_b64 s[72:73], s[72:73], s[52:53]\n"
+                      "s_or_b64 s[76:77], s[76:77], s[72:73]\n"
+                      "s_xor_b64 s[78:79], s[64:65], s[70:71]\n s_xor_b64 s[80:81], s[78:79], s[76:77]\n"
+                      "s_and_b64 s[82:83], s[64:65], s[70:71]\n s_and_b64 s[78:79], s[78:79], s[76:77]\n"
+                      "s_or_b64 s[82:83], s[82:83], s[78:79]\n"
+                      "v_cndmask_b32_e64 %5, 0, 2, s[80:81]\n v_cndmask_b32_e64 %6, 0, 4, s[82:83]\n"
+                      "v_addc_co_u32 %1, s[84:85], %5, %6, s[74:75]\n"
+                      "v_add_u32 %7, %7, %9\n v_add_u32 %7, %7, %9\n v_add_u32 %7, %7, %9\n")
+                   : "+v"(x0), "+v"(u0), "=&s"(s0), "=&s"(s1), "=&s"(s2), "=&v"(u1), "=&v"(u2), "+v"(u3), "+v"(x1)
+                   : "v"(a), "v"(b)
+                   : "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s53",
+                     "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71", "s72", "s73",
+                     "s74", "s75", "s76", "s77", "s78", "s79", "s80", "s81", "s82", "s83", "s84", "s85", "scc");
     if (P == 24)  // 16 mads + 16 v_mov (the product-scanning column shift), interleaved
       asm volatile(R8("v_mad_u64_u32 %0, %4, %5, %6, %0\n v_mov_b32 %7, %5\n v_mad_u64_u32 %1, %4, %5, %6, %1\n"
                       "v_mov_b32 %8, %6\n")
@@ -152,7 +203,8 @@ __global__ __launch_bounds__(256) void k_pat(stamp *out, uint32_t seed) {
 typedef void (*kfn)(stamp *, uint32_t);
 #define K(n) k_pat<n>
 static const kfn kernels[] = {K(0),  K(1),  K(2),  K(3),  K(4),  K(5),  K(6),  K(7),  K(8),  K(9),  K(10), K(11), K(12),
-                              K(13), K(14), K(15), K(16), K(17), K(18), K(19), K(20), K(21), K(22), K(23), K(24)};
+                              K(13), K(14), K(15), K(16), K(17), K(18), K(19), K(20), K(21), K(22), K(23), K(24),
+                              K(25), K(26), K(27), K(28)};
 static const char *names[] = {
     "mad_u64_u32 acc, 4 chains",      "mad,nop,addc,nop (as hipcc)",  "mad+addc, hazards scheduled", "addc_e32 vcc chain + s_nop 1",
     "add_co/addc, 4 sgpr chains",     "v_mov_b32",                    "v_add_u32",                   "v_and_b32",
@@ -160,37 +212,49 @@ static const char *names[] = {
     "v_pk_lshlrev_b16",               "v_perm_b32",                   "v_cmp_eq_u32 (vcc)",          "v_cndmask_b32_e64 (sgpr)",
     "v_add_co_u32_e32 (vcc) indep",   "v_lshrrev_b64",                "v_lshl_add_u64",              "v_mov_b64",
     "v_mul_lo/hi_u32",                "s_nop 0 only",                 "v_add_u32 + s_nop 0",         "mad + s_nop 0 (no hazard)",
-    "mad + v_mov interleaved"};
+    "mad + v_mov interleaved",        "mad + SALU interleaved",       "SALU only (s_xor/and/or_b64)", "7-col: 7 addc (+2 add)",
+    "7-col: SALU count (+3 add)"};
 
-int main() {
+int main(int argc, char **argv) {
+  // optional: the pattern numbers to run (default all)
+  setvbuf(stdout, nullptr, _IOLBF, 0);
   const int NP = sizeof(kernels) / sizeof(kernels[0]);
+  std::vector<int> only;
+  for (int i = 1; i < argc; i++) only.push_back(atoi(argv[i]));
   const int waves_per_simd[] = {1, 2, 4, 8};
   stamp *d;
   const int max_blocks = 256 * 8;
   (void)hipMalloc(&d, sizeof(stamp) * max_blocks * 4);
   std::vector<stamp> h(max_blocks * 4);
-  printf("%-32s %s\n", "pattern (32 instr per trip)", "SIMD cycles per wave-instruction at W waves/SIMD [in-kernel GHz]");
+  printf("%-32s %s\n", "pattern (32 instr per trip)",
+         "at W waves/SIMD: span = SIMD cycles per wave-instruction (whole launch), wave = one wave's cycles per instruction [in-kernel GHz]");
   for (int p = 0; p < NP; p++) {
+    if (!only.empty() && std::find(only.begin(), only.end(), p) == only.end()) continue;
     printf("%-32s", names[p]);
     for (int w : waves_per_simd) {
       const int blocks = 256 * w;  // 256 CUs x w blocks of 4 waves: w waves per SIMD
-      double cyc = 0, ghz = 0;
+      double cyc = 0, ghz = 0, span = 0;
       for (int rep = 0; rep < 2; rep++) {  // the first launch warms the clock
         hipLaunchKernelGGL(kernels[p], dim3(blocks), dim3(256), 0, 0, d, 1u);
         (void)hipDeviceSynchronize();
         (void)hipMemcpy(h.data(), d, sizeof(stamp) * blocks * 4, hipMemcpyDeviceToHost);
         std::vector<double> c, g;
+        uint64_t rmin = ~0ull, rmax = 0;
         for (int i = 0; i < blocks * 4; i++) {
           const double dt = (double)(h[i].t1 - h[i].t0), dr = (double)(h[i].r1 - h[i].r0);
-          c.push_back(dt / (TRIPS * 32.0) / w);
+          c.push_back(dt / (TRIPS * 32.0));
           if (dr > 0) g.push_back(dt / dr * 0.1);  // s_memrealtime ticks at 100 MHz
+          rmin = std::min(rmin, h[i].r0);
+          rmax = std::max(rmax, h[i].r1);
         }
         std::sort(c.begin(), c.end());
         std::sort(g.begin(), g.end());
         cyc = c[c.size() / 2];
         ghz = g.empty() ? 0 : g[g.size() / 2];
+        // whole-launch SIMD cycles / wave-instructions per SIMD (blocks x 4 waves over 1024 SIMDs)
+        span = (double)(rmax - rmin) * 10.0 * ghz / ((double)blocks * 4 * TRIPS * 32 / 1024.0);
       }
-      printf("  W%d %5.2f [%.2f]", w, cyc, ghz);
+      printf("  W%d span %5.2f wave %5.2f [%.2f]", w, span, cyc, ghz);
     }
     printf("\n");
   }

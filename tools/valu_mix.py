@@ -12,15 +12,19 @@ block (kh_math.h KH_RARE_MARK: carries rippling past limb 1, reductions with an 
 recorded hits).  A rare region runs from a marked block to the label its guarding branch jumps to;
 everything else in the loop is the common path, executed once per trip.  Per point:
     (forward-loop trip + backward-loop trip) / 2
-since both loops of a 2H-point group run H trips (one prefix product / one symmetric pair each);
+since both loops of a 2H-point group run H trips (one prefix product / one symmetric pair each); the
+hash walks' per-point side loop inside the backward loop counts once per point;
 the inversion and the centre step (once per group) are left out (< 1 %: they are checked against the
 PMC count below).  The sparse BSGS pad rebuilds every other prefix product in the backward loop
 (SPARSE, kh_kernels.hip), a block taken on half the trips: the tool counts it at 1/2 when it finds
 it (a branch on the loop counter's parity, s_bitcmp).  The resulting VALU per point is printed beside
 the PMC SQ_INSTS_VALU per point of the shipped build; they agree within a few %.
 
-Class costs (SIMD cycles per wave-instruction at 4 waves/SIMD, in shader cycles):
-profiles/r03b_ubench_cost.txt (tools/ubench_cost.hip).
+Class costs (SIMD cycles per wave-instruction at 4 waves/SIMD, in shader cycles, whole-launch
+throughput): profiles/r03e_ubench_cost.txt (tools/ubench_cost.hip).  On gfx950 they fall in two
+rates: ~2.2 cycles (32-bit add / logic / shifts / v_mov_b32 / v_bitop3: a wave64 over a SIMD-32) and
+~4.2 (v_mad_u64_u32, every carry-in/out op, v_alignbit, v_add3, v_perm, packed 16-bit ops, compares,
+v_cndmask, 64-bit ALU ops, 32-bit multiplies); an s_nop stream issues at ~1.1 cycles per wait state.
 
 usage: python tools/valu_mix.py LISTING.s PMC_SUMMARY.json OUT.json [COST.txt]
 """
@@ -28,9 +32,10 @@ import json
 import re
 import sys
 
-KERNELS = {"k_walk<7, 2048>": "_Z6k_walkILi7ELi2048EEv9walk_args",
-           "k_walk<10, 2048>": "_Z6k_walkILi10ELi2048EEv9walk_args",
-           "k_walk<11, 2048>": "_Z6k_walkILi11ELi2048EEv9walk_args"}
+# kernel -> (symbol, its largest loop runs once per point: the hash walks' side loop)
+KERNELS = {"k_walk<7, 2048>": ("_Z6k_walkILi7ELi2048EEv9walk_args", False),
+           "k_walk<10, 2048>": ("_Z6k_walkILi10ELi2048EEv9walk_args", False),
+           "k_walk<11, 2048>": ("_Z6k_walkILi11ELi2048EEv9walk_args", True)}
 
 # ubench_cost.txt pattern name -> class
 PATTERN = {"mad_u64_u32 acc, 4 chains": "mad64", "add_co/addc, 4 sgpr chains": "carry", "v_mov_b32": "mov",
@@ -82,10 +87,11 @@ def klass(op: str) -> str | None:
 
 
 def costs(path: str) -> dict:
-    """{class: SIMD cycles per wave-instruction at 4 waves/SIMD} from ubench_cost.txt."""
+    """{class: SIMD cycles per wave-instruction at 4 waves/SIMD} from ubench_cost.txt: the "span"
+    figure (whole launch, in-kernel clock), i.e. the SIMD's throughput for that class."""
     c = {}
     for line in open(path):
-        m = re.match(r"^(.*?)\s+W1\s+([\d.]+).*W4\s+([\d.]+)", line)
+        m = re.match(r"^(.*?)\s+W1 span\s+([\d.]+).*W4 span\s+([\d.]+)", line)
         if m and m.group(1).strip() in PATTERN:
             c[PATTERN[m.group(1).strip()]] = float(m.group(3))
     half = sorted(v for k, v in c.items() if k in ("mad64", "carry", "cmp", "alignbit", "add3", "perm", "alu64"))
@@ -167,36 +173,52 @@ def common_path(bl, a, b):
     return w
 
 
-def mix(listing: str, sym: str):
+def mix(listing: str, sym: str, per_point_loop: bool):
+    """Lane-instructions per point by class.  The largest loop of the kernel is its per-pair
+    backward loop (deferred-probe walks) or, with per_point_loop, the per-point side loop of the
+    hash walks inside it; loops overlapping it are the rest of the backward loop (per pair), and the
+    largest loop before it is the forward loop (per prefix product = per pair)."""
     lines = open(listing).read().split("\n")
     bl = blocks(function(lines, sym))
     ls = loops(bl)
-    # the backward loop (largest) and the forward loop (largest one not overlapping it)
-    bwd = ls[0]
-    fwd = next(x for x in ls[1:] if x[1] < bwd[0] or x[0] > bwd[1])
+    top = ls[0]
+    over = [x for x in ls if not (x[1] < top[0] or x[0] > top[1])]
+    lo, hi = min(x[0] for x in over), max(x[1] for x in over)
+    fwd = next(x for x in ls if x[1] < lo)
+    weight = {}
+    for k in range(fwd[0], fwd[1] + 1):
+        weight[k] = 0.5
+    for k in range(lo, hi + 1):
+        weight[k] = 1.0 if (per_point_loop and top[0] <= k <= top[1]) else 0.5
+    cp = [common_path(bl, x[0], x[1]) for x in over + [fwd]]
+    rare = {k for w in cp for k in range(len(w)) if w[k] == 0.0}
+    half = {k for w in cp for k in range(len(w)) if w[k] == 0.5}
     per_point = {}
-    for (a, b) in (bwd, fwd):
-        w = common_path(bl, a, b)
-        for k in range(a, b + 1):
-            for t in bl[k][1]:
-                op = t.split()[0]
-                c = klass(op)
-                if c is None:
-                    continue
-                n = w[k] / 2.0  # one trip = one pair per lane (backward) / one prefix (forward)
-                if c == "s_nop":
-                    n *= int(t.split()[1]) + 1 if len(t.split()) > 1 else 1  # s_nop N = N + 1 states
-                per_point[c] = per_point.get(c, 0.0) + n
+    for k, wt in weight.items():
+        if k in rare:
+            continue
+        if k in half:
+            wt *= 0.5
+        for t in bl[k][1]:
+            op = t.split()[0]
+            c = klass(op)
+            if c is None:
+                continue
+            n = wt
+            if c == "s_nop":
+                n *= int(t.split()[1]) + 1 if len(t.split()) > 1 else 1  # s_nop N = N + 1 states
+            per_point[c] = per_point.get(c, 0.0) + n
     return per_point
 
 
 def main():
     listing, pmc, out = sys.argv[1:4]
-    cost = costs(sys.argv[4] if len(sys.argv) > 4 else "profiles/r03b_ubench_cost.txt")
+    cost_path = sys.argv[4] if len(sys.argv) > 4 else "profiles/r03e_ubench_cost.txt"
+    cost = costs(cost_path)
     pm = json.load(open(pmc))
     res = {}
-    for name, sym in KERNELS.items():
-        pp = mix(listing, sym)
+    for name, (sym, ppl) in KERNELS.items():
+        pp = mix(listing, sym, ppl)
         # pp: lane-instructions per point (every lane walks its own points); a wave-instruction
         # serves 64 points, so SIMD cycles per point = sum(count x class cost) / 64
         valu = sum(v for k, v in pp.items() if k != "s_nop")
@@ -207,7 +229,8 @@ def main():
              "simd_cycles_per_point": cyc,
              "simd_cycles_by_class": {k: round(v * cost[k] / 64, 4)
                                       for k, v in sorted(pp.items(), key=lambda x: -x[1] * cost[x[0]])},
-             "listing": listing, "costs": "profiles/r03b_ubench_cost.txt"}
+             "listing": listing, "costs": cost_path,
+             "recompute": "simd_cycles_per_point = sum(lane_instructions_per_point[c] * class_cost_simd_cycles[c]) / 64 * pmc_over_static"}
         if name in pm and "valu_lane_instructions_per_point" in pm[name]:
             e["valu_per_point_pmc"] = pm[name]["valu_lane_instructions_per_point"]
             # scale the static mix to the measured dynamic VALU count (inversion, centre step)
