@@ -136,6 +136,16 @@ int kh_set_vanity(kh_ctx *ctx, const uint8_t *ranges, uint64_t n, uint32_t probe
  * lanes instead of starting them again: sequential chunks are cheaper, results are the same. */
 int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride[32], uint64_t n_keys, uint32_t mode,
             uint32_t search, kh_hit *hits, uint32_t cap, uint32_t *n_hits);
+/* -m rmd160 --rmd-batch-size (keyhunt.cpp:815-829, 3301-3307): group = the reference's clamped
+ * rmd_batch_size (a multiple of 4 in [4, 1024]; 1024 or 0 = the ordinary walk).  Below 1024 the
+ * following hash160 kh_scan calls reproduce the reference's groups of `group` keys exactly as it
+ * computes them: its batch inversion then runs over a partly zero IntGroup and returns 0 for every
+ * inverse, so each group holds one real point (its centre, slot group/2) and group - 1 points
+ * x = -(C.x + (i+1)D.x) that are no multiples of G; a chunk of n_keys becomes ceil(n_keys/group)
+ * whole groups (it overshoots its end like the reference's do-while), and hits on those points
+ * carry the key of their slot with the reference's key resolution.  KH_MODE_ADDRESS and
+ * KH_MODE_ETH (-m rmd160 -c eth), exact targets. */
+int kh_set_rmd_batch(kh_ctx *ctx, uint32_t group);
 
 /* ---- BSGS --------------------------------------------------------------------------------- */
 /* layer-1 layout for the next kh_bsgs_setup (KH_LAYER1_BLOCKED unless changed) */

@@ -348,6 +348,7 @@ struct kh_ctx {
   bool vanity = false;
   std::vector<uint8_t> v_ranges;
   uint32_t probe_len = 20;
+  uint32_t rmd_batch = 0;  // kh_set_rmd_batch: 0 = the ordinary walk, else the reference's group < 1024
   bloom_desc tbd{};
   uint64_t t_entries = 0;  // the target bloom's struct bloom `entries`
   std::vector<uint8_t> h_tbloom;
@@ -708,6 +709,21 @@ int kh_set_geometry(kh_ctx *ctx, uint32_t lanes, uint32_t groups_per_launch) {
   return KH_OK;
 }
 
+int kh_set_rmd_batch(kh_ctx *ctx, uint32_t group) {
+  if (!ctx) return KH_E_ARG;
+  if (group == 0 || group == 2 * KH_WALK_H) {
+    ctx->rmd_batch = 0;
+    return KH_OK;
+  }
+  if (group < 4 || group > 2 * KH_WALK_H || group % 4) {
+    ctx->err = "rmd batch size: a multiple of 4 in [4, 1024] (keyhunt.cpp:815-829 clamps to that)";
+    return KH_E_ARG;
+  }
+  ctx->rmd_batch = group;
+  ctx->cont_valid = false;
+  return KH_OK;
+}
+
 int kh_synchronize(kh_ctx *ctx) {
   if (!ctx) return KH_E_ARG;
   (void)hipSetDevice(ctx->device);
@@ -793,10 +809,17 @@ int kh_set_vanity(kh_ctx *ctx, const uint8_t *ranges, uint64_t n, uint32_t probe
 
 int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride_be[32], uint64_t n_keys, uint32_t mode,
             uint32_t search, kh_hit *hits, uint32_t cap, uint32_t *n_hits) {
-  if (!ctx || !start || !n_hits || (n_keys % (2 * KH_WALK_H)) || n_keys == 0) return KH_E_ARG;
+  if (!ctx || !start || !n_hits || n_keys == 0) return KH_E_ARG;
+  // --rmd-batch-size below 1024: groups of zg slots (kh_set_rmd_batch, k_walk_zinv)
+  const uint32_t zg = ctx->rmd_batch;
+  if (!zg && n_keys % (2 * KH_WALK_H)) return KH_E_ARG;
   const bool endo = (mode & KH_MODE_ENDO) != 0;
   mode &= ~(uint32_t)KH_MODE_ENDO;
   if (mode > KH_MODE_ETH || search > KH_SEARCH_BOTH) return KH_E_ARG;
+  if (zg && (mode == KH_MODE_XPOINT || ctx->vanity)) {
+    ctx->err = "--rmd-batch-size applies to -m rmd160 (hash160 or -c eth) with exact targets only";
+    return KH_E_ARG;
+  }
   if (!ctx->d_tbloom) return KH_E_STATE;
   (void)hipSetDevice(ctx->device);
   int km = mode == KH_MODE_XPOINT ? KM_XPOINT
@@ -813,14 +836,28 @@ int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride_be[32], u
   // reaches the group order keeps the reference's 1024-key groups: there a centre can equal
   // -(i+1)*stride*G, whose zero difference collapses the group's batch inversion (parity note 4),
   // and only the reference's own geometry collapses the same groups (fixtures *_near_order)
-  const int H = ((km == KM_XPOINT || km == KM_H160C) && n_keys % (2 * KH_WALK_HB) == 0 &&
-                 !reaches_order(st, stride, n_keys + 4 * KH_WALK_HB) && !getenv("KH_NO_BIG_GROUPS"))
+  const int H = zg ? (int)(zg / 2)
+                : ((km == KM_XPOINT || km == KM_H160C) && n_keys % (2 * KH_WALK_HB) == 0 &&
+                   !reaches_order(st, stride, n_keys + 4 * KH_WALK_HB) && !getenv("KH_NO_BIG_GROUPS"))
                     ? KH_WALK_HB
                     : KH_WALK_H;
   const uint32_t *tab = nullptr;
   int r;
 
-  uint64_t total_groups = n_keys / (2 * H);
+  // m * stride mod n (m < 2^128): double-and-add over the bits of m
+  auto mul_stride = [&](u128 m) {
+    if (u256_cmp(stride, u256_u64(1)) == 0) return sc_reduce(u256_from_u128(m));
+    u256 acc = u256_u64(0), x = stride;
+    for (int b = 0; b < 128; b++) {
+      if ((m >> b) & 1) acc = sc_add(acc, x);
+      x = sc_add(x, x);
+    }
+    return acc;
+  };
+  // the reference's do-while runs whole groups (keyhunt.cpp:3350, 3836): a chunk that is no
+  // multiple of the group overshoots its end
+  uint64_t total_groups = (n_keys + 2 * H - 1) / (2 * H);
+  const uint64_t n_points = total_groups * 2 * H;
   job_geom jg = plan(ctx, total_groups, 0);
   // large-group modes interleave lanes (lane g walks groups g, g + L, ...) when the lanes divide
   // the chunk: after the call every lane sits on its group of the chunk that follows, so a call
@@ -835,17 +872,7 @@ int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride_be[32], u
   std::vector<u256> s(resume ? 0 : jg.L);
   for (uint32_t g = 0; g < s.size(); g++) {
     u128 off = inter ? (u128)g * (2 * H) + H : (u128)g * jg.gpl * (2 * H) + H;
-    u256 o = sc_reduce(u256_from_u128(off));
-    if (u256_cmp(stride, u256_u64(1)) != 0) {
-      // o * stride mod n (o < 2^128): double-and-add over the bits of o
-      u256 acc = u256_u64(0), x = stride;
-      for (int b = 0; b < 128; b++) {
-        if ((off >> b) & 1) acc = sc_add(acc, x);
-        x = sc_add(x, x);
-      }
-      o = acc;
-    }
-    s[g] = sc_add(st, o);
+    s[g] = sc_add(st, mul_stride(off));
     if (u256_is_zero(s[g])) {
       ctx->err = "lane centre scalar is 0 mod n";
       return KH_E_ARG;
@@ -867,7 +894,8 @@ int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride_be[32], u
   A.L = jg.L;
   A.lane_stride = jg.gpl * 2 * H;
   A.interleave = inter ? 1 : 0;
-  A.n_points = n_keys;
+  A.n_points = n_points;
+  A.zhalf = zg ? (uint32_t)H : 0;
   A.bloom = ctx->d_tbloom;
   A.bd = ctx->tbd;
   A.tblk = ctx->vanity || getenv("KH_REF_TARGET_BLOOM") ? nullptr : ctx->d_tblk;
@@ -897,19 +925,7 @@ int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride_be[32], u
     A.hit_cap = ctx->hit_cap;
     if (s.empty()) {  // resumed lanes: compute their start scalars for the redo
       s.resize(jg.L);
-      for (uint32_t g = 0; g < jg.L; g++) {
-        u128 off = (u128)g * (2 * H) + H;
-        u256 o = sc_reduce(u256_from_u128(off));
-        if (u256_cmp(stride, u256_u64(1)) != 0) {
-          u256 acc = u256_u64(0), x = stride;
-          for (int b = 0; b < 128; b++) {
-            if ((off >> b) & 1) acc = sc_add(acc, x);
-            x = sc_add(x, x);
-          }
-          o = acc;
-        }
-        s[g] = sc_add(st, o);
-      }
+      for (uint32_t g = 0; g < jg.L; g++) s[g] = sc_add(st, mul_stride((u128)g * (2 * H) + H));
     }
     r = run_setup(ctx, s, nullptr);  // the walk moved the lane centres on: start them again
     if (r) return r;
@@ -965,23 +981,33 @@ int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride_be[32], u
       fe{{0x8e6afa40u, 0x3ec693d6u, 0xed0a766au, 0x630fb68au, 0x53cbcb16u, 0x919bb861u, 0x9a83f8efu, 0x851695d4u}}};
   std::vector<kh_hit> out;
   for (auto &h : dh) {
-    u256 k = sc_add(st, sc_reduce(u256_from_u128((u128)h.idx)));
-    if (u256_cmp(stride, u256_u64(1)) != 0) {
-      u256 acc = u256_u64(0), x = stride;
-      for (int b = 0; b < 64; b++) {
-        if ((h.idx >> b) & 1) acc = sc_add(acc, x);
-        x = sc_add(x, x);
-      }
-      k = sc_add(st, acc);
-    }
+    const u256 k = sc_add(st, mul_stride((u128)h.idx));
     ge P;
     if (!ctx->comb.mult(P, k)) continue;
     const uint32_t base = h.kind & 15u, e = (h.kind >> KH_DKIND_ENDO_SHIFT) & 3u;
     const bool neg = (h.kind & KH_DKIND_NEG) != 0;
     if (e > 2) continue;
-    fe xe = P.x, ye = P.y;
-    if (e) fe_mul(xe, P.x, BETA[e]);
-    if (neg) fe_neg(ye, P.y);
+    // the point the walk produced at this slot: k*G, or with --rmd-batch-size < 1024 and a slot
+    // other than its group's centre, x = -(C.x + (i+1)D.x), y = -+(i+1)D.y (k_walk_zinv)
+    ge S = P;
+    bool garbage = false;
+    if (zg && h.idx % zg != (uint64_t)H) {
+      const uint64_t grp = h.idx / zg, t = h.idx % zg;
+      const uint64_t i = t > (uint64_t)H ? t - H - 1 : H - t - 1;
+      ge C, Di;
+      if (!ctx->comb.mult(C, sc_add(st, mul_stride((u128)grp * zg + H))) ||
+          !ctx->comb.mult(Di, mul_stride((u128)(i + 1))))
+        continue;
+      fe sx;
+      fe_add(sx, C.x, Di.x);
+      fe_neg(S.x, sx);
+      S.y = Di.y;
+      if (t > (uint64_t)H) fe_neg(S.y, Di.y);
+      garbage = true;
+    }
+    fe xe = S.x, ye = S.y;
+    if (e) fe_mul(xe, S.x, BETA[e]);
+    if (neg) fe_neg(ye, S.y);
     uint8_t probe[20];
     uint32_t w[5];
     bool compressed = false;
@@ -992,7 +1018,7 @@ int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride_be[32], u
       hash160_uncomp(xe, ye, w);
     } else if (base == KH_KIND_ETH) {
       if (endo && e == 2 && !neg)  // the slot-4 twin: its image is eth(beta P)
-        fe_mul(xe, P.x, BETA[1]);
+        fe_mul(xe, S.x, BETA[1]);
       eth_address(xe, ye, w);
     } else {
       for (int j = 0; j < 5; j++) w[j] = bswap32(xe.d[7 - j]);
@@ -1012,8 +1038,13 @@ int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride_be[32], u
     u256 kr = e ? sc_mul(k, LAMBDA[e]) : k;  // (beta^e x, y) = lambda^e * (x, y)
     if (base == KH_KIND_ETH && endo && e == 2 && !neg) {
       kr = sc_neg(kr);  // the slot-4 twin: lambda^2 k gives (beta^2 X, Y), not the image: negated
+    } else if (garbage && (compressed ? !endo : endo)) {
+      // where the reference checks the found key's own image against the hit -- compressed without
+      // -e (keyhunt.cpp:3619-3636), 04 and eth with -e (3652-3680, 3714-3744) -- a point that is no
+      // multiple of G never matches it: negated
+      kr = sc_neg(kr);
     } else if (compressed) {
-      uint32_t odd = P.y.d[0] & 1;  // the image keeps Y
+      uint32_t odd = P.y.d[0] & 1;  // the image keeps Y; -e: the slot key's parity (3565-3600)
       if (odd != (base == KH_KIND_03 ? 1u : 0u)) kr = sc_neg(kr);
     } else if (neg) {
       kr = sc_neg(kr);

@@ -178,6 +178,8 @@ struct walk_args {
   uint32_t *rows_val;
   // dump
   uint32_t *dump_x, *dump_y;
+  // k_walk_zinv: half of the --rmd-batch-size group (groups of 2 * zhalf slots)
+  uint32_t zhalf;
 };
 
 struct setup_args {
@@ -213,6 +215,7 @@ struct refine_args {
 
 namespace kh {
 hipError_t launch_walk(int mode, const walk_args &A, hipStream_t st, int H = KH_WALK_H);
+hipError_t launch_walk_zinv(int mode, const walk_args &A, hipStream_t st);
 hipError_t launch_refine(const refine_args &A, hipStream_t st);
 hipError_t launch_setup(const setup_args &A, hipStream_t st);
 hipError_t launch_test_hash160(const uint32_t *xs, const uint32_t *ys, uint32_t n, uint32_t *out, hipStream_t st);

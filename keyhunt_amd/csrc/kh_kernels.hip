@@ -714,6 +714,61 @@ __global__ void __launch_bounds__((walk_threads<MODE, H>()), (walk_blocks_per_cu
 }
 
 // ------------------------------------------------------------------------------------------
+// -m rmd160 --rmd-batch-size G < 1024 (keyhunt.cpp:815-829, 3274, 3301-3307, 3349-3461): the
+// reference's batch inversion then runs over its first G/2 + 1 slots and leaves the rest of its
+// 513-entry IntGroup zero, so the product, its inverse and every derived inverse are 0
+// (IntGroup.cpp:36-58).  With s = 0 each non-centre point of a group degenerates to
+// x = -(C.x + T[i].x), y = -T[i].y (slot H + i + 1) or +T[i].y (slot H - i - 1), slot 0 using
+// T[H - 1]; only the centre C is a real point.  The next group's centre is recomputed from its key
+// (3350-3354): C += T[H] with its own inversion here.  One lane walks its groups of 2H = G slots.
+// ------------------------------------------------------------------------------------------
+template <int MODE>
+__global__ void __launch_bounds__(256, KH_WALK_LB_HASH) k_walk_zinv(walk_args A) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= A.L) return;
+  kconst_ptr T = (kconst_ptr)A.tab;  // (H+1) x {x[8], y[8]}
+  const int H = (int)A.zhalf;
+  fe cx, cy;
+  load_soa(cx, A.cx, A.L, g);
+  load_soa(cy, A.cy, A.L, g);
+  for (uint32_t j = 0; j < A.groups; j++) {
+    const uint64_t cidx = (uint64_t)g * A.lane_stride + (uint64_t)(A.group_base + j) * (2 * H) + H;
+    probe_point<MODE>(A, cx, cy, cidx);
+#pragma unroll 1
+    for (int i = 0; i < H; i++) {
+      fe tx, ty, x, s;
+      load_fe_k(tx, T + i * 16);
+      load_fe_k(ty, T + i * 16 + 8);
+      fe_add(s, cx, tx);
+      fe_neg(x, s);
+      probe_point<MODE>(A, x, ty, cidx - (uint64_t)(i + 1));  // C - T[i] side: y = +T[i].y
+      if (i < H - 1) {
+        fe nty;
+        fe_neg(nty, ty);
+        probe_point<MODE>(A, x, nty, cidx + (uint64_t)(i + 1));  // C + T[i] side: y = -T[i].y
+      }
+    }
+    fe t2x, t2y, dx, dy, s, s2, nx, ny, t;
+    load_fe_k(t2x, T + H * 16);
+    load_fe_k(t2y, T + H * 16 + 8);
+    fe_sub(dx, t2x, cx);
+    fe_inv(dx, dx);
+    fe_sub(dy, t2y, cy);
+    fe_mul(s, dy, dx);
+    fe_sqr(s2, s);
+    fe_sub(nx, s2, cx);
+    fe_sub(nx, nx, t2x);
+    fe_sub(t, t2x, nx);
+    fe_mul(ny, s, t);
+    fe_sub(ny, ny, t2y);
+    cx = nx;
+    cy = ny;
+  }
+  store_soa(A.cx, A.L, g, cx);
+  store_soa(A.cy, A.L, g, cy);
+}
+
+// ------------------------------------------------------------------------------------------
 // Lane setup: C_g = [Q +] s_g * G with a fixed-base byte comb, comb[j][v] = v * 2^(8j) * G.
 // Bytes are added from least to most significant, so the accumulator is always (partial
 // scalar)*G with partial < 2^(8j) while comb[j][v] >= 2^(8j): the mixed addition never meets
@@ -993,6 +1048,7 @@ __global__ void k_test_bloom(const uint8_t *items, uint32_t n, uint32_t len, con
 namespace kh {
 
 hipError_t launch_walk(int mode, const walk_args &A, hipStream_t st, int H) {
+  if (A.zhalf) return launch_walk_zinv(mode, A, st);
   dim3 block(256), grid((A.L + 255) / 256);
   if (KH_XPOINT_DEFER && mode == KM_XPOINT && A.tblk) mode = KM_XPOINTB;
   if (KH_H160_BLK && mode == KM_H160C && A.tblk) mode = KM_H160CB;
@@ -1035,6 +1091,23 @@ hipError_t launch_walk(int mode, const walk_args &A, hipStream_t st, int H) {
     case KM_H160B | KM_ENDO: hipLaunchKernelGGL(k_walk<KM_H160B | KM_ENDO>, grid, block, 0, st, A); break;
     case KM_XPOINT | KM_ENDO: hipLaunchKernelGGL(k_walk<KM_XPOINT | KM_ENDO>, grid, block, 0, st, A); break;
     case KM_ETH | KM_ENDO: hipLaunchKernelGGL(k_walk<KM_ETH | KM_ENDO>, grid, block, 0, st, A); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_walk_zinv(int mode, const walk_args &A, hipStream_t st) {
+  dim3 block(256), grid((A.L + 255) / 256);
+  if (A.zhalf < 2 || A.zhalf > KH_WALK_H) return hipErrorInvalidValue;
+  switch (mode) {
+    case KM_H160C: hipLaunchKernelGGL(k_walk_zinv<KM_H160C>, grid, block, 0, st, A); break;
+    case KM_H160U: hipLaunchKernelGGL(k_walk_zinv<KM_H160U>, grid, block, 0, st, A); break;
+    case KM_H160B: hipLaunchKernelGGL(k_walk_zinv<KM_H160B>, grid, block, 0, st, A); break;
+    case KM_H160C | KM_ENDO: hipLaunchKernelGGL(k_walk_zinv<KM_H160C | KM_ENDO>, grid, block, 0, st, A); break;
+    case KM_H160U | KM_ENDO: hipLaunchKernelGGL(k_walk_zinv<KM_H160U | KM_ENDO>, grid, block, 0, st, A); break;
+    case KM_H160B | KM_ENDO: hipLaunchKernelGGL(k_walk_zinv<KM_H160B | KM_ENDO>, grid, block, 0, st, A); break;
+    case KM_ETH: hipLaunchKernelGGL(k_walk_zinv<KM_ETH>, grid, block, 0, st, A); break;
+    case KM_ETH | KM_ENDO: hipLaunchKernelGGL(k_walk_zinv<KM_ETH | KM_ENDO>, grid, block, 0, st, A); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

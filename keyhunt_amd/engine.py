@@ -78,6 +78,7 @@ def lib() -> ctypes.CDLL:
     L.kh_close.argtypes = [P]
     L.kh_set_geometry.argtypes = [P, ctypes.c_uint32, ctypes.c_uint32]
     L.kh_synchronize.argtypes = [P]
+    L.kh_set_rmd_batch.argtypes = [P, ctypes.c_uint32]
     L.kh_set_targets.argtypes = [P, u8p, ctypes.c_uint64, ctypes.c_uint64]
     L.kh_scan.argtypes = [P, u8p, u8p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(KhHit),
                           ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]
@@ -167,6 +168,10 @@ class Engine:
 
     def set_geometry(self, lanes: int = 0, groups_per_launch: int = 0) -> None:
         self._chk(lib().kh_set_geometry(self._ctx, lanes, groups_per_launch), "kh_set_geometry")
+
+    def set_rmd_batch(self, group: int) -> None:
+        """-m rmd160 --rmd-batch-size: the reference's clamped group size (1024 = the ordinary walk)."""
+        self._chk(lib().kh_set_rmd_batch(self._ctx, group), "kh_set_rmd_batch")
 
     def synchronize(self) -> None:
         self._chk(lib().kh_synchronize(self._ctx), "kh_synchronize")

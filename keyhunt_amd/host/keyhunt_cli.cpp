@@ -153,13 +153,14 @@ struct options {
   uint64_t mapped_entries = 0;   // mapped_entries_override
   long double mapped_error = 0;  // mapped_error_override
   uint32_t mapped_chunks = 1;
+  int rmd_batch = 1024;  // --rmd-batch-size (keyhunt.cpp:301, 815-829), -m rmd160 only
 } opt;
 // keyhunt.cpp:419; ggsb and angrygiant walk like sequential (ggsb with BSGS_STEP = 2 x block size)
 const char *BSGS_MODES[7] = {"sequential", "backward", "both", "random", "dance", "ggsb", "angrygiant"};
 enum { BM_SEQUENTIAL, BM_BACKWARD, BM_BOTH, BM_RANDOM, BM_DANCE, BM_GGSB, BM_ANGRYGIANT };
 
 std::mutex g_keys_mtx, g_cursor_mtx;
-std::atomic<uint64_t> g_groups_done{0};  // 1024-key groups (address family)
+std::atomic<uint64_t> g_groups_done{0};  // groups walked (address family): 1024 keys each in the stats
 std::atomic<uint64_t> g_bases_done{0};   // BSGS bases
 std::atomic<int> g_running{0};
 U g_cursor;
@@ -773,6 +774,11 @@ void addr_worker(addr_job *j) {
     printf("[+] Writing file %s ........\n", j->data_file);
     r = kh_targets_save(ctx, j->data_file);
   }
+  // --rmd-batch-size below 1024: the reference's groups of that size (thread_process,
+  // keyhunt.cpp:3301-3307 -- FLAGMODE == MODE_RMD160 only), each counted as 1024 keys in the stats
+  // (steps[] x CPU_GRP_SIZE, 2847-2880) like every group
+  const uint64_t group = opt.mode == MODE_RMD160 ? (uint64_t)opt.rmd_batch : 1024;
+  if (!r && group != 1024) r = kh_set_rmd_batch(ctx, (uint32_t)group);
   if (r) fprintf(stderr, "[E] GPU %d: %s (%s)\n", j->device, kh_strerror(r), kh_last_error(ctx));
   std::vector<kh_hit> hits(1 << 16);
   uint8_t st_be[32], stride_be[32];
@@ -815,7 +821,7 @@ void addr_worker(addr_job *j) {
       else
         writekey(ctx, hits[i].compressed != 0, hits[i].key);
     }
-    g_groups_done += j->nseq / 1024;
+    g_groups_done += (j->nseq + group - 1) / group;
   }
   j->rc = r;
   kh_close(ctx);
@@ -1169,7 +1175,7 @@ void usage(const char *p) {
   printf("Usage: %s -m address|rmd160|xpoint|bsgs -f FILE [-b BITS | -r START:END] [-l compress|uncompress|both]\n"
          "       [-n N] [-k K] [-I STRIDE] [-g GPUS] [-q] [-s SECONDS] [-M] [-L blocked|reference]\n"
          "       [-e] [-c btc|eth] [-R] [-B sequential|backward|both|random|dance|angrygiant] [-S] [-6]\n"
-         "       [-z MULT] [-m vanity -v PREFIX ...] [-d] [-h]\n", p);
+         "       [-z MULT] [-m vanity -v PREFIX ...] [--rmd-batch-size N] [-d] [-h]\n", p);
 }
 
 }  // namespace
@@ -1194,6 +1200,7 @@ int main(int argc, char **argv) {
                                            {"bloom-bytes", required_argument, 0, 12},
                                            {"create-mapped", optional_argument, 0, 13},
                                            {"tmpdir", required_argument, 0, 14},
+                                           {"rmd-batch-size", required_argument, 0, 15},
                                            {0, 0, 0, 0}};
   // --mapped-size / --bloom-bytes / --create-mapped N: the entry count and error the byte budget
   // allows (bloom_entries_for_bytes, keyhunt.cpp:7510-7530)
@@ -1266,6 +1273,17 @@ int main(int argc, char **argv) {
         if (optarg) size_override(strtoull(optarg, NULL, 10));
         break;
       case 14: break;  // --tmpdir: where the reference puts an unnamed bP table mapping; unused here
+      case 15: {       // keyhunt.cpp:815-829: clamped to [4, 1024], rounded down to a multiple of 4
+        long v = strtol(optarg, NULL, 10);
+        if (v < 4) v = 4;
+        if (v > 1024) v = 1024;
+        if (v % 4) {
+          v -= v % 4;
+          if (v < 4) v = 4;
+        }
+        opt.rmd_batch = (int)v;
+        break;
+      }
       case 'm': {
         int m = -1;
         for (int i = 0; i < 5; i++)

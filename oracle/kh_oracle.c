@@ -659,18 +659,24 @@ static void batch_inv(fe *a, int n) {
   a[0] = inv;
   free(sub);
 }
-/* one group from centre C (affine, with y): pts[0..1023], next centre written to *next */
-static void walk_group(const walk_tab *t, const ge *c, ge *pts, int need_y, ge *next) {
+/* one group of 2*half points from centre C (affine, with y): pts[0..2*half), next centre written
+ * to *next.  half = HALF is the reference's 1024-key group.  A smaller half is -m rmd160
+ * --rmd-batch-size 2*half (keyhunt.cpp:3301-3307, 3349-3461): the reference still inverts its
+ * whole IntGroup of HALF + 1 elements (3274), of which only dx[0..half] are ever set -- the rest
+ * keep Int's zero -- so the product and every inverse are 0 (IntGroup.cpp:36-58, ModInv(0) = 0),
+ * as they are here: the same formulas then give the reference's points. */
+static void walk_group_n(const walk_tab *t, const ge *c, ge *pts, int need_y, ge *next, int half) {
   fe dx[HALF + 1];
   int i;
-  for (i = 0; i < HALF; i++) fe_sub(&dx[i], &t->gn[i].x, &c->x);
-  fe_sub(&dx[HALF], &t->g2n.x, &c->x);
+  memset(dx, 0, sizeof dx);
+  for (i = 0; i < half; i++) fe_sub(&dx[i], &t->gn[i].x, &c->x);
+  fe_sub(&dx[half], &t->g2n.x, &c->x);
   batch_inv(dx, HALF + 1);
-  pts[HALF] = *c;
-  for (i = 0; i < HALF; i++) {
+  pts[half] = *c;
+  for (i = 0; i < half; i++) {
     fe dy, s, p2, tmp;
     /* c + Gn[i] */
-    if (i < HALF - 1) {
+    if (i < half - 1) {
       ge pp;
       fe_sub(&dy, &t->gn[i].y, &c->y);
       fe_mul(&s, &dy, &dx[i]);
@@ -679,7 +685,7 @@ static void walk_group(const walk_tab *t, const ge *c, ge *pts, int need_y, ge *
       if (need_y) { fe_sub(&tmp, &t->gn[i].x, &pp.x); fe_mul(&pp.y, &tmp, &s); fe_sub(&pp.y, &pp.y, &t->gn[i].y); }
       else memset(&pp.y, 0, sizeof(fe));
       pp.inf = 0;
-      pts[HALF + i + 1] = pp;
+      pts[half + i + 1] = pp;
     }
     /* c - Gn[i] */
     ge pn; fe ny;
@@ -691,17 +697,20 @@ static void walk_group(const walk_tab *t, const ge *c, ge *pts, int need_y, ge *
     if (need_y) { fe_sub(&tmp, &t->gn[i].x, &pn.x); fe_mul(&pn.y, &tmp, &s); fe_add(&pn.y, &pn.y, &t->gn[i].y); }
     else memset(&pn.y, 0, sizeof(fe));
     pn.inf = 0;
-    pts[HALF - i - 1] = pn;
+    pts[half - i - 1] = pn;
   }
   if (next) {
     fe dy, s, p2, tmp;
     fe_sub(&dy, &t->g2n.y, &c->y);
-    fe_mul(&s, &dy, &dx[HALF]);
+    fe_mul(&s, &dy, &dx[half]);
     fe_sqr(&p2, &s);
     fe_sub(&next->x, &p2, &c->x); fe_sub(&next->x, &next->x, &t->g2n.x);
     fe_sub(&tmp, &t->g2n.x, &next->x); fe_mul(&next->y, &tmp, &s); fe_sub(&next->y, &next->y, &t->g2n.y);
     next->inf = 0;
   }
+}
+static void walk_group(const walk_tab *t, const ge *c, ge *pts, int need_y, ge *next) {
+  walk_group_n(t, c, pts, need_y, next, HALF);
 }
 
 /* X coordinates (and optionally Y) of keys K + t*stride for t in [0, n_groups*1024), computed by
@@ -766,7 +775,7 @@ static void push_hit(or_hit *hits, int cap, int *nh, const fe *k, int compressed
  * variants also over (X, -Y).  Kinds: base (0: 02, 1: 03, 2: 04, 3: xpoint) | e << 4 | neg << 6.
  * scan_groups does groups [g0, g1) of the chunk into its own hit list. */
 typedef struct {
-  int mode, search, endo;
+  int mode, search, endo, grp;  /* grp: keys per group (1024, or --rmd-batch-size) */
   fe start;
   uint64_t g0, g1;
   const uint8_t *rows; int64_t n_rows; const uint8_t *bf; uint64_t bits; uint32_t hashes;
@@ -785,14 +794,24 @@ static void *scan_groups(void *arg) {
   int nh = 0;
   int need_y = (search == 1 || search == 2 || mode == 2);
   int ne = endo ? 3 : 1;
+  const int grp = J->grp;
   fe key, one = {{1, 0, 0, 0}};
-  u256_add_u64(&key, &J->start, J->g0 * GRP);
-  uint8_t onebe[32]; fe_to_be(onebe, &one);
+  u256_add_u64(&key, &J->start, J->g0 * (uint64_t)grp);
+  walk_tab *wt = (walk_tab *)malloc(sizeof(walk_tab));
+  build_walk_tab(wt, &one);
+  ge *pts = (ge *)malloc(sizeof(ge) * GRP);
   uint8_t *xs = (uint8_t *)malloc(GRP * 32), *ys = (uint8_t *)malloc(GRP * 32);
   for (uint64_t g = J->g0; g < J->g1; g++) {
-    uint8_t kb[32]; fe_to_be(kb, &key);
-    or_walk_points(kb, onebe, 1, xs, need_y ? ys : 0);
-    for (int t = 0; t < GRP; t++) {
+    /* the centre from its key (keyhunt.cpp:3349-3353), then the group's points */
+    fe ck; ge c;
+    u256_add_u64(&ck, &key, (uint64_t)(grp / 2));
+    scalar_mult_g(&c, &ck);
+    walk_group_n(wt, &c, pts, need_y, 0, grp / 2);
+    for (int t = 0; t < grp; t++) {
+      fe_to_be(xs + t * 32, &pts[t].x);
+      fe_to_be(ys + t * 32, &pts[t].y);
+    }
+    for (int t = 0; t < grp; t++) {
       fe kf; u256_add_u64(&kf, &key, (uint64_t)t);
       fe x0; fe_from_be(&x0, xs + t * 32);
       uint8_t xe[3][32];
@@ -819,12 +838,20 @@ static void *scan_groups(void *arg) {
           uint8_t h[20];
           or_hash160_comp(xe[e], (uint8_t)(2 + pfx), h);
           if (or_bloom_check(bf, bits, hashes, h, 20) && or_searchbinary(rows, n_rows, h, 20, 0)) {
-            /* keyhunt.cpp:3525-3600 / 3619-3636: the image keeps Y; negate when its parity
-               disagrees with the matched prefix */
+            /* -e (keyhunt.cpp:3565-3600): the image keeps Y; negate when the slot key's parity
+               disagrees with the matched prefix.  Without -e (3619-3636): negate unless the slot
+               key's own compressed hash is the match */
             ge P; scalar_mult_g(&P, &kf);
             fe kr; sc_mul(&kr, &kf, &END_LAMBDA[e]);
-            int odd = (int)(P.y.v[0] & 1);
-            if (odd != pfx) sc_neg(&kr, &kr);
+            if (endo) {
+              int odd = (int)(P.y.v[0] & 1);
+              if (odd != pfx) sc_neg(&kr, &kr);
+            } else {
+              uint8_t px[32], h2[20];
+              fe_to_be(px, &P.x);
+              or_hash160_comp(px, (uint8_t)(2 + (P.y.v[0] & 1)), h2);
+              if (memcmp(h2, h, 20) != 0) sc_neg(&kr, &kr);
+            }
             push_hit(hits, cap, &nh, &kr, 1, pfx | (e << 4));
           }
         }
@@ -852,25 +879,27 @@ static void *scan_groups(void *arg) {
         }
       }
     }
-    fe k1024 = {{GRP, 0, 0, 0}};
-    u256_add(&key, &key, &k1024);
+    u256_add_u64(&key, &key, (uint64_t)grp);
   }
-  free(xs); free(ys);
+  free(xs); free(ys); free(pts); free(wt);
   J->nh = nh;
   return 0;
 }
 
 /* the chunk on up to 16 threads (contiguous group ranges, hits concatenated in key order) */
-int or_scan_chunk2(int mode, int search, int endo, const uint8_t start_be[32], uint64_t n_keys,
+/* grp: keys per group -- 1024, or -m rmd160 --rmd-batch-size (a multiple of 4 below 1024): the
+ * chunk is then ceil(n_keys / grp) whole groups (the reference's do-while, keyhunt.cpp:3350-3836) */
+int or_scan_chunk3(int mode, int search, int endo, int grp, const uint8_t start_be[32], uint64_t n_keys,
                    const uint8_t *rows, int64_t n_rows, const uint8_t *bf, uint64_t bits, uint32_t hashes,
                    or_hit *hits, int cap) {
-  uint64_t groups = n_keys / GRP;
+  if (grp < 4 || grp > GRP || grp % 4) return -1;
+  uint64_t groups = (n_keys + grp - 1) / grp;
   int nt = (int)(groups < 16 ? (groups ? groups : 1) : 16);
   scan_job *jobs = (scan_job *)calloc(nt, sizeof(scan_job));
   pthread_t *th = (pthread_t *)calloc(nt, sizeof(pthread_t));
   for (int i = 0; i < nt; i++) {
     scan_job *J = &jobs[i];
-    J->mode = mode; J->search = search; J->endo = endo;
+    J->mode = mode; J->search = search; J->endo = endo; J->grp = grp;
     fe_from_be(&J->start, start_be);
     J->g0 = groups * i / nt; J->g1 = groups * (i + 1) / nt;
     J->rows = rows; J->n_rows = n_rows; J->bf = bf; J->bits = bits; J->hashes = hashes;
@@ -888,6 +917,12 @@ int or_scan_chunk2(int mode, int search, int endo, const uint8_t start_be[32], u
   }
   free(jobs); free(th);
   return nh;
+}
+
+int or_scan_chunk2(int mode, int search, int endo, const uint8_t start_be[32], uint64_t n_keys,
+                   const uint8_t *rows, int64_t n_rows, const uint8_t *bf, uint64_t bits, uint32_t hashes,
+                   or_hit *hits, int cap) {
+  return or_scan_chunk3(mode, search, endo, GRP, start_be, n_keys, rows, n_rows, bf, bits, hashes, hits, cap);
 }
 
 int or_scan_chunk(int mode, int search, const uint8_t start_be[32], uint64_t n_keys,

@@ -108,6 +108,17 @@ E2E_RUNS = [
     # a key exactly at a base start: keyhunt's worker reaches it only through the point at infinity
     # and misses it (bsgsd has an extra per-base test and finds it, tests/golden/ref_bsgsd.json)
     ("bsgs_63_key_at_base", ["-m", "bsgs", "-f", "63.pub", "-n", "0x1000000", "-k", "2", "-r", "7cce5efdaccf6808:7cce5efdadcf6808", "-t", "8"], 300),
+    # --rmd-batch-size below 1024 (keyhunt.cpp:815-829, 3301-3461): groups of G whose batch
+    # inversion returns 0, so only each group's centre is a real point (targets from
+    # tests/golden/make_rmd_batch_targets.py); 1001 rounds down to 1000, eth walks the same points
+    ("rmd160_batch512_compress", ["-m", "rmd160", "-f", "rmd_batch.rmd", "-l", "compress", "--rmd-batch-size", "512", "-r", "10000:20ffff", "-n", "0x100000", "-t", "8"], 300),
+    ("rmd160_batch512_both", ["-m", "rmd160", "-f", "rmd_batch.rmd", "-l", "both", "--rmd-batch-size", "512", "-r", "10000:20ffff", "-n", "0x100000", "-t", "8"], 300),
+    ("rmd160_batch512_both_endo", ["-m", "rmd160", "-f", "rmd_batch.rmd", "-l", "both", "-e", "--rmd-batch-size", "512", "-r", "10000:20ffff", "-n", "0x100000", "-t", "8"], 300),
+    ("rmd160_batch1000_compress", ["-m", "rmd160", "-f", "rmd_batch.rmd", "-l", "compress", "--rmd-batch-size", "1000", "-r", "10000:20ffff", "-n", "0x100000", "-t", "8"], 300),
+    ("rmd160_batch1000_both", ["-m", "rmd160", "-f", "rmd_batch.rmd", "-l", "both", "--rmd-batch-size", "1000", "-r", "10000:20ffff", "-n", "0x100000", "-t", "8"], 300),
+    ("rmd160_batch1001_compress_endo", ["-m", "rmd160", "-f", "rmd_batch.rmd", "-l", "compress", "-e", "--rmd-batch-size", "1001", "-r", "10000:20ffff", "-n", "0x100000", "-t", "8"], 300),
+    ("rmd160_batch1024_both", ["-m", "rmd160", "-f", "rmd_batch.rmd", "-l", "both", "--rmd-batch-size", "1024", "-r", "10000:20ffff", "-n", "0x100000", "-t", "8"], 300),
+    ("rmd160_eth_batch8", ["-m", "rmd160", "-c", "eth", "-f", "eth_targets.rmd", "--rmd-batch-size", "8", "-r", "1:100000", "-n", "0x100000", "-t", "8"], 300),
     # no range at all: sequential from 1 (keyhunt.cpp:1250-1255)
     ("address_1to32_no_range", ["-m", "address", "-f", "1to32.txt", "-l", "compress", "-n", "0x100000", "-t", "8"], 20),
 ]

@@ -199,16 +199,18 @@ SEARCH_COMPRESS, SEARCH_UNCOMPRESS, SEARCH_BOTH = 0, 1, 2
 
 
 def scan_chunk(mode: int, search: int, start: int, n_keys: int, rows: list[bytes], cap: int = 4096,
-               endo: bool = False):
+               endo: bool = False, group: int = 1024):
     """Reference hit list for one chunk (thread_process).  rows: 20-byte targets (unsorted ok).
-    endo: -e (kinds then carry the image e << 4 and, for 04 hashes, the Y sign << 6)."""
+    endo: -e (kinds then carry the image e << 4 and, for 04 hashes, the Y sign << 6).  group:
+    -m rmd160 --rmd-batch-size after the reference's clamping (kh_oracle.c walk_group_n)."""
     srt = sorted(rows)
     table = b"".join(srt)
     bloom = Bloom(len(srt))
     for r in srt:
         bloom.add(r)
     hits = (OrHit * cap)()
-    n = lib().or_scan_chunk2(ctypes.c_int(mode), ctypes.c_int(search), ctypes.c_int(1 if endo else 0), be32(start),
+    n = lib().or_scan_chunk3(ctypes.c_int(mode), ctypes.c_int(search), ctypes.c_int(1 if endo else 0),
+                             ctypes.c_int(group), be32(start),
                              ctypes.c_uint64(n_keys),
                             table, ctypes.c_int64(len(srt)), bloom.bf, ctypes.c_uint64(bloom.bits),
                             ctypes.c_uint32(bloom.hashes), hits, ctypes.c_int(cap))

@@ -1,0 +1,93 @@
+"""-m rmd160 --rmd-batch-size G < 1024 on the GPU (kh_set_rmd_batch, k_walk_zinv).
+
+The reference's groups of G keys invert a partly zero IntGroup, so each group holds one real point
+(its centre) and G - 1 points that are no multiples of G (keyhunt.cpp:3274, 3301-3461; see
+oracle/kh_oracle.c walk_group_n).  The engine's hits are compared with the CPU oracle's restatement
+(itself pinned by the reference CLI's runs, tests/test_oracle.py::test_oracle_rmd_batch_vs_reference_cli)
+on targets built from centres, from those points (both sides of a group, slot 0, every hash kind)
+and from ordinary keys, and the CLI runs with --rmd-batch-size against the reference CLI's own
+fixtures in tests/test_gpu_scan.py (rmd160_batch*)."""
+import random
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+P = 2**256 - 2**32 - 977
+
+
+def _point_rows(oracle, pts, rng):
+    rows = []
+    for x, y in pts:
+        kind = rng.randrange(3)
+        if kind == 0:
+            rows.append(oracle.hash160_comp(x, 2 + (y & 1)))
+        elif kind == 1:
+            rows.append(oracle.hash160_comp(x, 3 - (y & 1)))
+        else:
+            rows.append(oracle.hash160_uncomp(x, y))
+    return rows
+
+
+def _targets(oracle, start, n_keys, G, rng, n=12):
+    """Points the reference's walk produces in groups of G from `start`: centres, and
+    x = -(C.x + (i+1)G.x) with y = -(i+1)G.y (slot G/2 + i + 1) or +(i+1)G.y (slot G/2 - i - 1)."""
+    half = G // 2
+    groups = (n_keys + G - 1) // G
+    pts = []
+    for _ in range(n):
+        g = rng.randrange(groups)
+        c = start + g * G + half
+        t = rng.choice([0, half, G - 1, rng.randrange(G)])
+        if t == half:
+            pts.append(oracle.pubkey(c))
+            continue
+        cx, _ = oracle.pubkey(c)
+        i = t - half - 1 if t > half else half - t - 1
+        tx, ty = oracle.pubkey(i + 1)
+        pts.append(((-(cx + tx)) % P, (P - ty) % P if t > half else ty))
+    # ordinary keys (found only where they are a centre)
+    pts += [oracle.pubkey(start + rng.randrange(n_keys)) for _ in range(3)]
+    return _point_rows(oracle, pts, rng)
+
+
+@pytest.mark.parametrize("G", [4, 8, 100, 512, 1000, 1020])
+@pytest.mark.parametrize("search,endo", [(0, False), (1, False), (2, False), (2, True), (0, True)])
+def test_engine_rmd_batch_vs_oracle(engine, oracle, G, search, endo):
+    rng = random.Random(G * 10 + search + (5 if endo else 0))
+    start = rng.getrandbits(66) | (1 << 65)
+    n_keys = 1 << 15  # not a multiple of 100/1000/1020: the last group overshoots the chunk
+    rows = _targets(oracle, start, n_keys, G, rng)
+    engine.set_targets(rows)
+    engine.set_rmd_batch(G)
+    try:
+        got = engine.scan(start, n_keys, mode=0, search=search, endo=endo)
+    finally:
+        engine.set_rmd_batch(1024)
+    ref = oracle.scan_chunk(0, search, start, n_keys, rows, endo=endo, group=G)
+    assert ref, "the targets should produce hits"
+    assert sorted((h.key, h.compressed, h.kind) for h in got) == sorted(ref)
+
+
+def test_engine_rmd_batch_1024_is_the_ordinary_walk(engine, oracle):
+    rng = random.Random(3)
+    start = rng.getrandbits(64)
+    keys = sorted(rng.sample(range(start, start + 8192), 5))
+    rows = [oracle.hash160_comp(*(lambda p: (p[0], 2 + (p[1] & 1)))(oracle.pubkey(k))) for k in keys]
+    engine.set_targets(rows)
+    engine.set_rmd_batch(1024)
+    got = engine.scan(start, 8192, mode=0, search=0)
+    assert [h.key for h in got] == keys
+
+
+def test_engine_rmd_batch_refuses_bad_sizes_and_xpoint(engine, oracle):
+    from keyhunt_amd.engine import KhError
+    for bad in (2, 6, 1025, 2048):
+        with pytest.raises(KhError):
+            engine.set_rmd_batch(bad)
+    engine.set_targets([bytes(20)])
+    engine.set_rmd_batch(512)
+    try:
+        with pytest.raises(KhError):
+            engine.scan(1, 4096, mode=1, search=2)
+    finally:
+        engine.set_rmd_batch(1024)

@@ -123,6 +123,29 @@ def test_oracle_scan_vs_reference_cli(oracle, name, fn, mode, search, endo):
     assert [f"{k:x}" for k in sorted(k for k, _, _ in hits)] == [x["key"] for x in E2E[name]["hits"]]
 
 
+@pytest.mark.parametrize("name,search,endo,group", [
+    ("rmd160_batch512_compress", 0, False, 512),
+    ("rmd160_batch512_both", 2, False, 512),
+    ("rmd160_batch512_both_endo", 2, True, 512),
+    ("rmd160_batch1000_compress", 0, False, 1000),
+    ("rmd160_batch1000_both", 2, False, 1000),
+    ("rmd160_batch1001_compress_endo", 0, True, 1000),  # the reference rounds 1001 down to 1000
+    ("rmd160_batch1024_both", 2, False, 1024),
+])
+def test_oracle_rmd_batch_vs_reference_cli(oracle, name, search, endo, group):
+    """-m rmd160 --rmd-batch-size G over 0x10000..0x20ffff in two 2^20 chunks: the oracle's walk
+    (the reference's partly zero batch inversion restated, kh_oracle.c walk_group_n) finds exactly
+    the reference CLI's keys -- group centres, and the negated or nominal slot keys of the points
+    that are no multiples of G (tests/golden/make_rmd_batch_targets.py)."""
+    assert E2E[name]["argv"][E2E[name]["argv"].index("--rmd-batch-size") + 1] in (str(group), str(group + 1))
+    rows = _read_rows(oracle, "rmd_batch.rmd", "addr")
+    keys = []
+    for chunk in range(2):
+        keys += [k for k, _, _ in oracle.scan_chunk(0, search, 0x10000 + chunk * (1 << 20), 1 << 20, rows,
+                                                    endo=endo, group=group)]
+    assert [f"{k:x}" for k in sorted(keys)] == [x["key"] for x in E2E[name]["hits"]]
+
+
 def test_oracle_scan_window_66(oracle):
     rows = _read_rows(oracle, "66.rmd", "addr")
     start = 0x2832ED74F2B5E0000
