@@ -20,7 +20,14 @@
 // Options: -k K, -n N, -i IP (127.0.0.1), -p PORT (8080), -6 (skip file checksums), -g contexts
 // (default: one per GPU; more than the GPUs share them), -L reference|blocked (layer-1 layout),
 // -t (accepted; one host thread per context), --ptable FILE, --ptable-size SIZE, --load-ptable,
-// --ptable-cache (the bP table file, its FILE.md5 and FILE.cache, bsgsd.cpp:1314-1470, 1719-1755).
+// --ptable-cache (the bP table file, its FILE.md5 and FILE.cache, bsgsd.cpp:1314-1470, 1719-1755),
+// and the bloom-file options (bsgsd.cpp:776-889): --mapped[=NAME], --mapped-size SIZE,
+// --mapped-chunks N, --bloom-file NAME, --load-bloom, --bloom-bytes SIZE, --create-mapped[=SIZE]
+// (kh_mapped.h: with --mapped the 3 x 256 shard files bloom-%u.dat, bloom2-%u.dat, bloom3-%u.dat
+// are written as the reference's mmap leaves them, and no -S files are read or written), --tmpdir
+// (where the reference maps an unnamed bP table; the table lives in HBM here),
+// --bsgs-block-count / --bsgs-block-size (parsed and sized by the reference, then unused,
+// bsgsd.cpp:1047-1066) and --rmd-batch-size (unused by the daemon, bsgsd.cpp:887-888).
 #include <arpa/inet.h>
 #include <ctype.h>
 #include <errno.h>
@@ -44,6 +51,7 @@
 
 #include "kh_gpu.h"
 #include "kh_host_util.h"
+#include "kh_mapped.h"
 
 using namespace kh;
 using namespace khh;
@@ -65,6 +73,7 @@ struct options {
   const char *ptable = nullptr;
   uint64_t ptable_size = 0;
   bool load_ptable = false, ptable_cache = false;
+  bool mapped = false, create_mapped = false;  // FLAGMAPPED, FLAGCREATEMAPPED (mapped::cfg holds the rest)
 } opt;
 
 std::vector<gpu> g_gpus;
@@ -87,6 +96,7 @@ std::string tbl_name(const kh_bsgs_info &I) {
 }
 
 bool files_present(const kh_bsgs_info &I) {
+  if (opt.mapped) return false;  // -S files are skipped with --mapped (bsgsd.cpp:1465, 1991)
   char f[3][96];
   snprintf(f[0], 96, "keyhunt_bsgs_4_%llu.blm", (unsigned long long)I.m);
   snprintf(f[1], 96, "keyhunt_bsgs_6_%llu.blm", (unsigned long long)I.m2);
@@ -202,9 +212,12 @@ int first_tables(gpu &g, std::vector<uint8_t> &rows, bool &present) {
   if (!present) {
     const bool had_tbl = access(tbl.c_str(), F_OK) == 0;
     int r = kh_bsgs_build(g.ctx);
-    if (!r) r = kh_bsgs_save(g.ctx, ".");
+    if (!r && !opt.mapped) r = kh_bsgs_save(g.ctx, ".");
     if (r) return r;
-    if (opt.load_ptable && !had_tbl) {
+    if (opt.mapped) {
+      // the shard files instead, filled from the tables just built (bsgsd.cpp:1180-1255, 1850-1980)
+      if (!mapped::bsgs_layers(g.ctx, I)) return KH_E_IO;
+    } else if (opt.load_ptable && !had_tbl) {
       unlink(tbl.c_str());  // the table came from the --ptable file: no .tbl is written
     } else {
       md5_refresh(tbl, md5, false);
@@ -231,6 +244,37 @@ int first_tables(gpu &g, std::vector<uint8_t> &rows, bool &present) {
   }
   if (opt.load_ptable) return kh_bsgs_set_table(g.ctx, rows.data(), I.m3);
   return KH_OK;
+}
+
+// bsgsd's initBloomFilterMapped without --mapped (bsgsd.cpp:657-680), per shard in the order of
+// bsgsd.cpp:1180-1255: --load-bloom, or a shard file already in the directory, makes it bloom_load
+// that file (bloom/bloom.cpp:323-372), which needs the BLOOM_MAGIC header bloom_save writes -- the
+// daemon never writes one, and a mapped shard file (raw bits) fails it -- so the start stops there
+// (exit 0) before any table is built
+bool plain_shards_ok() {
+  const char *pfx[3] = {"bloom-", "bloom2-", "bloom3-"};
+  for (int l = 0; l < 3; l++)
+    for (int i = 0; i < 256; i++) {
+      const std::string fn = pfx[l] + std::to_string(i) + ".dat";
+      struct stat st;
+      const bool have = stat(fn.c_str(), &st) == 0;
+      bool fail = false;
+      if (mapped::cfg.load_bloom) {
+        if (!have || st.st_size == 0)
+          fprintf(stderr, "[E] --load-bloom specified but bloom file '%s' does not exist or is empty\n", fn.c_str());
+        else
+          fprintf(stderr, "[E] bloom_load failed for '%s'\n", fn.c_str());
+        fail = true;
+      } else if (!mapped::cfg.entries && have) {
+        fprintf(stderr, "[E] bloom_load failed for '%s'\n", fn.c_str());
+        fail = true;
+      }
+      if (fail) {
+        fprintf(stderr, l < 2 ? "[E] error bloom_init _ %i\n" : "[E] error bloom_init %i\n", i);
+        return false;
+      }
+    }
+  return true;
 }
 
 // the walk of one request: bases from, from + 2N, ... while base < to, over every GPU
@@ -452,7 +496,34 @@ int main(int argc, char **argv) {
                                            {"ptable-size", required_argument, 0, 2},
                                            {"load-ptable", no_argument, 0, 3},
                                            {"ptable-cache", no_argument, 0, 4},
+                                           {"mapped", optional_argument, 0, 5},
+                                           {"mapped-size", required_argument, 0, 6},
+                                           {"mapped-chunks", required_argument, 0, 7},
+                                           {"bloom-file", required_argument, 0, 8},
+                                           {"load-bloom", no_argument, 0, 9},
+                                           {"bloom-bytes", required_argument, 0, 10},
+                                           {"create-mapped", optional_argument, 0, 11},
+                                           {"tmpdir", required_argument, 0, 12},
+                                           {"bsgs-block-count", required_argument, 0, 13},
+                                           {"bsgs-block-size", required_argument, 0, 13},
+                                           {"rmd-batch-size", required_argument, 0, 13},
                                            {0, 0, 0, 0}};
+  mapped::cfg.bsgsd = true;
+  // --mapped-size / --bloom-bytes / --create-mapped SIZE, with the k/m/g/t suffixes: the entry count
+  // and error bsgsd's bloom_entries_for_bytes gives any size (kh_mapped.h entries_for_bsgsd)
+  auto size_override = [](const char *arg) {
+    char *end;
+    uint64_t v = strtoull(arg, &end, 10);
+    if (*end) {
+      switch (tolower(*end)) {
+        case 'k': v *= 1024ull; break;
+        case 'm': v *= 1024ull * 1024ull; break;
+        case 'g': v *= 1024ull * 1024ull * 1024ull; break;
+        case 't': v *= 1024ull * 1024ull * 1024ull * 1024ull; break;
+      }
+    }
+    mapped::entries_for_bsgsd(v, &mapped::cfg.entries, &mapped::cfg.error);
+  };
   while ((c = getopt_long(argc, argv, "6hk:n:t:p:i:g:L:B:", long_opts, nullptr)) != -1) {
     switch (c) {
       case 1: opt.ptable = optarg; break;  // bsgsd.cpp:828-829
@@ -472,6 +543,31 @@ int main(int argc, char **argv) {
       }
       case 3: opt.load_ptable = true; break;
       case 4: opt.ptable_cache = true; break;
+      case 5:  // bsgsd.cpp:799-803
+        opt.mapped = true;
+        if (optarg) mapped::cfg.name = optarg;
+        break;
+      case 6:  // bsgsd.cpp:804-820
+        opt.mapped = true;
+        size_override(optarg);
+        break;
+      case 7:  // bsgsd.cpp:821-823
+        opt.mapped = true;
+        mapped::cfg.chunks = (uint32_t)strtoul(optarg, NULL, 10);
+        break;
+      case 8: mapped::cfg.name = optarg; break;        // bsgsd.cpp:824-825 (does not set --mapped)
+      case 9: mapped::cfg.load_bloom = true; break;    // bsgsd.cpp:826-827
+      case 10:                                         // bsgsd.cpp:844-859
+        opt.mapped = true;
+        size_override(optarg);
+        break;
+      case 11:  // bsgsd.cpp:860-878
+        opt.mapped = true;
+        opt.create_mapped = true;
+        if (optarg) size_override(optarg);
+        break;
+      case 12: break;  // --tmpdir
+      case 13: break;  // --bsgs-block-count/--bsgs-block-size/--rmd-batch-size: no effect on the daemon
       case '6':
         opt.skip_checksum = true;
         fprintf(stderr, "[W] Skipping checksums on files\n");
@@ -504,7 +600,9 @@ int main(int argc, char **argv) {
       case 'h':
       default:
         printf("usage: %s [-k K] [-n N] [-i IP] [-p PORT] [-6] [-g CONTEXTS] [-L reference|blocked]\n"
-               "       [--ptable FILE [--ptable-size SIZE] [--load-ptable] [--ptable-cache]]\n", argv[0]);
+               "       [--ptable FILE [--ptable-size SIZE] [--load-ptable] [--ptable-cache]]\n"
+               "       [--mapped[=NAME]] [--mapped-size SIZE] [--mapped-chunks N] [--bloom-file NAME]\n"
+               "       [--load-bloom] [--bloom-bytes SIZE] [--create-mapped[=SIZE]] [--tmpdir DIR]\n", argv[0]);
         return c == 'h' ? EXIT_SUCCESS : EXIT_FAILURE;
     }
   }
@@ -513,8 +611,10 @@ int main(int argc, char **argv) {
     fprintf(stderr, "--load-ptable requires --ptable <file>\n");
     return EXIT_FAILURE;
   }
+  if (opt.create_mapped) return mapped::create();  // bsgsd.cpp:955-995: the zeroed file(s), then exit
   if (!validate_nk(opt.n, opt.k)) return EXIT_FAILURE;
   printf("[+] Mode BSGS secuential\n[+] N = 0x%llx\n", (unsigned long long)opt.n);
+  if (!opt.mapped && !plain_shards_ok()) return 0;
   int ndev = 0;
   if (kh_device_count(&ndev) || ndev <= 0) {
     fprintf(stderr, "[E] no GPU\n");
@@ -556,6 +656,7 @@ int main(int argc, char **argv) {
       if (r == KH_E_IO) r = kh_bsgs_build(g.ctx);  // --load-ptable without a .tbl
       if (!r && opt.load_ptable) r = kh_bsgs_set_table(g.ctx, ptable_rows.data(), g.info.m3);
     }
+    if (r && mapped::open_failed) return 0;  // a shard file the reference cannot map either: exit(0)
     if (r) {
       fprintf(stderr, "[E] GPU %d: %s (%s)\n", d, kh_strerror(r), g.ctx ? kh_last_error(g.ctx) : "");
       return EXIT_FAILURE;

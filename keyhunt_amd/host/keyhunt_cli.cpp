@@ -35,6 +35,7 @@
 #include "kh_gpu.h"
 #include "../csrc/kh_math.h"
 #include "kh_host_util.h"
+#include "kh_mapped.h"
 
 using namespace kh;
 using namespace khh;
@@ -432,253 +433,8 @@ bool read_targets(const char *fn, int mode, std::vector<uint8_t> &rows, uint64_t
 // top of its bits.  With chunks, the reference's bit -> chunk map (byte / chunk_bytes) equals the
 // concatenation except for bytes past c * chunk_bytes, which it indexes out of bounds.
 // ---------------------------------------------------------------------------------------------
-namespace mapped {
-
-// bloom_bytes_for_entries_error (keyhunt.cpp:7495-7507) == bytes_for_entries_error (bloom.cpp:454-464)
-uint64_t bytes_for(uint64_t entries, long double error) {
-  long double num = -logl(error);
-  long double denom = 0.480453013918201L;
-  long double bpe = num / denom;
-  long double allbits = (long double)entries * bpe;
-  uint64_t bits = (uint64_t)allbits;
-  return bits / 8 + ((bits % 8) ? 1 : 0);
-}
-// bloom_entries_for_bytes (keyhunt.cpp:7510-7530) == entries_hashes_for_bytes (bloom.cpp:465-489)
-void entries_for(uint64_t bytes, uint64_t *entries, uint32_t *hashes) {
-  uint64_t best_n = 0;
-  uint32_t best_k = 0;
-  for (uint32_t b = 20; b <= 64; b += 2) {
-    const uint64_t n = 1ULL << (b == 64 ? 63 : b);
-    const uint32_t k = 1U << ((b - 20) / 2);
-    if (b == 64 || bytes_for(n, powl(0.5L, (long double)k)) > bytes) break;
-    best_n = n;
-    best_k = k;
-  }
-  if (best_n == 0) {
-    best_n = 1ULL << 20;
-    best_k = 1;
-  }
-  *entries = best_n;
-  *hashes = (uint32_t)(uint8_t)best_k;
-}
-
-struct filter {
-  std::string name;                 // NAME, or the base of NAME.i
-  uint32_t chunks = 1;
-  uint64_t bits = 0, bytes = 0;
-  uint32_t hashes = 0;
-  std::vector<uint64_t> chunk_bytes;  // size of each file
-  std::vector<uint8_t> bf;          // flat bit array
-  std::string file(uint32_t i) const { return chunks > 1 ? name + "." + std::to_string(i) : name; }
-};
-bool applied = false;  // initBloomFilterMapped's static mapped_override_applied
-
-bool exists(const std::string &f) {
-  struct stat st;
-  return stat(f.c_str(), &st) == 0;
-}
-
-// bloom_load_mmap (bloom.cpp:491-578): geometry from the files' total size
-bool load(filter &F) {
-  F.chunk_bytes.assign(F.chunks, 0);
-  F.bf.clear();
-  for (uint32_t i = 0; i < F.chunks; i++) {
-    FILE *f = fopen(F.file(i).c_str(), "rb");
-    if (!f) return false;
-    std::vector<uint8_t> b;
-    uint8_t buf[1 << 16];
-    size_t n;
-    while ((n = fread(buf, 1, sizeof buf, f)) > 0) b.insert(b.end(), buf, buf + n);
-    fclose(f);
-    F.chunk_bytes[i] = b.size();
-    F.bf.insert(F.bf.end(), b.begin(), b.end());
-  }
-  F.bytes = F.bf.size();
-  F.bits = F.bytes * 8;
-  uint64_t entries;
-  entries_for(F.bytes, &entries, &F.hashes);
-  return true;
-}
-
-// bloom_init_mmap (bloom.cpp:589-700): geometry from entries and error (bpe kept as a double, the
-// ln(2)^2 denominator a double literal); existing files are kept, resized only when `resize`
-bool init(filter &F, uint64_t entries, long double error, bool resize) {
-  if (entries < 1000 || error <= 0 || error >= 1) return false;
-  long double num = -logl(error);
-  long double denom = 0.480453013918201;
-  const double bpe = (double)(num / denom);
-  F.bits = (uint64_t)((long double)entries * bpe);
-  F.bytes = F.bits / 8 + ((F.bits % 8) ? 1 : 0);
-  F.hashes = (uint32_t)(uint8_t)ceil(0.693147180559945 * bpe);
-  const uint64_t cb = F.chunks > 1 ? F.bytes / F.chunks : F.bytes;
-  F.chunk_bytes.assign(F.chunks, cb);
-  F.chunk_bytes[F.chunks - 1] = F.bytes - cb * (F.chunks - 1);
-  F.bf.assign(F.bytes, 0);
-  uint64_t off = 0;
-  for (uint32_t i = 0; i < F.chunks; i++) {
-    const std::string fn = F.file(i);
-    struct stat st;
-    if (stat(fn.c_str(), &st) == 0) {
-      if ((uint64_t)st.st_size != F.chunk_bytes[i] && !resize) {
-        fprintf(stderr, "bloom_init_mmap: file '%s' size %lld does not match expected %llu\n", fn.c_str(),
-                (long long)st.st_size, (unsigned long long)F.chunk_bytes[i]);
-        return false;
-      }
-      FILE *f = fopen(fn.c_str(), "rb");  // the bytes it keeps (ftruncate never moves them)
-      if (f) {
-        size_t got = fread(F.bf.data() + off, 1, (size_t)std::min<uint64_t>(st.st_size, F.chunk_bytes[i]), f);
-        (void)got;
-        fclose(f);
-      }
-    }
-    off += F.chunk_bytes[i];
-  }
-  return true;
-}
-
-bool save(const filter &F) {
-  uint64_t off = 0;
-  for (uint32_t i = 0; i < F.chunks; i++) {
-    FILE *f = fopen(F.file(i).c_str(), "wb");
-    bool ok = f && (F.chunk_bytes[i] == 0 || fwrite(F.bf.data() + off, F.chunk_bytes[i], 1, f) == 1);
-    if (f) ok = fclose(f) == 0 && ok;
-    if (!ok) {
-      fprintf(stderr, "[E] Error writing the mapped bloom file %s\n", F.file(i).c_str());
-      return false;
-    }
-    off += F.chunk_bytes[i];
-  }
-  return true;
-}
-
-// initBloomFilterMapped (keyhunt.cpp:7630-7706), FLAGMAPPED set: load or create the filter of
-// `items` elements; fname names a BSGS shard file, else --mapped/--bloom-file or bloom.dat
-bool open_filter(filter &F, uint64_t items, const char *fname, bool quiet = false) {
-  F.name = fname ? fname : (opt.mapped_name ? opt.mapped_name : "bloom.dat");
-  F.chunks = opt.mapped_chunks ? opt.mapped_chunks : 1;
-  if (!quiet) printf("[+] Bloom filter for %llu elements.\n", (unsigned long long)items);
-  if (opt.load_bloom) {
-    if (!exists(F.file(0))) {
-      fprintf(stderr, "[E] --load-bloom specified but mapped bloom file '%s' does not exist\n", F.file(0).c_str());
-      return false;
-    }
-    if (!load(F)) {
-      fprintf(stderr, "[E] bloom_load_mmap failed for '%s'\n", F.name.c_str());
-      return false;
-    }
-    if (!F.bytes) {
-      fprintf(stderr, "[E] Mapped bloom file '%s' has zero length; regenerate it or remove --load-bloom\n", F.name.c_str());
-      return false;
-    }
-    return true;
-  }
-  if (!opt.mapped_entries && exists(F.file(0))) {
-    if (!load(F)) {
-      fprintf(stderr, "[E] bloom_load_mmap failed for '%s'\n", F.name.c_str());
-      return false;
-    }
-    if (!F.bytes) {
-      fprintf(stderr, "[E] Existing mapped bloom file '%s' is empty; delete it or rerun without --load-bloom\n",
-              F.name.c_str());
-      return false;
-    }
-    return true;
-  }
-  uint64_t total;
-  if (opt.mapped_entries && (!applied || items >= opt.mapped_entries)) {
-    total = opt.mapped_entries;
-    applied = true;  // the override is applied once (to the first filter) by default
-  } else {
-    total = items <= 10000 ? 10000 : (uint64_t)opt.bloom_mult * items;
-  }
-  const long double error = opt.mapped_error ? opt.mapped_error : 0.000001L;
-  if (!init(F, total, error, opt.mapped_entries != 0)) {
-    fprintf(stderr, "[E] bloom_init_mmap failed for '%s' (%llu bytes for %llu elements).\n", F.name.c_str(),
-            (unsigned long long)bytes_for(total, error), (unsigned long long)total);
-    return false;
-  }
-  return true;
-}
-
-// --create-mapped (keyhunt.cpp:1131-1172): the zeroed file(s) of the override's size, then exit 0
-int create() {
-  if (!opt.mapped_entries) {
-    fprintf(stderr, "[E] --create-mapped requires size via argument or --bloom-bytes\n");
-    return EXIT_FAILURE;
-  }
-  filter F;
-  F.name = opt.mapped_name ? opt.mapped_name : "bloom.dat";
-  F.chunks = opt.mapped_chunks ? opt.mapped_chunks : 1;
-  const long double error = opt.mapped_error ? opt.mapped_error : 0.000001L;
-  if (!init(F, opt.mapped_entries, error, true)) {
-    fprintf(stderr, "[E] bloom_init_mmap failed for '%s' (%llu bytes for %llu elements).\n", F.name.c_str(),
-            (unsigned long long)bytes_for(opt.mapped_entries, error), (unsigned long long)opt.mapped_entries);
-    return EXIT_FAILURE;
-  }
-  std::fill(F.bf.begin(), F.bf.end(), 0);
-  return save(F) ? EXIT_SUCCESS : EXIT_FAILURE;
-}
-
-// a target filter (address / rmd160 / xpoint / eth / vanity): open it, add the items, write it back
-bool targets(uint64_t items, const std::vector<uint8_t> &adds, uint32_t len) {
-  filter F;
-  if (!open_filter(F, items, nullptr)) return false;
-  if (kh_bloom_add(F.bf.data(), F.bits, F.hashes, adds.data(), adds.size() / len, len) != KH_OK) return false;
-  printf("[+] Loading data to the bloomfilter total: %.2f MB\n", (double)F.bytes / 1048576.0);
-  return save(F);
-}
-
-// the BSGS layers (keyhunt.cpp:1631-1785): 3 x 256 shard files bloom-%u.dat, bloom2-%u.dat,
-// bloom3-%u.dat of itemsbloom / itemsbloom2 / itemsbloom3 elements each, in that order (the size
-// override is applied to the first), filled by the baby steps of their layer on the GPU
-bool bsgs_layers(kh_ctx *ctx, const kh_bsgs_info &I) {
-  const uint64_t ms[3] = {I.m, I.m2, I.m3};
-  const uint64_t floor_[3] = {10000, 1000, 1000};
-  const char *pfx[3] = {"bloom-", "bloom2-", "bloom3-"};
-  for (int l = 0; l < 3; l++) {
-    uint64_t items = ms[l] / 256 > floor_[l] ? ms[l] / 256 + (ms[l] % 256 ? 1 : 0) : 1000;
-    std::vector<filter> F(256);
-    for (int i = 0; i < 256; i++) {
-      const std::string fn = pfx[l] + std::to_string(i) + ".dat";
-      if (!open_filter(F[i], items, fn.c_str(), true)) {
-        fprintf(stderr, "[E] error bloom_init [%d]\n", i);
-        return false;
-      }
-    }
-    // one GPU pass per distinct shard geometry
-    std::vector<bool> done(256, false);
-    for (int i = 0; i < 256; i++) {
-      if (done[i]) continue;
-      const uint64_t bits = F[i].bits, bytes = F[i].bytes;
-      const uint32_t hashes = F[i].hashes;
-      std::vector<uint8_t> all(256 * bytes, 0);
-      std::vector<int> group;
-      for (int j = i; j < 256; j++)
-        if (!done[j] && F[j].bits == bits && F[j].bytes == bytes && F[j].hashes == hashes) {
-          group.push_back(j);
-          memcpy(&all[(size_t)j * bytes], F[j].bf.data(), bytes);
-        }
-      int r = kh_bsgs_layer_bits(ctx, (uint32_t)l + 1, bits, hashes, bytes, all.data());
-      if (r) {
-        fprintf(stderr, "[E] %s (%s)\n", kh_strerror(r), kh_last_error(ctx));
-        return false;
-      }
-      for (int j : group) {
-        memcpy(F[j].bf.data(), &all[(size_t)j * bytes], bytes);
-        done[j] = true;
-      }
-    }
-    uint64_t total = 0;
-    for (int i = 0; i < 256; i++) {
-      if (!save(F[i])) return false;
-      total += F[i].bytes;
-    }
-    printf("[+] Bloom filter for %llu elements : %.2f MB\n", (unsigned long long)ms[l], (double)total / 1048576.0);
-  }
-  return true;
-}
-
-}  // namespace mapped
+// the mapped bloom files live in kh_mapped.h (shared with bsgsd-amd); mapped::cfg is filled
+// from the options once they are parsed
 
 // ---------------------------------------------------------------------------------------------
 // stats (keyhunt.cpp:2850-2962)
@@ -1410,6 +1166,12 @@ int main(int argc, char **argv) {
     fprintf(stderr, "--load-ptable requires --ptable <file>\n");
     return EXIT_FAILURE;
   }
+  mapped::cfg.name = opt.mapped_name;
+  mapped::cfg.chunks = opt.mapped_chunks;
+  mapped::cfg.load_bloom = opt.load_bloom;
+  mapped::cfg.entries = opt.mapped_entries;
+  mapped::cfg.error = opt.mapped_error;
+  mapped::cfg.bloom_mult = opt.bloom_mult;
   if (opt.create_mapped) return mapped::create();  // keyhunt.cpp:1131-1172: make the file(s) and exit
   if (opt.mode == MODE_BSGS) printf("[+] Mode BSGS %s\n", BSGS_MODES[opt.bsgs_mode]);  // keyhunt.cpp:1209-1211
   if (!opt.file && !(opt.mode == MODE_VANITY && opt.vanity.targets)) {

@@ -404,6 +404,113 @@ def gen_bsgsd() -> None:
         json.dump(out, f, indent=1)
 
 
+# bsgsd's bloom-file options (bsgsd.cpp:776-889 parsing, 584-660 initBloomFilterMapped, 955-995
+# --create-mapped, 1180-1255 the 3 x 256 shard filters bloom-%u.dat / bloom2-%u.dat / bloom3-%u.dat):
+# sequences of daemon starts sharing one directory; each start serves one found request (when the
+# daemon comes up) and is then stopped.  Recorded per start: whether it listened, its exit status
+# when it did not, the [E]/[W] lines it printed, the reply, and every file it left (the -S files
+# masked as in ref_bsgsd.json, the shard files per layer as in ref_mapped.json).
+BSGSD_MAPPED_SEQS = [
+    ("mapped_fresh_then_reload", [["--mapped"], ["--mapped"]]),
+    ("mapped_then_load_bloom", [["--mapped"], ["--mapped", "--load-bloom"]]),
+    ("load_bloom_missing", [["--mapped", "--load-bloom"]]),
+    ("mapped_named_chunks", [["--mapped=named.dat", "--mapped-chunks", "4"], ["--mapped-chunks", "4"]]),
+    ("mapped_size_override", [["--mapped-size", "64k"], ["--mapped-size", "64k"]]),
+    ("bloom_bytes", [["--bloom-bytes", "100000"]]),
+    ("create_then_mapped", [["--create-mapped=100000", "--bloom-file", "cm.dat"], ["--mapped", "--bloom-file", "cm.dat"]]),
+    ("create_chunks", [["--create-mapped=100000", "--mapped-chunks", "4"]]),
+    ("create_without_size", [["--create-mapped"]]),
+    ("mapped_then_plain", [["--mapped"], []]),
+    ("block_count_tmpdir_rmd_batch", [["--bsgs-block-count", "4", "--tmpdir", "tmpdir_x", "--rmd-batch-size", "8"],
+                                      ["--bsgs-block-size", "1024"]]),
+]
+
+
+def bsgsd_dir_files(d: str) -> dict:
+    """Every file in d: the 256 shard files of a layer (or of one chunk index of it) as one entry
+    [sizes, sha256 of their concatenation], -S files by masked digest, others [size, sha256]."""
+    import hashlib
+    out, layers = {}, {}
+    for f in sorted(os.listdir(d)):
+        if not os.path.isfile(os.path.join(d, f)):
+            continue
+        m = re.match(r"(bloom[23]?-)(\d+)\.dat((?:\.\d+)?)$", f)
+        if m:
+            layers.setdefault(m.group(1) + "*.dat" + m.group(3), {})[int(m.group(2))] = f
+        elif f.startswith("keyhunt_bsgs_"):
+            out[f] = masked_table_digest(os.path.join(d, f))
+        else:
+            b = open(os.path.join(d, f), "rb").read()
+            out[f] = [len(b), hashlib.sha256(b).hexdigest()]
+    for key, shards in layers.items():
+        h = hashlib.sha256()
+        sizes = []
+        for i in sorted(shards):
+            b = open(os.path.join(d, shards[i]), "rb").read()
+            sizes.append(len(b))
+            h.update(b)
+        out[key] = [sizes, h.hexdigest()]
+        if len(shards) != 256:  # a start that stopped part-way through a layer
+            out[key].append(sorted(shards))
+    return out
+
+
+def gen_bsgsd_mapped() -> None:
+    import socket
+    import time
+    subprocess.run(["make", "-s", "-C", HERE, "-f", "Makefile.ref", "-j8"], check=True)
+    res = {"args": BSGSD_ARGS, "request": BSGSD_REQUESTS[0][1].decode(),
+           "_generator": "oracle/make_golden.py --bsgsd-mapped running oracle/_ref/bsgsd"}
+    for name, starts in BSGSD_MAPPED_SEQS:
+        steps = []
+        with tempfile.TemporaryDirectory() as td:
+            os.mkdir(os.path.join(td, "tmpdir_x"))
+            for extra in starts:
+                sk = socket.socket()
+                sk.bind(("127.0.0.1", 0))
+                port = sk.getsockname()[1]
+                sk.close()
+                logp = os.path.join(td, "daemon.log")
+                log = open(logp, "w")
+                p = subprocess.Popen(["stdbuf", "-oL", os.path.join(HERE, "_ref", "bsgsd")] + BSGSD_ARGS + extra +
+                                     ["-t", "4", "-p", str(port), "-i", "127.0.0.1"], cwd=td, stdout=log,
+                                     stderr=subprocess.STDOUT)
+                t0 = time.time()
+                while "Listening in" not in open(logp).read() and p.poll() is None and time.time() - t0 < 300:
+                    time.sleep(0.2)
+                step = {"extra": extra, "listened": p.poll() is None}
+                if step["listened"]:
+                    with socket.create_connection(("127.0.0.1", port), timeout=300) as c:
+                        c.sendall(BSGSD_REQUESTS[0][1])
+                        reply = b""
+                        while True:
+                            b = c.recv(4096)
+                            if not b:
+                                break
+                            reply += b
+                    step["reply"] = reply.decode()
+                    p.kill()
+                p.wait()
+                if not step["listened"]:
+                    step["exit"] = p.returncode
+                log.close()
+                text = open(logp).read()
+                step["notes"] = sorted(set(m.strip() for m in re.findall(r"\[[EW]\] [^\n]*", text)))
+                os.remove(logp)
+                for f in ("KEYFOUNDKEYFOUND.txt",):
+                    if os.path.exists(os.path.join(td, f)):
+                        os.remove(os.path.join(td, f))
+                step["files"] = bsgsd_dir_files(td)
+                step["tmpdir_files"] = sorted(os.listdir(os.path.join(td, "tmpdir_x")))
+                steps.append(step)
+                print(name, extra, step["listened"], step.get("exit"), repr(step.get("reply")), step["notes"],
+                      {k: (v[0] if isinstance(v, list) and isinstance(v[0], int) else "...") for k, v in step["files"].items()},
+                      step["tmpdir_files"], flush=True)
+        res[name] = steps
+    with open(os.path.join(REPO, "tests", "golden", "ref_bsgsd_mapped.json"), "w") as f:
+        json.dump(res, f, indent=1)
+
+
 # --mapped bloom files (keyhunt.cpp:724-806, 1131-1172, 1700-1785, 7630-7706; bloom/bloom.cpp:491-747):
 # sequences of reference-CLI runs sharing one directory per sequence; after each run every mapped file
 # is recorded (BSGS shard files per layer: their sizes and the sha256 of their concatenation).  The
@@ -482,10 +589,11 @@ if __name__ == "__main__":
     ap.add_argument("--data", action="store_true")
     ap.add_argument("--bsgsd", action="store_true")
     ap.add_argument("--mapped", action="store_true")
+    ap.add_argument("--bsgsd-mapped", action="store_true")
     ap.add_argument("--only", nargs="*")
     a = ap.parse_args()
-    if not (a.vectors or a.e2e or a.tables or a.data or a.bsgsd or a.mapped):
-        a.vectors = a.e2e = a.tables = a.data = a.bsgsd = a.mapped = True
+    if not (a.vectors or a.e2e or a.tables or a.data or a.bsgsd or a.mapped or a.bsgsd_mapped):
+        a.vectors = a.e2e = a.tables = a.data = a.bsgsd = a.mapped = a.bsgsd_mapped = True
     if a.vectors:
         gen_vectors()
     if a.e2e:
@@ -498,3 +606,5 @@ if __name__ == "__main__":
         gen_bsgsd()
     if a.mapped:
         gen_mapped()
+    if a.bsgsd_mapped:
+        gen_bsgsd_mapped()

@@ -57,6 +57,20 @@ def run_cli(argv: list[str], timeout: int = 600, kill_after: int | None = None):
         return p, parse_keyfound(text)
 
 
+def without_threads(argv: list[str]) -> list[str]:
+    """argv without its "-t N" pair (the engine's CLI takes -g for devices; other "8"s stay)."""
+    out, skip = [], False
+    for i, a in enumerate(argv):
+        if skip:
+            skip = False
+            continue
+        if a == "-t" and i + 1 < len(argv):
+            skip = True
+            continue
+        out.append(a)
+    return out
+
+
 def _uniq(xs):
     return [x for i, x in enumerate(xs) if x not in xs[:i]]
 

@@ -9,7 +9,7 @@ import os
 import pytest
 
 from conftest import GOLDEN
-from _cli import check_against_reference, run_cli
+from _cli import check_against_reference, run_cli, without_threads
 
 pytestmark = pytest.mark.gpu
 VEC = json.load(open(os.path.join(GOLDEN, "ref_vectors.json")))
@@ -103,7 +103,7 @@ def test_cli_bsgs_matches_reference(name):
     CLI's; each distinct hit once (overlapping GGSB bases let several reference threads print the
     same key before the exit)."""
     ref = E2E[name]
-    check_against_reference(ref, [a for a in ref["argv"] if a not in ("-t", "8")], name)
+    check_against_reference(ref, without_threads(ref["argv"]), name)
 
 
 def test_bench_config_k128_known_answer():

@@ -16,7 +16,7 @@ import time
 import pytest
 
 from conftest import DATA, GOLDEN, REPO
-from _cli import STDOUT_BLOCK, parse_keyfound
+from _cli import STDOUT_BLOCK, parse_keyfound, without_threads
 
 pytestmark = pytest.mark.gpu
 E2E = json.load(open(os.path.join(GOLDEN, "ref_e2e.json")))
@@ -53,7 +53,7 @@ def run_patched(argv, td=None, timeout=600):
 def test_patched_reference_on_gpu_matches_reference(name, threads):
     """-t 1 and -t 2: with two threads both workers share the device's one context (section 1)."""
     ref = E2E[name]
-    argv = [a for a in ref["argv"] if a not in ("-t", "8")] + ["-t", str(threads), "-q"]
+    argv = without_threads(ref["argv"]) + ["-t", str(threads), "-q"]
     p, text, _ = run_patched(argv)
     assert p.returncode == ref["exit"], p.stdout[-2000:] + p.stderr[-2000:]
     assert "kh_" not in p.stderr, p.stderr  # no engine error
@@ -68,7 +68,7 @@ def test_patched_reference_bench_geometry_k128_without_cpu_tables():
     pool: ~120 s on 8 cores and 1.9 GB of host blooms in the unpatched reference) and finds the key
     in well under 15 s."""
     ref = E2E["bsgs_125_window"]
-    argv = [a for a in ref["argv"] if a not in ("-t", "8")] + ["-k", "128", "-t", "1"]
+    argv = without_threads(ref["argv"]) + ["-k", "128", "-t", "1"]
     p, text, wall = run_patched(argv)
     assert p.returncode == 1, p.stdout[-2000:] + p.stderr[-2000:]
     assert parse_keyfound(text) == ref["hits"]
@@ -82,7 +82,7 @@ def test_patched_reference_bsgs_table_files():
     (kh_bsgs_save); the second reads them back (kh_bsgs_load) and finds the same key; the
     unpatched reference reads the engine's files too (tests/test_gpu_tables.py)."""
     ref = E2E["bsgs_120_window"]
-    argv = [a for a in ref["argv"] if a not in ("-t", "8")] + ["-t", "1", "-S"]
+    argv = without_threads(ref["argv"]) + ["-t", "1", "-S"]
     td = tempfile.mkdtemp()
     try:
         for fn in os.listdir(DATA):

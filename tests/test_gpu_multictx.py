@@ -13,7 +13,7 @@ import os
 import pytest
 
 from conftest import GOLDEN
-from _cli import check_against_reference
+from _cli import check_against_reference, without_threads
 
 pytestmark = pytest.mark.gpu
 E2E = json.load(open(os.path.join(GOLDEN, "ref_e2e.json")))
@@ -21,7 +21,7 @@ CASES = [k for k in E2E if not k.startswith("_")]
 
 
 def _argv(name: str, contexts: int) -> list[str]:
-    return [a for a in E2E[name]["argv"] if a not in ("-t", "8")] + ["-g", str(contexts)]
+    return without_threads(E2E[name]["argv"]) + ["-g", str(contexts)]
 
 
 @pytest.mark.parametrize("contexts", [2, 3])
