@@ -648,6 +648,28 @@ bool take_bases(const U &twoN, uint64_t want, std::vector<U> &out) {
   return !out.empty();
 }
 
+// The sequential schedules (sequential, angrygiant, ggsb) as one progression: up to `want` bases
+// from the cursor, step apart, while below the end -- the bases take_bases would list, counted
+// instead of listed (a call of 2^20 bases spent ~9 % of the GPU's time listing, sorting and
+// checking them on the host between calls)
+bool take_progression(const U &step, uint64_t want, U &start, uint64_t &count) {
+  std::lock_guard<std::mutex> lk(g_cursor_mtx);
+  if (u_cmp(g_cursor, g_top) >= 0) return false;
+  start = g_cursor;
+  const U rem = u_sub(g_top, g_cursor);
+  uint64_t n = want;
+  if (step.v[1] == 0 && step.v[2] == 0 && step.v[3] == 0 && step.v[4] == 0 && step.v[0]) {
+    uint64_t r = 0;
+    const U q = u_divmod_u64(rem, step.v[0], &r);  // bases below the end: ceil(rem / step)
+    if (u_bitlen(q) < 63) n = std::min<uint64_t>(want, q.v[0] + (r ? 1 : 0));
+    count = n;
+    g_cursor = u_add(g_cursor, u_mul_u64(step, n));
+    return true;
+  }
+  for (count = 0; count < want && u_cmp(g_cursor, g_top) < 0; count++) g_cursor = u_add(g_cursor, step);
+  return true;
+}
+
 // --ptable-cache: FILE.md5 holds the file's MD5 as hex text; FILE.cache the 257 bucket starts of
 // the rows by value[0] under that MD5 (struct bptable_cache_file, keyhunt.cpp:137-143, 186-241).
 // With --load-ptable an existing FILE.md5 is trusted (1958-1981); otherwise the MD5 is computed
@@ -834,6 +856,52 @@ int bsgs_tables(kh_ctx *ctx, const kh_bsgs_info &info, bool first) {
   return KH_OK;
 }
 
+// the targets a call found, printed and recorded as the reference's sequential worker does
+// (keyhunt.cpp:4790-4830); the run ends when every target is found
+void report_found(kh_ctx *ctx, const bsgs_job *j, const std::vector<kh_bsgs_found> &found, uint32_t nf) {
+  for (uint32_t i = 0; i < nf; i++) {
+    uint32_t t = found[i].target;
+    std::lock_guard<std::mutex> lk(g_found_mtx);
+    if (g_found[t]) continue;
+    g_found[t] = 1;
+    std::string k = u_hex(u_from_be32(found[i].key));
+    uint8_t pxy[64];
+    kh_pubkeys(ctx, found[i].key, 1, pxy);
+    std::string pub;
+    if ((*j->comp)[t]) {
+      uint8_t p = (pxy[63] & 1) ? 3 : 2;
+      pub = hex(&p, 1) + hex(pxy, 32);
+    } else {
+      uint8_t p = 4;
+      pub = hex(&p, 1) + hex(pxy, 64);
+    }
+    {
+      std::lock_guard<std::mutex> lk2(g_keys_mtx);
+      // each BSGS worker of the reference has its own format: the sequential one (also -B ggsb and
+      // angrygiant) continues its string over a backslash-newline, so no newline is printed
+      // (keyhunt.cpp:4826-4827); random 5079, dance 5885, backward 6144, both 6429
+      const int bm = opt.bsgs_mode;
+      printf(bm == BM_SEQUENTIAL || bm == BM_GGSB || bm == BM_ANGRYGIANT ? "[+] Thread Key found privkey %s   "
+             : bm == BM_RANDOM                                          ? "[+] Thread Key found privkey %s    \n"
+                                                                        : "[+] Thread Key found privkey %s   \n",
+             k.c_str());
+      printf("[+] Publickey %s\n", pub.c_str());
+      FILE *f = fopen("KEYFOUNDKEYFOUND.txt", "a");
+      if (f) {
+        fprintf(f, "Key found privkey %s\nPublickey %s\n", k.c_str(), pub.c_str());
+        fclose(f);
+      }
+      fflush(stdout);
+    }
+    bool all = std::all_of(g_found.begin(), g_found.end(), [](uint8_t v) { return v != 0; });
+    if (all) {
+      printf("All points were found\n");
+      fflush(stdout);
+      _exit(EXIT_FAILURE);  // keyhunt.cpp:4811-4814
+    }
+  }
+}
+
 void bsgs_worker(bsgs_job *j) {
   kh_ctx *ctx = nullptr;
   int r = kh_open(j->device, &ctx);
@@ -858,7 +926,32 @@ void bsgs_worker(bsgs_job *j) {
   std::vector<kh_bsgs_found> found(nt + 1);
   std::vector<U> bases;
   std::vector<uint8_t> list_be;
+  const bool progression = opt.bsgs_mode == BM_SEQUENTIAL || opt.bsgs_mode == BM_ANGRYGIANT || opt.bsgs_mode == BM_GGSB;
   while (!r) {
+    if (progression) {
+      U st;
+      uint64_t nb = 0;
+      if (!take_progression(g_step, j->bases_per_call, st, nb)) break;
+      bases.assign(1, st);
+      uint8_t st_be[32];
+      u_to_be32(st, st_be);
+      uint32_t nf = 0;
+      if (u_cmp(g_step, twoN) == 0) {
+        r = kh_bsgs_scan(ctx, st_be, nb, found.data(), (uint32_t)found.size(), &nf);
+      } else {  // ggsb: bases 2 x block size apart, each walking its own 2N keys
+        list_be.resize(32 * nb);
+        U b = st;
+        for (uint64_t i = 0; i < nb; i++, b = u_add(b, g_step)) u_to_be32(b, &list_be[32 * i]);
+        r = kh_bsgs_scan_list(ctx, list_be.data(), nb, found.data(), (uint32_t)found.size(), &nf);
+      }
+      if (r) {
+        fprintf(stderr, "[E] kh_bsgs_scan: %s (%s)\n", kh_strerror(r), kh_last_error(ctx));
+        break;
+      }
+      g_bases_done += nb;
+      report_found(ctx, j, found, nf);
+      continue;
+    }
     if (!take_bases(g_step, j->bases_per_call, bases)) break;
     const uint64_t nb = bases.size();
     // consecutive ascending bases go through kh_bsgs_scan (one progression), others as a list
@@ -880,47 +973,7 @@ void bsgs_worker(bsgs_job *j) {
       break;
     }
     g_bases_done += nb;
-    for (uint32_t i = 0; i < nf; i++) {
-      uint32_t t = found[i].target;
-      std::lock_guard<std::mutex> lk(g_found_mtx);
-      if (g_found[t]) continue;
-      g_found[t] = 1;
-      std::string k = u_hex(u_from_be32(found[i].key));
-      uint8_t pxy[64];
-      kh_pubkeys(ctx, found[i].key, 1, pxy);
-      std::string pub;
-      if ((*j->comp)[t]) {
-        uint8_t p = (pxy[63] & 1) ? 3 : 2;
-        pub = hex(&p, 1) + hex(pxy, 32);
-      } else {
-        uint8_t p = 4;
-        pub = hex(&p, 1) + hex(pxy, 64);
-      }
-      {
-        std::lock_guard<std::mutex> lk2(g_keys_mtx);
-        // each BSGS worker of the reference has its own format: the sequential one (also -B ggsb and
-        // angrygiant) continues its string over a backslash-newline, so no newline is printed
-        // (keyhunt.cpp:4826-4827); random 5079, dance 5885, backward 6144, both 6429
-        const int bm = opt.bsgs_mode;
-        printf(bm == BM_SEQUENTIAL || bm == BM_GGSB || bm == BM_ANGRYGIANT ? "[+] Thread Key found privkey %s   "
-               : bm == BM_RANDOM                                          ? "[+] Thread Key found privkey %s    \n"
-                                                                          : "[+] Thread Key found privkey %s   \n",
-               k.c_str());
-        printf("[+] Publickey %s\n", pub.c_str());
-        FILE *f = fopen("KEYFOUNDKEYFOUND.txt", "a");
-        if (f) {
-          fprintf(f, "Key found privkey %s\nPublickey %s\n", k.c_str(), pub.c_str());
-          fclose(f);
-        }
-        fflush(stdout);
-      }
-      bool all = std::all_of(g_found.begin(), g_found.end(), [](uint8_t v) { return v != 0; });
-      if (all) {
-        printf("All points were found\n");
-        fflush(stdout);
-        _exit(EXIT_FAILURE);  // keyhunt.cpp:4811-4814
-      }
-    }
+    report_found(ctx, j, found, nf);
   }
   j->rc = r;
   kh_close(ctx);
