@@ -86,8 +86,12 @@ void *kh_gpu_thread_process(void *vargp) {
 	const int dev = thread_number % kh_gpu_devices();
 	bool fresh;
 	kh_ctx *gpu = kh_gpu_open_dev(dev, &fresh);
-	if (fresh)  /* the first thread of this device loads its targets */
+	/* -m rmd160 --rmd-batch-size (keyhunt.cpp:3301-3307): the reference's groups of that size */
+	const uint32_t group = FLAGMODE == MODE_RMD160 ? (uint32_t)rmd_batch_size : CPU_GRP_SIZE;
+	if (fresh) {  /* the first thread of this device loads its targets */
 		kh_gpu_check(gpu, kh_set_targets(gpu, (const uint8_t *)addressTable, N, N), "kh_set_targets");
+		kh_gpu_check(gpu, kh_set_rmd_batch(gpu, group), "kh_set_rmd_batch");
+	}
 	pthread_mutex_unlock(&kh_gpu_open_mutex);
 	uint8_t start_be[32], stride_be[32];
 	stride.Get32Bytes(stride_be);
@@ -122,7 +126,7 @@ void *kh_gpu_thread_process(void *vargp) {
 			else
 				writekey(hits[i].compressed != 0, &k);
 		}
-		steps[thread_number].fetch_add(N_SEQUENTIAL_MAX / 1024, std::memory_order_relaxed);
+		steps[thread_number].fetch_add((N_SEQUENTIAL_MAX + group - 1) / group, std::memory_order_relaxed);  /* one per group */
 	}
 	ends[thread_number] = 1;
 	return NULL;

@@ -386,6 +386,13 @@ __device__ __forceinline__ uint4 blk_load(const walk_args &A, const uint4 &r) {
 #ifdef KH_TIMING_NO_PROBE_LOADS
   // timing-only build: no HBM reads (outputs are wrong); isolates the probe's compute
   return make_uint4(r.x, r.x * 3u, r.x * 5u, r.x * 7u);
+#elif defined(KH_TIMING_PROBE_REGION_LOG2)
+  // timing-only build: every probe reads a block of the layer's first 2^LOG2 blocks, a region
+  // that stays on die (Infinity Cache / L2) -- the loads without their HBM traffic (outputs wrong)
+  return ld_nt16(reinterpret_cast<const uint4 *>(A.bloom) + (r.x & ((1u << KH_TIMING_PROBE_REGION_LOG2) - 1u)));
+#elif defined(KH_PROBE_PLAIN_LOAD)
+  const uint8_t *shard = A.bloom + (uint64_t)(r.w >> 24) * A.bstride32;
+  return reinterpret_cast<const uint4 *>(shard)[r.x];
 #else
   const uint8_t *shard = A.bloom + (uint64_t)(r.w >> 24) * A.bstride32;
   return ld_nt16(reinterpret_cast<const uint4 *>(shard) + r.x);
@@ -1048,6 +1055,14 @@ __global__ void k_test_bloom(const uint8_t *items, uint32_t n, uint32_t len, con
 namespace kh {
 
 hipError_t launch_walk(int mode, const walk_args &A, hipStream_t st, int H) {
+#ifdef KH_ISA_ONLY_BSGSB
+  // analysis builds (tools/isa_hot.py): the BSGS giant walk alone, compiled in seconds
+  constexpr int TB1 = walk_threads<KM_BSGSB, KH_WALK_HB>();
+  hipLaunchKernelGGL((k_walk<KM_BSGSB, KH_WALK_HB>), dim3((A.L + TB1 - 1) / TB1), dim3(TB1), 0, st, A);
+  (void)mode;
+  (void)H;
+  return hipGetLastError();
+#else
   if (A.zhalf) return launch_walk_zinv(mode, A, st);
   dim3 block(256), grid((A.L + 255) / 256);
   if (KH_XPOINT_DEFER && mode == KM_XPOINT && A.tblk) mode = KM_XPOINTB;
@@ -1094,9 +1109,16 @@ hipError_t launch_walk(int mode, const walk_args &A, hipStream_t st, int H) {
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
+#endif
 }
 
 hipError_t launch_walk_zinv(int mode, const walk_args &A, hipStream_t st) {
+#ifdef KH_ISA_ONLY_BSGSB
+  (void)mode;
+  (void)A;
+  (void)st;
+  return hipErrorInvalidValue;
+#else
   dim3 block(256), grid((A.L + 255) / 256);
   if (A.zhalf < 2 || A.zhalf > KH_WALK_H) return hipErrorInvalidValue;
   switch (mode) {
@@ -1111,6 +1133,7 @@ hipError_t launch_walk_zinv(int mode, const walk_args &A, hipStream_t st) {
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
+#endif
 }
 
 hipError_t launch_refine(const refine_args &A, hipStream_t st) {

@@ -22,7 +22,9 @@ pytestmark = pytest.mark.gpu
 E2E = json.load(open(os.path.join(GOLDEN, "ref_e2e.json")))
 PATCHED = os.path.join(REPO, "oracle", "_ref", "keyhunt_gpu")
 CASES = ["rmd160_66_window", "bsgs_125_window", "xpoint_63_window", "address_66_window", "bsgs_120_window",
-         "rmd160_1to32_compress_2p20", "bsgs_test120_b120"]
+         "rmd160_1to32_compress_2p20", "bsgs_test120_b120",
+         # --rmd-batch-size below 1024: the binding hands the reference's group size to kh_set_rmd_batch
+         "rmd160_batch512_both", "rmd160_batch1001_compress_endo"]
 
 
 def run_patched(argv, td=None, timeout=600):
