@@ -127,7 +127,8 @@ __device__ __forceinline__ bool blk_match(const uint4 &v, uint32_t s0, uint32_t 
 #else
   blk_masks(s0, s1, s2, m);
 #endif
-  return ((v.x & m[0]) == m[0]) & ((v.y & m[1]) == m[1]) & ((v.z & m[2]) == m[2]) & ((v.w & m[3]) == m[3]);
+  // a miss is a mask bit its block word lacks: OR the four words' misses and compare once
+  return ((m[0] & ~v.x) | (m[1] & ~v.y) | (m[2] & ~v.z) | (m[3] & ~v.w)) == 0;
 }
 __device__ __forceinline__ void blk_insert(uint8_t *__restrict__ bf_shard, const bloom_desc &bd, const fe &x) {
   uint32_t m[4];
@@ -595,7 +596,14 @@ __global__ void __launch_bounds__((walk_threads<MODE, H>()), (walk_blocks_per_cu
     // prefix[i-1] is fetched one iteration ahead so its HBM latency overlaps the previous pair
     uint4 pm = make_uint4(0u, 0u, 0u, 0u), pp = make_uint4(0u, 0u, 0u, 0u);  // DEFER: previous pair's probe records
     uint64_t poff = 0;
-    uint32_t plive = 0;
+    // liveness of the previous pair's points as two lane masks (bools across the loop edge):
+    // C - off lies inside the job iff off > lm, C + off iff off < hp (off = i + 1 <= H, so 32-bit
+    // compares against per-group thresholds replace the 64-bit index compares)
+    bool plm = false, plp = false;
+    const uint64_t nm = cidx < A.n_points ? 0u : cidx - A.n_points;   // (no min(): no u64 overload)
+    const uint64_t np = A.n_points > cidx ? A.n_points - cidx : 0u;
+    const uint32_t lm = nm < (uint64_t)H ? (uint32_t)nm : (uint32_t)H;
+    const uint32_t hp = np < (uint64_t)H ? (uint32_t)np : (uint32_t)H;
     // every point of this group, for every lane of the wave, lies inside the job (all but a job's
     // last groups): the per-pair liveness test then needs no 64-bit compares (xpoint +0.9 %; the BSGS
     // walk measured 0.2 % slower with it, so it keeps the compares)
@@ -636,25 +644,28 @@ __global__ void __launch_bounds__((walk_threads<MODE, H>()), (walk_blocks_per_cu
         // never an in-flight load destination.
         const uint4 vm = dload(pm), vp = dload(pp);
         fe xm, xp, s, dy, sx;
-        fe_add(sx, cx, tx);  // x3 = s^2 - (C.x + T.x) for both points
-        fe_add(dy, ty, cy);  // -(dy of C - T[i]); only s^2 is needed, so the sign drops out
+        // x3 = s^2 - (C.x + T.x) for both points; dy = -(dy of C - T[i]): only s^2 is needed, so
+        // the sign drops out.  Adjacent independent add/sub pairs share one interleaved chain.
+        fe_addsub2<false, false>(sx, cx, tx, dy, ty, cy);
         fe_mul(s, dy, di);
         fe_sqr(xm, s);
-        fe_sub(xm, xm, sx);
-        fe_sub(dy, ty, cy);
+        fe_addsub2<true, true>(xm, xm, sx, dy, ty, cy);
         fe_mul(s, dy, di);
         fe_sqr(xp, s);
         fe_sub(xp, xp, sx);
-        if ((plive & 1u) && blk_match_rec(vm, pm)) record_hit(A, cidx - poff, DKIND);
-        if ((plive & 2u) && blk_match_rec(vp, pp)) record_hit(A, cidx + poff, DKIND);
-        const uint64_t off = (uint64_t)(i + 1);
+        if (plm && blk_match_rec(vm, pm)) record_hit(A, cidx - poff, DKIND);
+        if (plp && blk_match_rec(vp, pp)) record_hit(A, cidx + poff, DKIND);
+        const uint32_t off = (uint32_t)(i + 1);
         pm = drec(xm);
         pp = drec(xp);
         poff = off;
-        if (wfull)
-          plive = i < H - 1 ? 3u : 1u;
-        else
-          plive = (cidx - off < A.n_points ? 1u : 0u) | (i < H - 1 && cidx + off < A.n_points ? 2u : 0u);
+        if (wfull) {
+          plm = true;
+          plp = i < H - 1;
+        } else {
+          plm = off > lm;
+          plp = off < hp;  // also false at i = H - 1 (off = H >= hp): C + H is the next group's
+        }
         continue;
       }
       if constexpr (MODE == KM_BSGS) {
@@ -698,8 +709,8 @@ __global__ void __launch_bounds__((walk_threads<MODE, H>()), (walk_blocks_per_cu
       }
     }
     if constexpr (DEFER) {  // the last pair of the group
-      if ((plive & 1u) && blk_match_rec(dload(pm), pm)) record_hit(A, cidx - poff, DKIND);
-      if ((plive & 2u) && blk_match_rec(dload(pp), pp)) record_hit(A, cidx + poff, DKIND);
+      if (plm && blk_match_rec(dload(pm), pm)) record_hit(A, cidx - poff, DKIND);
+      if (plp && blk_match_rec(dload(pp), pp)) record_hit(A, cidx + poff, DKIND);
     }
     // next centre C += T[H]  (keyhunt.cpp:3840-3855)
     {
@@ -1004,12 +1015,21 @@ __global__ void k_test_field(const uint32_t *a, const uint32_t *b, uint32_t n, u
   fe_inv(r, x);
 #pragma unroll
   for (int k = 0; k < 8; k++) o[16 + k] = r.d[k];
-  fe_add(r, x, y);
+  // add and sub: even inputs through the single forms, odd ones through the paired-chain form
+  // (fe_addsub2, both operand orders), so every wave runs both and their rare fix-ups side by side
+  fe q;
+  if ((i & 1) == 0) {
+    fe_add(r, x, y);
+    fe_sub(q, x, y);
+  } else if ((i & 3) == 1) {
+    fe_addsub2<false, true>(r, x, y, q, x, y);
+  } else {
+    fe_addsub2<true, false>(q, x, y, r, x, y);
+  }
 #pragma unroll
   for (int k = 0; k < 8; k++) o[24 + k] = r.d[k];
-  fe_sub(r, x, y);
 #pragma unroll
-  for (int k = 0; k < 8; k++) o[32 + k] = r.d[k];
+  for (int k = 0; k < 8; k++) o[32 + k] = q.d[k];
 }
 
 // bloom_check of n items of `len` bytes (20 or 32); shard = first byte when sharded.

@@ -116,10 +116,85 @@ KH_HD void fe_canon(fe &r) {
 // (a carry rippling past limb 1, a value in [p, 2^256)).  When no lane needs it the wave jumps
 // over it with one scalar branch; when taken, lanes that do not need it run it as a no-op.
 __device__ __forceinline__ bool kh_any(bool v) { return __builtin_amdgcn_ballot_w64(v) != 0; }
+__device__ __forceinline__ uint32_t kh_lane() {
+  return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+}
+#endif
+
+// KH_ADDSUB_MAD: the +-0x1000003D1 fix-up of fe_add / fe_sub on limbs 0..1 as ONE 64-bit
+// multiply-add.  0x1000003D1 = 3 * 1431656091, so with a selector s in {0, 3} (add) or {0, -3}
+// (sub, signed v_mad_i64_i32), {r0, r1} + s * 1431656091 is the fix-up mod 2^64; the multiply-add's
+// carry-out (add) or a grown limb 1 (sub: subtracting 0x1000003D1 < 2^33 wraps iff the new limb 1
+// exceeds the old) flags the rare ripple past limb 1 as a lane mask the SALU tests.  Replaces two
+// selects, an add pair and a bool-to-mask round trip per call.
+#ifndef KH_ADDSUB_MAD
+#define KH_ADDSUB_MAD 1
+#endif
+#define KH_P_DIV3 1431656091u
+
+#if defined(__HIP_DEVICE_COMPILE__)
+// a*b + c with b wave-uniform (an SGPR); m = the lane mask of the sum's 65th bit
+__device__ __forceinline__ uint64_t mad_co(uint32_t a, uint32_t b, uint64_t c, uint64_t &m) {
+  uint64_t d;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(d), "=s"(m) : "v"(a), "s"(b), "v"(c));
+  return d;
+}
+// signed a*b + c mod 2^64 with b wave-uniform
+__device__ __forceinline__ uint64_t mad_i_s(uint32_t a, uint32_t b, uint64_t c) {
+  uint64_t d, m;
+  asm("v_mad_i64_i32 %0, %1, %2, %3, %4" : "=v"(d), "=s"(m) : "v"(a), "s"(b), "v"(c));
+  return d;
+}
+__device__ __forceinline__ uint64_t pack64(uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; }
+#endif
+
+#if defined(__HIP_DEVICE_COMPILE__)
+// The pieces of the KH_ADDSUB_MAD forms.  Tail of an addition: limbs 0..1 of r += c * 0x1000003D1;
+// m = lanes whose fix-up carries past limb 1; returns the lanes that need fe_add_fix (m, or a top
+// limb of all ones: r may be in [p, 2^256)).
+__device__ __forceinline__ uint64_t fe_add_tail(fe &r, uint32_t c, uint64_t &m) {
+  const uint64_t lo = mad_co(c ? 3u : 0u, KH_P_DIV3, pack64(r.d[0], r.d[1]), m);
+  r.d[0] = (uint32_t)lo;
+  r.d[1] = (uint32_t)(lo >> 32);
+  return m | __builtin_amdgcn_ballot_w64(r.d[7] == 0xFFFFFFFFu);
+}
+__device__ __forceinline__ void fe_add_fix(fe &r, uint64_t m) {
+  uint32_t c1 = (uint32_t)(m >> kh_lane()) & 1u;
+#pragma unroll
+  for (int i = 2; i < 8; i++) r.d[i] = addc(r.d[i], 0, c1, c1);
+  fe_canon(r);
+}
+// Tail of a subtraction: limbs 0..1 of r -= br * 0x1000003D1; returns the lanes whose borrow
+// ripples past limb 1 (limb 1 grew)
+__device__ __forceinline__ uint64_t fe_sub_tail(fe &r, uint32_t br) {
+  const uint32_t r1 = r.d[1];
+  const uint64_t lo = mad_i_s(br ? 0xFFFFFFFDu : 0u, KH_P_DIV3, pack64(r.d[0], r.d[1]));  // -3 * ...
+  r.d[0] = (uint32_t)lo;
+  r.d[1] = (uint32_t)(lo >> 32);
+  uint64_t m;
+  asm("v_cmp_gt_u32 %0, %1, %2" : "=s"(m) : "v"(r.d[1]), "v"(r1));
+  return m;
+}
+__device__ __forceinline__ void fe_sub_fix(fe &r, uint64_t m) {
+  uint32_t b2 = (uint32_t)(m >> kh_lane()) & 1u;
+#pragma unroll
+  for (int i = 2; i < 8; i++) r.d[i] = subb(r.d[i], 0, b2, b2);
+}
 #endif
 
 KH_HD void fe_add(fe &r, const fe &a, const fe &b) {
 #if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (KH_ADDSUB_MAD) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) r.d[i] = addc(a.d[i], b.d[i], c, c);
+    uint64_t m;
+    if (fe_add_tail(r, c, m) != 0) {
+      KH_RARE_MARK();
+      fe_add_fix(r, m);
+    }
+    return;
+  }
   // a, b < p.  r = a + b; on a carry out of 2^256 (a + b - 2^256 < p) add 2^256 - p = 0x1000003D1:
   // the carry past limb 1 is rare.  Without a carry r < 2^256 is >= p only if its top limb is
   // all ones (rare).
@@ -156,6 +231,14 @@ KH_HD void fe_sub(fe &r, const fe &a, const fe &b) {
 #pragma unroll
   for (int i = 0; i < 8; i++) r.d[i] = subb(a.d[i], b.d[i], br, br);
 #if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (KH_ADDSUB_MAD) {
+    const uint64_t m = fe_sub_tail(r, br);
+    if (m != 0) {
+      KH_RARE_MARK();
+      fe_sub_fix(r, m);
+    }
+    return;
+  }
   // borrow: r += p == r -= 0x1000003D1 (mod 2^256); the borrow past limb 1 is rare
   {
     uint32_t b2;
@@ -180,6 +263,42 @@ KH_HD void fe_neg(fe &r, const fe &a) {
   fe z;
   fe_set_u32(z, 0);
   fe_sub(r, z, a);
+}
+
+// r = a (+|-) b and q = x (+|-) y (SUB1 / SUB2 pick subtraction), two independent operations with
+// their carry chains interleaved limb by limb (KH_CHAIN2): each chain's next link reads a carry
+// the other chain's link separates from its write, filling the pad a lone chain needs per link.
+// Same results as the two single calls; r may alias a or b, q may alias x or y (never across).
+#ifndef KH_CHAIN2
+#define KH_CHAIN2 1
+#endif
+template <bool SUB1, bool SUB2>
+KH_HD void fe_addsub2(fe &r, const fe &a, const fe &b, fe &q, const fe &x, const fe &y) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (KH_ADDSUB_MAD && KH_CHAIN2) {
+    uint32_t c = 0, d = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      r.d[i] = SUB1 ? subb(a.d[i], b.d[i], c, c) : addc(a.d[i], b.d[i], c, c);
+      q.d[i] = SUB2 ? subb(x.d[i], y.d[i], d, d) : addc(x.d[i], y.d[i], d, d);
+    }
+    uint64_t m1 = 0, m2 = 0, f1, f2;
+    if constexpr (SUB1) f1 = fe_sub_tail(r, c); else f1 = fe_add_tail(r, c, m1);
+    if constexpr (SUB2) f2 = fe_sub_tail(q, d); else f2 = fe_add_tail(q, d, m2);
+    if ((f1 | f2) != 0) {
+      KH_RARE_MARK();
+      if (f1 != 0) {
+        if constexpr (SUB1) fe_sub_fix(r, f1); else fe_add_fix(r, m1);
+      }
+      if (f2 != 0) {
+        if constexpr (SUB2) fe_sub_fix(q, f2); else fe_add_fix(q, m2);
+      }
+    }
+    return;
+  }
+#endif
+  if constexpr (SUB1) fe_sub(r, a, b); else fe_add(r, a, b);
+  if constexpr (SUB2) fe_sub(q, x, y); else fe_add(q, x, y);
 }
 
 // 512-bit t (16 limbs) -> canonical r.  t = lo + hi*2^256 == lo + hi*(2^32 + 977) (mod p).
@@ -262,17 +381,12 @@ __device__ __forceinline__ uint64_t mad_nc(uint32_t a, uint32_t b, uint64_t acc)
 #ifndef KH_COLS
 #define KH_COLS 1
 #endif
-#include "kh_cols.h"
-
-#if defined(__HIP_DEVICE_COMPILE__)
-// a*b + c with b wave-uniform (an SGPR); m = the lane mask of the sum's 65th bit
-__device__ __forceinline__ uint64_t mad_co(uint32_t a, uint32_t b, uint64_t c, uint64_t &m) {
-  uint64_t d;
-  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(d), "=s"(m) : "v"(a), "s"(b), "v"(c));
-  return d;
-}
-__device__ __forceinline__ uint64_t pack64(uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; }
+// KH_MULRED: fe_mul's reduction slices and chain links issued inside its last column statements
+// (kh_cols.h mul_red_cols), so the chain's carries wait behind column work instead of s_nop pads
+#ifndef KH_MULRED
+#define KH_MULRED 1
 #endif
+#include "kh_cols.h"
 
 // The fold with 64-bit multiply-adds only (device): with h = t[8..15], l = t[0..7],
 //   t == sum_{j even} V_j 2^(32j) + sum_{i odd} W_i 2^(32i)  (mod p),
@@ -285,11 +399,60 @@ __device__ __forceinline__ uint64_t pack64(uint32_t lo, uint32_t hi) { return ((
 // in [p, 2^256), puts the lost bits back into R and redoes the second fold the long way -- from R
 // and the masks only, so t is dead after the mads.  Replaces the 64-bit adds and zero-extension
 // moves of the long form (fe_reduce512_gen) by multiply-adds.
+#if defined(__HIP_DEVICE_COMPILE__)
+// The second fold and the rare block, from the chain's limbs R[0..8] (R = A + B 2^32) and the slice
+// masks; r9() gives a lane's carry out of limb 8 (0/1), read in the rare block only.
+template <typename R9F>
+__device__ __forceinline__ void fe_reduce_tail(fe &r, uint32_t R[9], uint64_t m0, uint64_t m1, uint64_t m2,
+                                               uint64_t m3, uint64_t m4, uint64_t m5, uint64_t m6, uint64_t m7,
+                                               R9F r9) {
+  const uint32_t K = 977u;
+  uint64_t m8;
+  // second fold: R8 (2^32 + 977) at limb 0
+  const uint64_t X = mad_co(R[8], K, pack64(R[0], R[1]), m8);
+  r.d[0] = (uint32_t)X;
+#pragma unroll
+  for (int i = 3; i < 8; i++) r.d[i] = R[i];
+  // limbs 1..2 (+ R8 at limb 1) with the carry past limb 2 and the [p, 2^256) candidates as SGPR
+  // lane masks (a bool carry read back through a ballot would round-trip through a VGPR); a
+  // carry out of limb 8 (R9) leaves R8 = 0, so the mask of R8 == 0 stands for it
+  uint64_t c2m, f7, c1m;
+  asm("v_add_co_u32 %0, %3, %5, %6\n\tv_cmp_eq_u32 %4, -1, %8\n\ts_nop 0\n\tv_addc_co_u32 %1, %2, %7, 0, %3"
+      : "=&v"(r.d[1]), "=v"(r.d[2]), "=s"(c2m), "=&s"(c1m), "=&s"(f7)
+      : "v"((uint32_t)(X >> 32)), "v"(R[8]), "v"(R[2]), "v"(R[7]));
+  if ((m0 | m1 | m2 | m3 | m4 | m5 | m6 | m7 | m8 | c2m | f7 | __builtin_amdgcn_ballot_w64(R[8] == 0)) != 0) {
+    // rare: put back the 2^64 each overflowing V_j / W_i lost (limb j+2 / i+2; lane bits of
+    // the masks), then the second fold the long way from R: h = R8 + R9 2^32 < 2^34
+    KH_RARE_MARK();
+    const uint32_t lane = kh_lane();
+    const uint64_t ms[8] = {m0, m1, m2, m3, m4, m5, m6, m7};
+    uint32_t cc = 0, Rq[9];
+#pragma unroll
+    for (int q = 0; q < 9; q++) Rq[q] = R[q];
+#pragma unroll
+    for (int q = 2; q < 9; q++) Rq[q] = addc(Rq[q], (uint32_t)(ms[q - 2] >> lane) & 1u, cc, cc);
+    const uint32_t R9 = r9() + cc + ((uint32_t)(m7 >> lane) & 1u);
+    const uint64_t h = (uint64_t)Rq[8] + ((uint64_t)R9 << 32);
+    uint64_t v = h * 977u + Rq[0];
+    r.d[0] = (uint32_t)v;
+    v = (v >> 32) + Rq[1] + (h & 0xFFFFFFFFu);
+    r.d[1] = (uint32_t)v;
+    v = (v >> 32) + Rq[2] + (h >> 32);
+    r.d[2] = (uint32_t)v;
+    cc = (uint32_t)(v >> 32);
+#pragma unroll
+    for (int i = 3; i < 8; i++) r.d[i] = addc(Rq[i], 0, cc, cc);
+    if (cc) fe_sub_p(r);  // wrapped past 2^256 once: + 0x1000003D1 cannot wrap again
+    fe_canon(r);
+  }
+}
+#endif
+
 KH_HD void fe_reduce512(fe &r, const uint32_t t[16]) {
 #if defined(__HIP_DEVICE_COMPILE__)
   if constexpr (KH_RED2) {
     const uint32_t K = 977u;
-    uint64_t m0, m1, m2, m3, m4, m5, m6, m7, m8;
+    uint64_t m0, m1, m2, m3, m4, m5, m6, m7;
     const uint64_t V0 = mad_co(t[8], K, pack64(t[0], t[1]), m0);
     const uint64_t W1 = mad_co(t[9], K, pack64(t[8], t[9]), m1);
     const uint64_t V2 = mad_co(t[10], K, pack64(t[2], t[3]), m2);
@@ -298,7 +461,7 @@ KH_HD void fe_reduce512(fe &r, const uint32_t t[16]) {
     const uint64_t W5 = mad_co(t[13], K, pack64(t[12], t[13]), m5);
     const uint64_t V6 = mad_co(t[14], K, pack64(t[6], t[7]), m6);
     const uint64_t W7 = mad_co(t[15], K, pack64(t[14], t[15]), m7);
-    uint32_t R[10], c;
+    uint32_t R[9], c, R9;
     R[0] = (uint32_t)V0;
     R[1] = addc((uint32_t)(V0 >> 32), (uint32_t)W1, 0, c);
     R[2] = addc((uint32_t)V2, (uint32_t)(W1 >> 32), c, c);
@@ -307,38 +470,8 @@ KH_HD void fe_reduce512(fe &r, const uint32_t t[16]) {
     R[5] = addc((uint32_t)(V4 >> 32), (uint32_t)W5, c, c);
     R[6] = addc((uint32_t)V6, (uint32_t)(W5 >> 32), c, c);
     R[7] = addc((uint32_t)(V6 >> 32), (uint32_t)W7, c, c);
-    uint32_t c1, c2;
-    R[8] = addc((uint32_t)(W7 >> 32), 0, c, R[9]);
-    // second fold: R8 (2^32 + 977) at limb 0
-    const uint64_t X = mad_co(R[8], K, pack64(R[0], R[1]), m8);
-    r.d[0] = (uint32_t)X;
-    r.d[1] = addc((uint32_t)(X >> 32), R[8], 0, c1);
-    r.d[2] = addc(R[2], 0, c1, c2);
-#pragma unroll
-    for (int i = 3; i < 8; i++) r.d[i] = R[i];
-    if ((m0 | m1 | m2 | m3 | m4 | m5 | m6 | m7 | m8) != 0 || kh_any((R[9] | c2) != 0 || r.d[7] == 0xFFFFFFFFu)) {
-      // rare: put back the 2^64 each overflowing V_j / W_i lost (limb j+2 / i+2; lane bits of
-      // the masks), then the second fold the long way from R: h = R8 + R9 2^32 < 2^34
-      KH_RARE_MARK();
-      const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-      const uint64_t ms[8] = {m0, m1, m2, m3, m4, m5, m6, m7};
-      uint32_t cc = 0;
-#pragma unroll
-      for (int q = 2; q < 9; q++) R[q] = addc(R[q], (uint32_t)(ms[q - 2] >> lane) & 1u, cc, cc);
-      R[9] += cc + ((uint32_t)(m7 >> lane) & 1u);
-      const uint64_t h = (uint64_t)R[8] + ((uint64_t)R[9] << 32);
-      uint64_t v = h * 977u + R[0];
-      r.d[0] = (uint32_t)v;
-      v = (v >> 32) + R[1] + (h & 0xFFFFFFFFu);
-      r.d[1] = (uint32_t)v;
-      v = (v >> 32) + R[2] + (h >> 32);
-      r.d[2] = (uint32_t)v;
-      cc = (uint32_t)(v >> 32);
-#pragma unroll
-      for (int i = 3; i < 8; i++) r.d[i] = addc(R[i], 0, cc, cc);
-      if (cc) fe_sub_p(r);  // wrapped past 2^256 once: + 0x1000003D1 cannot wrap again
-      fe_canon(r);
-    }
+    R[8] = addc((uint32_t)(W7 >> 32), 0, c, R9);
+    fe_reduce_tail(r, R, m0, m1, m2, m3, m4, m5, m6, m7, [&]() { return R9; });
     return;
   }
 #endif
@@ -348,6 +481,16 @@ KH_HD void fe_reduce512(fe &r, const uint32_t t[16]) {
 KH_HD void fe_mul(fe &r, const fe &a, const fe &b) {
   uint32_t t[16];
 #if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (KH_COLS && KH_RED2 && KH_MULRED) {
+    // the columns with the reduction's slices and first chain links interleaved (kh_cols.h)
+    uint32_t R[9];
+    uint64_t mk[8], r9;
+    mul_red_cols(a.d, b.d, R, mk, r9);
+    (void)t;
+    fe_reduce_tail(r, R, mk[0], mk[1], mk[2], mk[3], mk[4], mk[5], mk[6], mk[7],
+                   [&]() { return (uint32_t)(r9 >> kh_lane()) & 1u; });
+    return;
+  }
   if constexpr (KH_COLS) {
     mul_cols(a.d, b.d, t);  // the same columns, one scheduled asm statement each (kh_cols.h)
     fe_reduce512(r, t);

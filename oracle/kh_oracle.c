@@ -1127,15 +1127,49 @@ int or_bsgs_refine(const or_bsgs_params *p, const uint8_t *bf2, const uint8_t *b
   return 0;
 }
 
+/* The engine's blocked layer 1 (its own layout, in place of the reference's layer-1 bloom_check
+ * of keyhunt.cpp:4819-4822; specified in keyhunt_amd/csrc/kh_kernels.h, KH_PK_MASKS, restated
+ * here independently of the device code): shard X[0] holds `blocks` 16-byte blocks; the item's
+ * block is (u * blocks) >> 32 with u the big-endian u32 X[8..12); little-endian block word w must
+ * cover, with s the big-endian u32 X[12 + 4*(w/2) ..), a = s >> 8*(w%2) and b = a >> 4, the bits
+ * a & 15, 16 + ((a >> 16) & 15), b & 15 and 16 + ((b >> 16) & 15). */
+static uint32_t rd_be32(const uint8_t *b) {
+  return ((uint32_t)b[0] << 24) | ((uint32_t)b[1] << 16) | ((uint32_t)b[2] << 8) | b[3];
+}
+int or_blk_check(const uint8_t *bf1, uint64_t blocks, const uint8_t x[32]) {
+  const uint8_t *blk = bf1 + (uint64_t)x[0] * blocks * 16 + ((rd_be32(x + 8) * blocks) >> 32) * 16;
+  for (int w = 0; w < 4; w++) {
+    uint32_t a = rd_be32(x + 12 + 4 * (w / 2)) >> (8 * (w % 2)), b = a >> 4;
+    uint32_t mask = (1u << (a & 15)) | (1u << (16 + ((a >> 16) & 15))) | (1u << (b & 15)) |
+                    (1u << (16 + ((b >> 16) & 15)));
+    uint32_t word = (uint32_t)blk[4 * w] | ((uint32_t)blk[4 * w + 1] << 8) | ((uint32_t)blk[4 * w + 2] << 16) |
+                    ((uint32_t)blk[4 * w + 3] << 24);
+    if ((word & mask) != mask) return 0;
+  }
+  return 1;
+}
+
 /* Giant-step scan over whole bases [start, start + n_bases*2N) for ONE target, exactly as the
  * sequential worker does (keyhunt.cpp:4549-4888): per base, startP = Q - (base + 1025M)G,
  * 1024-point groups along GSn[i] = -(i+1)*2M*G, probe bloom1[X[0]] with the 32-byte X, refine
  * candidates.  Stops at the first found key (bsgs_found).  cand_out (optional): list of
- * (base index, a) first-level candidates, in order.  Returns 1 if found. */
+ * (base index, a) first-level candidates, in order.  Returns 1 if found.  l1_blocks != 0: layer 1
+ * is the engine's blocked layout with that many blocks per shard (or_blk_check), else the
+ * reference's bloom. */
+int or_bsgs_scan_l1(const or_bsgs_params *p, const uint8_t *bf1, uint64_t l1_blocks, const uint8_t *bf2,
+                    const uint8_t *bf3, const or_bxrow *table, const uint8_t start_be[32], uint64_t n_bases,
+                    const uint8_t qx[32], const uint8_t qy[32], uint8_t key_out[32],
+                    uint64_t *cand_out, uint64_t cand_cap, uint64_t *n_cand);
 int or_bsgs_scan(const or_bsgs_params *p, const uint8_t *bf1, const uint8_t *bf2, const uint8_t *bf3,
                  const or_bxrow *table, const uint8_t start_be[32], uint64_t n_bases,
                  const uint8_t qx[32], const uint8_t qy[32], uint8_t key_out[32],
                  uint64_t *cand_out, uint64_t cand_cap, uint64_t *n_cand) {
+  return or_bsgs_scan_l1(p, bf1, 0, bf2, bf3, table, start_be, n_bases, qx, qy, key_out, cand_out, cand_cap, n_cand);
+}
+int or_bsgs_scan_l1(const or_bsgs_params *p, const uint8_t *bf1, uint64_t l1_blocks, const uint8_t *bf2,
+                    const uint8_t *bf3, const or_bxrow *table, const uint8_t start_be[32], uint64_t n_bases,
+                    const uint8_t qx[32], const uint8_t qy[32], uint8_t key_out[32],
+                    uint64_t *cand_out, uint64_t cand_cap, uint64_t *n_cand) {
   bsgs_ctx c; bsgs_ctx_init(&c, p, bf1, bf2, bf3, table);
   ge Q; fe_from_be(&Q.x, qx); fe_from_be(&Q.y, qy); Q.inf = 0;
   /* GSn[i] = -(i+1)*2M*G, _2GSn = 2*GSn[511] (keyhunt.cpp:1797-1816) */
@@ -1165,7 +1199,8 @@ int or_bsgs_scan(const or_bsgs_params *p, const uint8_t *bf1, const uint8_t *bf2
       for (int i = 0; i < GRP && !found; i++) {
         uint8_t xr[32];
         fe_to_be(xr, &pts[i].x);
-        if (or_bloom_check(bf1 + xr[0] * p->bytes[0], p->bits[0], p->hashes[0], xr, 32)) {
+        if (l1_blocks ? or_blk_check(bf1, l1_blocks, xr)
+                      : or_bloom_check(bf1 + xr[0] * p->bytes[0], p->bits[0], p->hashes[0], xr, 32)) {
           uint32_t a = (uint32_t)(j * 1024 + i);
           if (cand_out && nc < cand_cap) { cand_out[2 * nc] = b; cand_out[2 * nc + 1] = a; }
           nc++;

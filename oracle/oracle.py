@@ -242,6 +242,7 @@ def bsgs_params(n: int, k: int) -> BsgsParams:
 class BsgsTables:
     def __init__(self, p: BsgsParams, build: bool = True):
         self.p = p
+        self.l1_blocks = 0   # reference-layout layer 1
         self.bf1 = ctypes.create_string_buffer(256 * p.bytes[0])
         self.bf2 = ctypes.create_string_buffer(256 * p.bytes[1])
         self.bf3 = ctypes.create_string_buffer(256 * p.bytes[2])
@@ -250,10 +251,15 @@ class BsgsTables:
             lib().or_bsgs_build(ctypes.byref(p), self.bf1, self.bf2, self.bf3, self.table)
 
     @classmethod
-    def from_raw(cls, p: BsgsParams, bf1: bytes, bf2: bytes, bf3: bytes, table: bytes) -> "BsgsTables":
+    def from_raw(cls, p: BsgsParams, bf1: bytes, bf2: bytes, bf3: bytes, table: bytes,
+                 l1_blocks: int = 0) -> "BsgsTables":
         """Tables given as bytes (reference layout), e.g. ones already checked byte-identical to the
-        reference's: skips the oracle's own (slow, single-threaded) baby-step build."""
+        reference's: skips the oracle's own (slow, single-threaded) baby-step build.  l1_blocks != 0:
+        bf1 is the engine's blocked layer 1 with that many 16-byte blocks per shard (or_blk_check)."""
         t = cls(p, build=False)
+        t.l1_blocks = l1_blocks
+        if l1_blocks:
+            t.bf1 = ctypes.create_string_buffer(256 * 16 * l1_blocks)
         assert len(bf1) == len(t.bf1.raw) and len(bf2) == len(t.bf2.raw) and len(bf3) == len(t.bf3.raw)
         assert len(table) == ctypes.sizeof(t.table)
         ctypes.memmove(t.bf1, bf1, len(bf1))
@@ -269,9 +275,10 @@ class BsgsTables:
         key = ctypes.create_string_buffer(32)
         cands = (ctypes.c_uint64 * (2 * cand_cap))()
         ncand = ctypes.c_uint64()
-        found = lib().or_bsgs_scan(ctypes.byref(self.p), self.bf1, self.bf2, self.bf3, self.table, be32(start),
-                                   ctypes.c_uint64(n_bases), be32(q[0]), be32(q[1]), key, cands,
-                                   ctypes.c_uint64(cand_cap), ctypes.byref(ncand))
+        found = lib().or_bsgs_scan_l1(ctypes.byref(self.p), self.bf1, ctypes.c_uint64(self.l1_blocks),
+                                      self.bf2, self.bf3, self.table, be32(start),
+                                      ctypes.c_uint64(n_bases), be32(q[0]), be32(q[1]), key, cands,
+                                      ctypes.c_uint64(cand_cap), ctypes.byref(ncand))
         nc = min(ncand.value, cand_cap)
         cl = [(cands[2 * i], cands[2 * i + 1]) for i in range(nc)]
         return (int.from_bytes(key.raw, "big") if found else None), cl

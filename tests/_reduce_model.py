@@ -32,9 +32,12 @@ def fast(T):
     full = _slices(T)
     rare = {f"{'V' if k % 2 == 0 else 'W'}{k}" for k, v in full.items() if v >> 64}
     R = _chain(full)
-    if R >> 288:
-        rare.add("c8")
     R8 = (R >> 256) & M32
+    # the device tests R8 == 0, which a carry out of limb 8 (R9) implies (R8 = W7.hi + c wraps to 0)
+    if R >> 288:
+        assert R8 == 0
+    if R8 == 0:
+        rare.add("c8")
     X = R8 * 977 + (R & M64)
     if X >> 64:
         rare.add("m8")

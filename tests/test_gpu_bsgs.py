@@ -45,9 +45,13 @@ def test_candidates_and_key_vs_oracle(engine, oracle, n, k):
     # no hit in the first 3 bases: the same first-level candidates as the oracle; found in the 4th
     engine.bsgs_set_targets([q])
     c0 = engine.bsgs_candidates()
+    engine.bsgs_log_candidates(True)
     assert engine.bsgs_scan(start, 3) == []
+    got = sorted((b, a) for b, a, _ in engine.bsgs_logged_candidates())
+    engine.bsgs_log_candidates(False)
     okey, ocands = tabs.scan(start, 3, q)
-    assert okey is None and engine.bsgs_candidates() - c0 == len(ocands)
+    # the same first-level candidates (base, giant index), not only as many
+    assert okey is None and engine.bsgs_candidates() - c0 == len(ocands) and got == ocands
     found = engine.bsgs_scan(start + 3 * 2 * p.n, 1)
     assert found == [(0, key)]
     okey, _ = tabs.scan(start, 4, q)
@@ -91,6 +95,38 @@ def test_candidate_list_and_masks_vs_oracle(engine, oracle):
     ref = json.load(open(os.path.join(GOLDEN, "ref_tables.json")))["n100000000_k64"]["files"]
     tbl = raw[3] + hashlib.sha256(raw[3]).digest()
     assert hashlib.sha256(tbl).hexdigest() == ref[f"keyhunt_bsgs_2_{p.m3}.tbl"]
+
+
+def test_blocked_layer1_candidate_list_vs_oracle(engine, oracle):
+    """The shipped layer-1 layout (blocked, the engine's own) on the same footing as the reference
+    layout above: over 8000 bases (8.2M giant points) the engine's first-level candidates are
+    exactly those of the oracle's sequential worker probing the blocked layout by its specification
+    (oracle/kh_oracle.c or_blk_check), false positives included, and each one's layer-2 mask equals
+    the oracle's bsgs_secondcheck.  Layer 1 is handed over as the engine built it (its bytes are
+    pinned to the specification by test_blocked_layer1_bytes_match_layout_spec); layers 2-3 and the
+    bP rows are the reference layout."""
+    n, k, nb = 1 << 32, 64, 8000
+    p = oracle.bsgs_params(n, k)
+    info = engine.bsgs_setup(n, k, layer1=1)
+    assert info.layer1_layout == 1
+    blocks = info.bloom_bits[0] // 128
+    engine.bsgs_build()
+    raw = [engine.get_bloom(1), engine.get_bloom(2), engine.get_bloom(3), engine.get_bsgs_table()]
+    assert len(raw[0]) == 256 * 16 * blocks
+    tabs = oracle.BsgsTables.from_raw(p, *raw, l1_blocks=blocks)
+    key = 0x5A5A5A5A123456
+    q = oracle.pubkey(key)
+    start = key - nb * 2 * p.n + 12345        # the key lies in the last base
+    okey, ocands = tabs.scan(start, nb, q)
+    assert okey == key and len(ocands) >= 2   # false positives and the true candidate
+    engine.bsgs_set_targets([q])
+    engine.bsgs_log_candidates(True)
+    assert engine.bsgs_scan(start, nb) == [(0, key)]
+    got = sorted(engine.bsgs_logged_candidates())
+    engine.bsgs_log_candidates(False)
+    assert [(b, a) for b, a, _ in got][: len(ocands)] == ocands
+    omask = oracle.bsgs_second_masks(tabs, [start + b * 2 * p.n + a * 2 * p.m for b, a in ocands], q)
+    assert [m for _, _, m in got[: len(ocands)]] == omask
 
 
 BSGS_CASES = [k for k in E2E if k.startswith("bsgs")]

@@ -37,6 +37,14 @@ def test_field_ops_random(engine):
                                              2**255 - 1]
     a = [rng.randrange(P) for _ in range(4096)] + [0, 1, P - 1, 2**255, P - 2**32] + edges + edges[::-1]
     b = [rng.randrange(P) for _ in range(4096)] + [P - 1, P - 1, P - 1, 2**255, 2**32] + edges + edges
+    # fix-ups of +-0x1000003D1 that ripple past limb 1 (the kernel's rare blocks), each pair four times
+    # so it runs through the single and both paired-chain forms: a - b wraps with low 64 bits below
+    # 0x1000003D1; a + b carries out of 2^256 with low 64 bits at or above 2^64 - 0x1000003D1
+    ripple = [(2**64 + 7, 5 * 2**64 + 3), (0, 1), (2**64, 2**128), (P - 1, 2**255 + 0x1000003CD),
+              (2**255 + 0x1000003CD, P - 1), (P - 1, P - 2**64 + 0x1000003D1 + 0x1000003D2 - 1)]
+    for x, y in ripple:
+        a += [x] * 4
+        b += [y] * 4
     got = engine.field_ops(a, b)
     for x, y, (mul, sqr, inv, add, sub) in zip(a, b, got):
         assert mul == x * y % P

@@ -203,3 +203,36 @@ def test_oracle_second_masks_window(oracle):
     for d, m in zip(ds, masks):
         assert (m >> min(d // (2 * p.m2), 31)) & 1, (d, hex(m))
     assert oracle.bsgs_second_masks(t, [0], q) == [0]
+
+
+def test_oracle_blocked_layer1_check_vs_spec_model(oracle):
+    """or_blk_check (the oracle's probe of the engine's blocked layer 1) against a filter written
+    from the layout's specification in Python (the same model test_blocked_layer1_bytes_match_
+    layout_spec pins the GPU build to): every inserted X passes, and random X's pass at about the
+    fill-implied rate only."""
+    import ctypes
+    rng = random.Random(5)
+    blocks = 64
+    model = bytearray(256 * blocks * 16)
+
+    def words(xb):
+        base = xb[0] * blocks * 16 + ((int.from_bytes(xb[8:12], "big") * blocks) >> 32) * 16
+        s = [int.from_bytes(xb[12 + 4 * q:16 + 4 * q], "big") for q in range(2)]
+        for w in range(4):
+            a = s[w // 2] >> (8 * (w % 2))
+            for v in (a, a >> 4):
+                for f in (v & 15, 16 + ((v >> 16) & 15)):
+                    yield base + 4 * w + (f >> 3), 1 << (f & 7)
+
+    ins = [rng.getrandbits(256).to_bytes(32, "big") for _ in range(3000)]
+    for xb in ins:
+        for off, bit in words(xb):
+            model[off] |= bit
+    buf = ctypes.create_string_buffer(bytes(model), len(model))
+    chk = oracle.lib().or_blk_check
+    assert all(chk(buf, ctypes.c_uint64(blocks), xb) == 1 for xb in ins)
+    rnd = [rng.getrandbits(256).to_bytes(32, "big") for _ in range(20000)]
+    hits = sum(chk(buf, ctypes.c_uint64(blocks), xb) for xb in rnd)
+    # a random X passes iff all 16 of its bits are set: the model says so too
+    exp = sum(all(model[o] & b for o, b in words(xb)) for xb in rnd)
+    assert hits == exp and hits < 200

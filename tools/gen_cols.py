@@ -112,6 +112,158 @@ def emit_column(name_acc: str, prods: list[tuple[str, str]], safe: int, first_ze
             f'{indent}    : {ins});\n'), counted
 
 
+def col_asm_named(n: int, safe: int, first_zero: bool, extras: list[str]):
+    """Column text with named operands ([acc], [cnt], [m0..2], [a<p>], [b<p>]) and `extras` -- asm
+    lines of the reduction interleaved into the column (fe_mul_red below) -- placed in the wait-state
+    slots the column's own schedule would pad with s_nop, else after the column's first
+    multiply-add.  Extras never read a mask the column writes, so each one counts as one wait state."""
+    sch = schedule(n, safe)
+    ex = list(extras)
+    # extras beyond the s_nop slots go right after the first multiply-add
+    slots = sum(x[1] + 1 for x in sch if x[0] == "nop")
+    early, ex = ex[:max(0, len(ex) - slots)], ex[max(0, len(ex) - slots):]
+    out = []
+    for ins in sch:
+        if ins[0] == "nop" and ex:
+            k = ins[1] + 1           # wait states this s_nop supplied
+            while k > 0 and ex:
+                out.append(("x", ex.pop(0)))
+                k -= 1
+            if k > 0:
+                out.append(("nop", k - 1))
+            continue
+        out.append(ins)
+        if ins == ("mad", 0):
+            out += [("x", e) for e in early]
+    # re-check the mask rule with extras counted as one wait state each
+    chk = [("nop", 0) if x[0] == "x" else x for x in out]
+    check(chk, n, safe)
+    lines, counted = [], 0
+    for ins in out:
+        if ins[0] == "mad":
+            p = ins[1]
+            src2 = "0" if (first_zero and p == 0) else "%[acc]"
+            lines.append(f"v_mad_u64_u32 %[acc], %[m{p % 3}], %[a{p}], %[b{p}], {src2}")
+        elif ins[0] == "cnt":
+            m = f"%[m{ins[1] % 3}]"
+            prev = "%[cnt]" if counted else "0"
+            lines.append(f"v_addc_co_u32 %[cnt], {m}, 0, {prev}, {m}")
+            counted += 1
+        elif ins[0] == "nop":
+            lines.append(f"s_nop {ins[1]}")
+        else:
+            lines.append(ins[1])
+    return "\\n\\t".join(lines), counted
+
+
+# The reduction (kh_math.h fe_reduce512: V_j = h_j*977 + (l_j, l_j+1), W_i = h_i*977 + (h_i-1, h_i),
+# R = A + B 2^32) interleaved into fe_mul's last columns: each slice's multiply-add goes into the
+# first column statement after its inputs exist, each chain link into the statement after its two
+# slices (a 32-bit half of a 64-bit asm operand cannot be named inside the statement that writes
+# it).  The links' carry lives in an SGPR pair across statements, so the chain pays no per-link pad.
+# (slice name, multiplier t index, addend pair (lo, hi) t indices), in issue order
+SLICES = [("V0", 8, (0, 1)), ("W1", 9, (8, 9)), ("V2", 10, (2, 3)), ("W3", 11, (10, 11)),
+          ("V4", 12, (4, 5)), ("W5", 13, (12, 13)), ("V6", 14, (6, 7)), ("W7", 15, (14, 15))]
+# chain link j: R_j = x + y (+ carry); operands as (slice, half)
+LINKS = {1: (("V0", 1), ("W1", 0)), 2: (("V2", 0), ("W1", 1)), 3: (("V2", 1), ("W3", 0)),
+         4: (("V4", 0), ("W3", 1)), 5: (("V4", 1), ("W5", 0)), 6: (("V6", 0), ("W5", 1)),
+         7: (("V6", 1), ("W7", 0)), 8: (("W7", 1), None)}
+
+
+def gen_mul_red():
+    """fe_mul's columns with the reduction's slices and chain links interleaved (mul_red_cols)."""
+    out = ['// R[0..8] = limbs of A + B 2^32 for t = a * b (fe_reduce512\'s slices and chain, interleaved into',
+           '// the columns); mk[j] = slice j\'s carry-out mask, r9 = the chain\'s carry out of limb 8',
+           '__device__ __forceinline__ void mul_red_cols(const uint32_t *a, const uint32_t *b, uint32_t R[9], uint64_t mk[8],',
+           '                                             uint64_t &r9) {',
+           '  uint64_t acc, m0, m1, m2, c;',
+           '  uint32_t cnt, cnt_unused, t[16];',
+           '  uint64_t V0, W1, V2, W3, V4, W5, V6, W7;',
+           '  const uint32_t K = 977u;']
+    # statement index s: columns 0..14, then F1 (15), F2 (16).  Slice i needs t[mult] and its pair:
+    # available after column max(mult, pair hi) -> goes into the next statement.
+    ready_slice = {name: max(mu, lo, hi) + 1 for name, mu, (lo, hi) in SLICES}
+    # W7 needs t[15] = column 14's high half: statement 15
+    ready_slice["W7"] = 15
+    place_slice = {}
+    for name, _, _ in SLICES:
+        place_slice[name] = ready_slice[name]
+    # links: after both slices' statements, and after the previous link's statement (carry order)
+    place_link = {}
+    prev = -1
+    for j in range(1, 9):
+        x, y = LINKS[j]
+        st = max(place_slice[x[0]], place_slice[y[0]] if y else 0) + 1
+        st = max(st, prev + 1 if j > 1 else st)
+        place_link[j] = st
+        prev = st
+    nstat = max(place_link.values()) + 1
+    sl = {name: (mu, pair) for name, mu, pair in SLICES}
+    for st in range(nstat):
+        extras, outs, ins = [], [], []
+        for name, _, _ in SLICES:
+            if place_slice[name] == st:
+                mu, (lo, hi) = sl[name]
+                j = int(name[1:])
+                extras.append(f"v_mad_u64_u32 %[{name}], %[mk{j}], %[t{mu}], %[K], %[p{name}]")
+                outs.append(f'[{name}] "=&v"({name}), [mk{j}] "=&s"(mk[{j}])')
+                ins.append(f'[t{mu}] "v"(t[{mu}]), [p{name}] "v"(pack64(t[{lo}], t[{hi}]))')
+                if '[K] "s"(K)' not in ins:
+                    ins.append('[K] "s"(K)')
+        for j in range(1, 9):
+            if place_link[j] != st:
+                continue
+            x, y = LINKS[j]
+            xs = f"(uint32_t)({x[0]} >> 32)" if x[1] else f"(uint32_t){x[0]}"
+            if y:
+                ys = f"(uint32_t)({y[0]} >> 32)" if y[1] else f"(uint32_t){y[0]}"
+            if j == 1:
+                extras.append(f"v_add_co_u32 %[R{j}], %[c], %[x{j}], %[y{j}]")
+                outs.append(f'[R{j}] "=&v"(R[{j}]), [c] "=&s"(c)')
+            elif j < 8:
+                extras.append(f"v_addc_co_u32 %[R{j}], %[c], %[x{j}], %[y{j}], %[c]")
+                outs.append(f'[R{j}] "=&v"(R[{j}]), [c] "+s"(c)')
+            else:
+                extras.append(f"v_addc_co_u32 %[R{j}], %[c], %[x{j}], 0, %[c]")
+                outs.append(f'[R{j}] "=&v"(R[{j}]), [c] "+s"(c)')
+            ins.append(f'[x{j}] "v"({xs})' + (f', [y{j}] "v"({ys})' if y else ""))
+        if st < 15:
+            k = st
+            prods = [(f"a[{i}]", f"b[{k - i}]") for i in range(8) if 0 <= k - i <= 7]
+            safe = len(prods) if k == 0 else (1 if k == 1 else 0)
+            # two links in one statement would need a pad between them: never placed so
+            text, counted = col_asm_named(len(prods), safe, k == 0, extras)
+            acc_c = '[acc] "=&v"(acc)' if k == 0 else '[acc] "+v"(acc)'
+            cnt_c = '[cnt] "=&v"(cnt)' if counted else '[cnt] "=&v"(cnt_unused)'
+            o = [acc_c, cnt_c, '[m0] "=&s"(m0)', '[m1] "=&s"(m1)', '[m2] "=&s"(m2)'] + outs
+            pi = [f'[a{p}] "v"({pa}), [b{p}] "v"({pb})' for p, (pa, pb) in enumerate(prods)] + ins
+            out.append(f'  asm("{text}"\n      : {", ".join(o)}\n      : {", ".join(pi)});')
+            out.append(f"  t[{k}] = (uint32_t)acc;")
+            if k < 14:
+                hi = "((uint64_t)cnt << 32)" if counted else "0"
+                out.append(f"  acc = (acc >> 32) | {hi};")
+            else:
+                out.append("  t[15] = (uint32_t)(acc >> 32);")
+        else:
+            # statements after the last column: the remaining slices and links; consecutive links
+            # need two wait states between them
+            lines = []
+            links_here = [e for e in extras if "v_add" in e]
+            mads_here = [e for e in extras if "v_mad" in e]
+            seq = mads_here[:]
+            for i, l in enumerate(links_here):
+                if i > 0:
+                    seq.append("s_nop 1")
+                seq.append(l)
+            text = "\\n\\t".join(seq)
+            out.append(f'  asm("{text}"\n      : {", ".join(outs)}\n      : {", ".join(ins)});')
+    out.append("  R[0] = (uint32_t)V0;")
+    out.append("  r9 = c;")
+    out.append("  (void)cnt_unused;")
+    out.append("}")
+    return out
+
+
 def gen():
     out = ['// kh_cols.h -- GENERATED by tools/gen_cols.py: the product-scanning columns of fe_mul and',
            '// fe_sqr, one asm statement per column, scheduled so that every carry count reads a mask',
@@ -156,6 +308,8 @@ def gen():
     out.append("  t[15] = (uint32_t)(acc >> 32);")
     out.append("  (void)cnt_unused;")
     out.append("}")
+    out.append("")
+    out += gen_mul_red()
     out += ["#endif"]
     return "\n".join(out) + "\n"
 

@@ -152,24 +152,29 @@ def common_path(bl, a, b):
             if m and idx.get(m.group(1), -1) > j:
                 for k in range(j + 1, min(idx[m.group(1)], b + 1)):
                     w[k] = 0.5
-    i = a
-    while i <= b:
-        if bl[i][2]:
-            # the guarding branch: last instruction of the previous block with a forward target
-            j = i - 1
-            while j >= a and not bl[j][1]:
-                j -= 1
-            tgt = None
-            if j >= a:
-                m = re.match(r"s_cbranch_\w+\s+(\.LBB\d+_\d+)", bl[j][1][-1])
-                if m and idx.get(m.group(1), -1) > i:
-                    tgt = idx[m.group(1)]
-            end = tgt if tgt is not None else i + 1
-            for k in range(i, min(end, b + 1)):
-                w[k] = 0.0
-            i = max(end, i + 1)
-            continue
-        i += 1
+    # rare regions: the blocks of [a, b] that the loop reaches only through a marked block.  A walk
+    # of the control-flow graph from the loop's first block that never enters a marked block (the
+    # compiler may lay a rare block out before its join, so layout order alone does not bound it)
+    def succ(k):
+        ins = bl[k][1]
+        out = []
+        last = ins[-1] if ins else ""
+        m = re.match(r"s_(cbranch_\w+|branch)\s+(\.LBB\d+_\d+)", last)
+        if m and m.group(2) in idx:
+            out.append(idx[m.group(2)])
+        if not last.startswith("s_branch") and k + 1 <= b:
+            out.append(k + 1)
+        return out
+    seen, todo = {a}, [a]
+    while todo:
+        k = todo.pop()
+        for s in succ(k):
+            if a <= s <= b and s not in seen and not bl[s][2]:
+                seen.add(s)
+                todo.append(s)
+    for k in range(a, b + 1):
+        if k not in seen:
+            w[k] = 0.0
     return w
 
 
@@ -190,7 +195,8 @@ def mix(listing: str, sym: str, per_point_loop: bool):
         weight[k] = 0.5
     for k in range(lo, hi + 1):
         weight[k] = 1.0 if (per_point_loop and top[0] <= k <= top[1]) else 0.5
-    cp = [common_path(bl, x[0], x[1]) for x in over + [fwd]]
+    # one control-flow walk over the whole backward loop (its nested ranges share the header lo)
+    cp = [common_path(bl, lo, hi), common_path(bl, fwd[0], fwd[1])]
     rare = {k for w in cp for k in range(len(w)) if w[k] == 0.0}
     half = {k for w in cp for k in range(len(w)) if w[k] == 0.5}
     per_point = {}
