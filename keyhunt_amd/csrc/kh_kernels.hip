@@ -562,16 +562,34 @@ __global__ void __launch_bounds__((walk_threads<MODE, H>()), (walk_blocks_per_cu
                                        : (uint64_t)g * A.lane_stride + (uint64_t)(A.group_base + j) * (2 * H) + H;
     // forward: prefix products of dx_i = T[i].x - C.x
     fe acc;
+    if constexpr (DEFER) {
+      // two prefix products per trip: their two differences share one interleaved carry chain
 #pragma unroll 1
-    for (int i = 0; i < H; i++) {
-      fe tx, dx;
-      ld_tx(tx, i);
-      fe_sub(dx, tx, cx);
-      if (i == 0)
-        acc = dx;
-      else
-        fe_mul(acc, acc, dx);
-      if (!SPARSE || (i & 1) == 0) scr_store(scr, slot(i), acc);
+      for (int i = 0; i < H; i += 2) {
+        fe tx0, tx1, dx0, dx1;
+        ld_tx(tx0, i);
+        ld_tx(tx1, i + 1);
+        fe_addsub2<true, true>(dx0, tx0, cx, dx1, tx1, cx);
+        if (i == 0)
+          acc = dx0;
+        else
+          fe_mul(acc, acc, dx0);
+        scr_store(scr, slot(i), acc);
+        fe_mul(acc, acc, dx1);
+        if (!SPARSE) scr_store(scr, slot(i + 1), acc);
+      }
+    } else {
+#pragma unroll 1
+      for (int i = 0; i < H; i++) {
+        fe tx, dx;
+        ld_tx(tx, i);
+        fe_sub(dx, tx, cx);
+        if (i == 0)
+          acc = dx;
+        else
+          fe_mul(acc, acc, dx);
+        if (!SPARSE || (i & 1) == 0) scr_store(scr, slot(i), acc);
+      }
     }
     fe t2x, t2y, dxn;
     ld_tx(t2x, H);

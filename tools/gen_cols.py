@@ -21,11 +21,13 @@ hardware.  The scheduler below asserts both rules for every column it emits.
 usage: python tools/gen_cols.py > keyhunt_amd/csrc/kh_cols.h
 """
 GAP = 2  # independent instructions (or s_nop wait states) between a mask's write and its read
+NM = 4   # SGPR pairs the masks rotate over: up to NM - 1 counts outstanding, so a column's last
+         # counts need no pad (3 pairs left one s_nop at the end of most columns)
 
 
 def schedule(n: int, safe: int):
     """Order of ('mad', p) / ('cnt', p) / ('nop', w) for a column of n products, the first `safe`
-    of them uncounted; masks m[p % 3]."""
+    of them uncounted; masks m[p % NM]."""
     out = []
     pending = []  # counted products whose count is not yet emitted, in order
     pos = {}      # instruction index of each product's multiply-add
@@ -34,20 +36,20 @@ def schedule(n: int, safe: int):
         return sum(x[1] + 1 if x[0] == "nop" else 1 for x in out[pos[q] + 1:])
     for p in range(n):
         # emit ready counts first while keeping at most 2 masks outstanding before a third mad
-        while pending and len(pending) >= 2:
+        while pending and len(pending) >= NM - 1:
             q = pending[0]
             if waited(q) < GAP:
                 break
             out.append(("cnt", q))
             pending.pop(0)
-        if len(pending) >= 3:
+        if len(pending) >= NM:
             raise AssertionError("mask reuse before read")
         pos[p] = len(out)
         out.append(("mad", p))
         if p >= safe:
             pending.append(p)
         # a count becomes due once GAP instructions follow its mad
-        if len(pending) >= 2:
+        if len(pending) >= NM - 1:
             q = pending[0]
             if waited(q) >= GAP:
                 out.append(("cnt", q))
@@ -77,7 +79,7 @@ def check(out, n, safe):
         mi = next(i for i, x in enumerate(out) if x == ("mad", p))
         assert sum(waits[mi + 1:idx]) >= GAP, (n, safe, out)
         for x in out[mi + 1:idx]:
-            assert not (x[0] == "mad" and x[1] % 3 == p % 3), (n, safe, out)
+            assert not (x[0] == "mad" and x[1] % NM == p % NM), (n, safe, out)
     assert sorted(x[1] for x in out if x[0] == "mad") == list(range(n))
     assert sorted(x[1] for x in out if x[0] == "cnt") == list(range(safe, n))
 
@@ -91,9 +93,9 @@ def col_asm(n: int, safe: int, first_zero: bool):
         if ins[0] == "mad":
             p = ins[1]
             src2 = "0" if (first_zero and p == 0) else "%0"
-            lines.append(f"v_mad_u64_u32 %0, %{2 + p % 3}, %{5 + 2 * p}, %{6 + 2 * p}, {src2}")
+            lines.append(f"v_mad_u64_u32 %0, %{2 + p % NM}, %{2 + NM + 2 * p}, %{3 + NM + 2 * p}, {src2}")
         elif ins[0] == "cnt":
-            m = f"%{2 + ins[1] % 3}"
+            m = f"%{2 + ins[1] % NM}"
             prev = "%1" if counted else "0"
             lines.append(f"v_addc_co_u32 %1, {m}, 0, {prev}, {m}")
             counted += 1
@@ -102,17 +104,26 @@ def col_asm(n: int, safe: int, first_zero: bool):
     return "\\n\\t".join(lines), counted
 
 
-def emit_column(name_acc: str, prods: list[tuple[str, str]], safe: int, first_zero: bool, indent="  "):
+def emit_column(name_acc: str, prods: list[tuple[str, str]], safe: int, first_zero: bool, indent="  ",
+                shift_in: bool = False):
+    """shift_in: the previous column counted no carry, so this column's accumulator is the previous
+    one shifted down 32 bits -- one v_lshrrev_b64 at the head of the statement (the C form
+    `acc >> 32` compiles to a move pair through a zero register)."""
     n = len(prods)
     text, counted = col_asm(n, safe, first_zero)
+    if shift_in:  # from a separate input (the previous accumulator keeps its low word, a t limb)
+        text = f"v_lshrrev_b64 %0, 32, %{2 + NM + 2 * n}\\n\\t" + text
     ins = ", ".join(f'"v"({a}), "v"({b})' for a, b in prods)
-    acc_c = f'"=&v"({name_acc})' if first_zero else f'"+v"({name_acc})'
+    if shift_in:
+        ins += f', "v"({name_acc}p)'
+    acc_c = f'"=&v"({name_acc})' if (first_zero or shift_in) else f'"+v"({name_acc})'
     cnt_c = '"=&v"(cnt)' if counted else '"=&v"(cnt_unused)'
-    return (f'{indent}asm("{text}"\n{indent}    : {acc_c}, {cnt_c}, "=&s"(m0), "=&s"(m1), "=&s"(m2)\n'
+    masks = ", ".join(f'"=&s"(m{q})' for q in range(NM))
+    return (f'{indent}asm("{text}"\n{indent}    : {acc_c}, {cnt_c}, {masks}\n'
             f'{indent}    : {ins});\n'), counted
 
 
-def col_asm_named(n: int, safe: int, first_zero: bool, extras: list[str]):
+def col_asm_named(n: int, safe: int, first_zero: bool, extras: list[str], shift_in: bool = False):
     """Column text with named operands ([acc], [cnt], [m0..2], [a<p>], [b<p>]) and `extras` -- asm
     lines of the reduction interleaved into the column (fe_mul_red below) -- placed in the wait-state
     slots the column's own schedule would pad with s_nop, else after the column's first
@@ -143,9 +154,9 @@ def col_asm_named(n: int, safe: int, first_zero: bool, extras: list[str]):
         if ins[0] == "mad":
             p = ins[1]
             src2 = "0" if (first_zero and p == 0) else "%[acc]"
-            lines.append(f"v_mad_u64_u32 %[acc], %[m{p % 3}], %[a{p}], %[b{p}], {src2}")
+            lines.append(f"v_mad_u64_u32 %[acc], %[m{p % NM}], %[a{p}], %[b{p}], {src2}")
         elif ins[0] == "cnt":
-            m = f"%[m{ins[1] % 3}]"
+            m = f"%[m{ins[1] % NM}]"
             prev = "%[cnt]" if counted else "0"
             lines.append(f"v_addc_co_u32 %[cnt], {m}, 0, {prev}, {m}")
             counted += 1
@@ -153,6 +164,8 @@ def col_asm_named(n: int, safe: int, first_zero: bool, extras: list[str]):
             lines.append(f"s_nop {ins[1]}")
         else:
             lines.append(ins[1])
+    if shift_in:  # from a separate input: the previous accumulator keeps its low word (a t limb)
+        lines.insert(0, "v_lshrrev_b64 %[acc], 32, %[accp]")
     return "\\n\\t".join(lines), counted
 
 
@@ -176,7 +189,7 @@ def gen_mul_red():
            '// the columns); mk[j] = slice j\'s carry-out mask, r9 = the chain\'s carry out of limb 8',
            '__device__ __forceinline__ void mul_red_cols(const uint32_t *a, const uint32_t *b, uint32_t R[9], uint64_t mk[8],',
            '                                             uint64_t &r9) {',
-           '  uint64_t acc, m0, m1, m2, c;',
+           '  uint64_t acc, accp, m0, m1, m2, m3, c;',
            '  uint32_t cnt, cnt_unused, t[16];',
            '  uint64_t V0, W1, V2, W3, V4, W5, V6, W7;',
            '  const uint32_t K = 977u;']
@@ -199,6 +212,7 @@ def gen_mul_red():
         prev = st
     nstat = max(place_link.values()) + 1
     sl = {name: (mu, pair) for name, mu, pair in SLICES}
+    shift = False
     for st in range(nstat):
         extras, outs, ins = [], [], []
         for name, _, _ in SLICES:
@@ -232,17 +246,22 @@ def gen_mul_red():
             prods = [(f"a[{i}]", f"b[{k - i}]") for i in range(8) if 0 <= k - i <= 7]
             safe = len(prods) if k == 0 else (1 if k == 1 else 0)
             # two links in one statement would need a pad between them: never placed so
-            text, counted = col_asm_named(len(prods), safe, k == 0, extras)
-            acc_c = '[acc] "=&v"(acc)' if k == 0 else '[acc] "+v"(acc)'
+            text, counted = col_asm_named(len(prods), safe, k == 0, extras, shift_in=shift)
+            acc_c = '[acc] "=&v"(acc)' if (k == 0 or shift) else '[acc] "+v"(acc)'
             cnt_c = '[cnt] "=&v"(cnt)' if counted else '[cnt] "=&v"(cnt_unused)'
-            o = [acc_c, cnt_c, '[m0] "=&s"(m0)', '[m1] "=&s"(m1)', '[m2] "=&s"(m2)'] + outs
+            o = [acc_c, cnt_c] + [f'[m{q}] "=&s"(m{q})' for q in range(NM)] + outs
             pi = [f'[a{p}] "v"({pa}), [b{p}] "v"({pb})' for p, (pa, pb) in enumerate(prods)] + ins
+            if shift:
+                out.append("  accp = acc;")
+                pi.append('[accp] "v"(accp)')
             out.append(f'  asm("{text}"\n      : {", ".join(o)}\n      : {", ".join(pi)});')
             out.append(f"  t[{k}] = (uint32_t)acc;")
+            shift = not counted
             if k < 14:
-                hi = "((uint64_t)cnt << 32)" if counted else "0"
-                out.append(f"  acc = (acc >> 32) | {hi};")
+                if counted:
+                    out.append("  acc = (acc >> 32) | ((uint64_t)cnt << 32);")
             else:
+                assert counted
                 out.append("  t[15] = (uint32_t)(acc >> 32);")
         else:
             # statements after the last column: the remaining slices and links; consecutive links
@@ -273,17 +292,21 @@ def gen():
     # fe_mul: t = a * b (16 limbs)
     out.append('// t[0..15] = a * b')
     out.append('__device__ __forceinline__ void mul_cols(const uint32_t *a, const uint32_t *b, uint32_t t[16]) {')
-    out.append('  uint64_t acc, m0, m1, m2;')
+    out.append('  uint64_t acc, accp, m0, m1, m2, m3;')
     out.append('  uint32_t cnt, cnt_unused;')
+    shift = False
     for k in range(15):
         prods = [(f"a[{i}]", f"b[{k - i}]") for i in range(8) if 0 <= k - i <= 7]
         # column 0 and the first product of column 1 cannot carry: (2^32-1)^2 + 2^32 - 1 < 2^64
         safe = len(prods) if k == 0 else (1 if k == 1 else 0)
-        s, counted = emit_column("acc", prods, safe, k == 0)
+        if shift:
+            out.append("  accp = acc;")
+        s, counted = emit_column("acc", prods, safe, k == 0, shift_in=shift)
         out.append(s.rstrip("\n"))
         out.append(f"  t[{k}] = (uint32_t)acc;")
-        hi = "((uint64_t)cnt << 32)" if counted else "0"
-        out.append(f"  acc = (acc >> 32) | {hi};")
+        shift = not counted
+        if counted:
+            out.append("  acc = (acc >> 32) | ((uint64_t)cnt << 32);")
     out.append("  t[15] = (uint32_t)acc;")
     out.append("  (void)cnt_unused;")
     out.append("}")
@@ -291,19 +314,24 @@ def gen():
     # fe_sqr cross products a_i * a_j, i < j: columns 1..13 (t[0] = 0, t[14..15] from the last acc)
     out.append('// t[1..15] = sum_{i<j} a_i a_j 2^(32(i+j)) (t[0] = 0): the cross products of a square, not doubled')
     out.append('__device__ __forceinline__ void sqr_cross_cols(const uint32_t *a, uint32_t t[16]) {')
-    out.append('  uint64_t acc, m0, m1, m2;')
+    out.append('  uint64_t acc, accp, m0, m1, m2, m3;')
     out.append('  uint32_t cnt, cnt_unused;')
     out.append('  t[0] = 0;')
+    shift = False
     for k in range(1, 14):
         prods = [(f"a[{i}]", f"a[{k - i}]") for i in range(8) if i < k - i <= 7]
         # columns 1 and 2 hold one cross product each and column 3 starts on an accumulator of at
         # most 2^32 - 1: their first products cannot carry
         safe = 1 if k <= 3 else 0
-        s, counted = emit_column("acc", prods, safe, k == 1)
+        if shift:
+            out.append("  accp = acc;")
+        s, counted = emit_column("acc", prods, safe, k == 1, shift_in=shift)
         out.append(s.rstrip("\n"))
         out.append(f"  t[{k}] = (uint32_t)acc;")
-        hi = "((uint64_t)cnt << 32)" if counted else "0"
-        out.append(f"  acc = (acc >> 32) | {hi};")
+        shift = not counted
+        if counted:
+            out.append("  acc = (acc >> 32) | ((uint64_t)cnt << 32);")
+    assert not shift
     out.append("  t[14] = (uint32_t)acc;")
     out.append("  t[15] = (uint32_t)(acc >> 32);")
     out.append("  (void)cnt_unused;")

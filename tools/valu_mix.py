@@ -32,10 +32,11 @@ import json
 import re
 import sys
 
-# kernel -> (symbol, its largest loop runs once per point: the hash walks' side loop)
-KERNELS = {"k_walk<7, 2048>": ("_Z6k_walkILi7ELi2048EEv9walk_args", False),
-           "k_walk<10, 2048>": ("_Z6k_walkILi10ELi2048EEv9walk_args", False),
-           "k_walk<11, 2048>": ("_Z6k_walkILi11ELi2048EEv9walk_args", True)}
+# kernel -> (symbol, its largest loop runs once per point: the hash walks' side loop, prefix
+# products per forward-loop trip: the deferred-probe walks pair two per trip, kh_kernels.hip)
+KERNELS = {"k_walk<7, 2048>": ("_Z6k_walkILi7ELi2048EEv9walk_args", False, 2),
+           "k_walk<10, 2048>": ("_Z6k_walkILi10ELi2048EEv9walk_args", False, 2),
+           "k_walk<11, 2048>": ("_Z6k_walkILi11ELi2048EEv9walk_args", True, 1)}
 
 # ubench_cost.txt pattern name -> class
 PATTERN = {"mad_u64_u32 acc, 4 chains": "mad64", "add_co/addc, 4 sgpr chains": "carry", "v_mov_b32": "mov",
@@ -178,7 +179,7 @@ def common_path(bl, a, b):
     return w
 
 
-def mix(listing: str, sym: str, per_point_loop: bool):
+def mix(listing: str, sym: str, per_point_loop: bool, fwd_per_trip: int = 1):
     """Lane-instructions per point by class.  The largest loop of the kernel is its per-pair
     backward loop (deferred-probe walks) or, with per_point_loop, the per-point side loop of the
     hash walks inside it; loops overlapping it are the rest of the backward loop (per pair), and the
@@ -192,7 +193,7 @@ def mix(listing: str, sym: str, per_point_loop: bool):
     fwd = next(x for x in ls if x[1] < lo)
     weight = {}
     for k in range(fwd[0], fwd[1] + 1):
-        weight[k] = 0.5
+        weight[k] = 0.5 / fwd_per_trip  # a trip makes fwd_per_trip prefix products (2 points each)
     for k in range(lo, hi + 1):
         weight[k] = 1.0 if (per_point_loop and top[0] <= k <= top[1]) else 0.5
     # one control-flow walk over the whole backward loop (its nested ranges share the header lo)
@@ -223,8 +224,8 @@ def main():
     cost = costs(cost_path)
     pm = json.load(open(pmc))
     res = {}
-    for name, (sym, ppl) in KERNELS.items():
-        pp = mix(listing, sym, ppl)
+    for name, (sym, ppl, fpt) in KERNELS.items():
+        pp = mix(listing, sym, ppl, fpt)
         # pp: lane-instructions per point (every lane walks its own points); a wave-instruction
         # serves 64 points, so SIMD cycles per point = sum(count x class cost) / 64
         valu = sum(v for k, v in pp.items() if k != "s_nop")
