@@ -345,6 +345,12 @@ def quarters(t0: float, recs: list, units_per_step: int, keys_per_unit: float, c
     return out
 
 
+def progress(msg: str) -> None:
+    """One line on stderr (rank 0) so a long leg shows it is alive."""
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def bsgs_leg(D: Dist, eng, args, clock):
     import keyhunt_amd as K
     C = BSGS_CONFIGS[args.config]
@@ -353,6 +359,7 @@ def bsgs_leg(D: Dist, eng, args, clock):
     eng.bsgs_build()
     eng.synchronize()
     build_s = time.perf_counter() - t
+    progress(f"BSGS tables built in {build_s:.2f} s (k = {C['k']})")
     q = decompress(C["pub"])
     eng.bsgs_set_targets([q])
     two_n = 2 * info.n
@@ -373,7 +380,9 @@ def bsgs_leg(D: Dist, eng, args, clock):
         run(B0)
         last = time.perf_counter() - t
     B = int(D.max(batch_for(args.seconds, args.steps, last / B0, B0, B0) if args.warmup else B0))
+    progress(f"BSGS warm-up done; timing {args.steps} steps of {B} bases")
     T, t0, _, recs = timed(D, eng, args.steps, lambda s: run(B), B, K.engine.TIME_BSGS, clock)
+    progress(f"BSGS timed region {T:.1f} s; known-answer window next")
     la, ms, pts = eng.kernel_time(K.engine.TIME_BSGS)
     my_pts_s = args.steps * B * info.cycles * 1024 / (recs[-1][0] - t0)
     # known answer (outside the timed region, same engine and tables): SURVEY.md 8c
@@ -578,15 +587,21 @@ def run_reference(argv: list[str], files: list[str], seconds: float, setup=None)
         for f in files:
             shutil.copy(os.path.join(REPO, "tests", "golden", "data", f), td)
         if setup:
+            progress("CPU baseline: writing the tables for the reference")
             setup(td)
+        progress(f"CPU baseline: oracle/_ref/{os.path.basename(REF_BIN)} {' '.join(argv)}")
         cmd = [REF_BIN] + argv + ["-t", str(thr), "-s", "5", "-q"]
         p = subprocess.Popen(cmd, cwd=td, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL)
         out = b""
         t0 = time.time()
         os.set_blocking(p.stdout.fileno(), False)
         last = None
+        tick = t0
         while time.time() - t0 < seconds + 120:
             time.sleep(0.5)
+            if time.time() - tick >= 60:
+                tick = time.time()
+                progress(f"CPU baseline running ({tick - t0:.0f} s)")
             try:
                 chunk = p.stdout.read()
             except Exception:
