@@ -172,6 +172,55 @@ def rank_origin(rank: int, span: int) -> int:
     return rank * span
 
 
+def walk_origin(origin: int, walk: int, walks: int, span: int, unit_keys: int) -> int:
+    """First key of walk `walk`'s part of a rank region that starts at key `origin` and holds `span`
+    units of `unit_keys` keys: the region is cut into `walks` contiguous parts, one per context, so each
+    context's consecutive calls continue its own lanes and no two contexts cover the same key."""
+    return origin + walk * (span // walks) * unit_keys
+
+
+class Walks:
+    """`walks` contexts on one device (kh_open each: own HIP stream, own tables, inversion pads and
+    lane states), each driven by its own host thread, so up to `walks` walk launches are in flight on
+    the chip at once.  One launch's tail and the phases in which all its waves wait on the same thing
+    (pad stores, the batch inversion, the probes) leave issue slots idle that the other context's
+    waves fill (profiles/r03t_rehearse2_one_gpu.json).  ctypes drops the GIL
+    for the duration of every kh_* call, so the threads' calls overlap."""
+
+    def __init__(self, K, device: int, walks: int):
+        from concurrent.futures import ThreadPoolExecutor
+        self.engs = [K.Engine(device) for _ in range(walks)]
+        self.pool = ThreadPoolExecutor(walks) if walks > 1 else None
+
+    def __len__(self):
+        return len(self.engs)
+
+    def each(self, fn) -> list:
+        """fn(i, engine) on every context, concurrently; results in context order."""
+        if self.pool is None:
+            return [fn(0, self.engs[0])]
+        return [f.result() for f in [self.pool.submit(fn, i, e) for i, e in enumerate(self.engs)]]
+
+    def synchronize(self) -> None:
+        for e in self.engs:
+            e.synchronize()
+
+    def kernel_time_reset(self) -> None:
+        for e in self.engs:
+            e.kernel_time_reset()
+
+    def kernel_time(self, kind: int) -> tuple[int, float, int]:
+        """Launches, event ms and points summed over the contexts."""
+        t = [e.kernel_time(kind) for e in self.engs]
+        return sum(x[0] for x in t), sum(x[1] for x in t), sum(x[2] for x in t)
+
+    def close(self) -> None:
+        for e in self.engs:
+            e.close()
+        if self.pool:
+            self.pool.shutdown()
+
+
 def batch_for(seconds: float, steps: int, unit_s: float, quantum: int, floor: int) -> int:
     """Units per step so that `steps` steps of unit_s seconds per unit last about `seconds`: a
     multiple of `quantum`, at least `floor`."""
@@ -351,28 +400,31 @@ def progress(msg: str) -> None:
         print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
-def bsgs_leg(D: Dist, eng, args, clock):
+def bsgs_leg(D: Dist, W: Walks, args, clock):
     import keyhunt_amd as K
     C = BSGS_CONFIGS[args.config]
-    info = eng.bsgs_setup(1 << 44, C["k"], layer1=args.layer1)
+    S = len(W)
+    info = W.each(lambda i, e: e.bsgs_setup(1 << 44, C["k"], layer1=args.layer1))[0]
     t = time.perf_counter()
-    eng.bsgs_build()
-    eng.synchronize()
+    W.each(lambda i, e: (e.bsgs_build(), e.synchronize()))
     build_s = time.perf_counter() - t
-    progress(f"BSGS tables built in {build_s:.2f} s (k = {C['k']})")
+    progress(f"BSGS tables built in {build_s:.2f} s (k = {C['k']}, {S} context(s))")
     q = decompress(C["pub"])
-    eng.bsgs_set_targets([q])
+    W.each(lambda i, e: e.bsgs_set_targets([q]))
     two_n = 2 * info.n
     origin = (1 << (C["bits"] - 1)) + rank_origin(D.rank, RANK_SPAN_BASES) * two_n
     B0 = args.bases or C["bases"]
+    assert B0 % S == 0, "--bases must be a multiple of --walks"
     walked = 0
 
     def run(nb):
+        # nb bases per step in all, nb / S per context, each in its own part of the rank's region
         nonlocal walked
-        assert walked + nb <= RANK_SPAN_BASES, "rank region exhausted"
-        found = eng.bsgs_scan(origin + walked * two_n, nb)
-        walked += nb
-        assert not found  # puzzle 125's (130's) key lies far from the start of the range
+        per = nb // S
+        assert walked + per <= RANK_SPAN_BASES // S, "rank region exhausted"
+        found = W.each(lambda i, e: e.bsgs_scan(walk_origin(origin, i, S, RANK_SPAN_BASES, two_n) + walked * two_n, per))
+        walked += per
+        assert not any(found)  # puzzle 125's (130's) key lies far from the start of the range
 
     last = 0.0
     for s in range(args.warmup):
@@ -381,19 +433,19 @@ def bsgs_leg(D: Dist, eng, args, clock):
         last = time.perf_counter() - t
     B = int(D.max(batch_for(args.seconds, args.steps, last / B0, B0, B0) if args.warmup else B0))
     progress(f"BSGS warm-up done; timing {args.steps} steps of {B} bases")
-    T, t0, _, recs = timed(D, eng, args.steps, lambda s: run(B), B, K.engine.TIME_BSGS, clock)
+    T, t0, t1, recs = timed(D, W, args.steps, lambda s: run(B), B, K.engine.TIME_BSGS, clock)
     progress(f"BSGS timed region {T:.1f} s; known-answer window next")
-    la, ms, pts = eng.kernel_time(K.engine.TIME_BSGS)
+    la, ms, pts = W.kernel_time(K.engine.TIME_BSGS)
     my_pts_s = args.steps * B * info.cycles * 1024 / (recs[-1][0] - t0)
     # known answer (outside the timed region, same engine and tables): SURVEY.md 8c
     ka_lo, ka_hi, ka_key = C["ka"]
-    ka_found = eng.bsgs_scan(ka_lo, (ka_hi - ka_lo) // two_n)
+    ka_found = W.engs[0].bsgs_scan(ka_lo, (ka_hi - ka_lo) // two_n)
     keys = D.world * args.steps * B * two_n
     pts_launch = pts / la
-    ms_launch = ms / la
+    ms_launch = chip_ms_per_launch(S, ms, la, t1 - t0)
     bpp = ALGO_BYTES_PER_GIANT_POINT[info.layer1_layout]
     kname = WALK_KERNEL[info.layer1_layout]
-    roof = walk_roofline(kname, pts_launch, ms_launch, bpp, la)
+    roof = walk_roofline(kname, pts_launch, ms_launch, bpp, la, walks=S, event_ms=ms / la)
     # the probe is one random 16-B load per giant point: its own ceiling is the chip's random-load
     # rate at this footprint (tools/ubench_random2.hip, profiles/r01l_random16B.txt: 24 GB, nt loads)
     rand = {"achieved": pts_launch / (ms_launch / 1e3) / 1e9, "ceiling": RANDOM16_CEILING_GPS, "unit": "G loads/s",
@@ -408,7 +460,7 @@ def bsgs_leg(D: Dist, eng, args, clock):
         "giant_points_per_s": D.world * args.steps * B * info.cycles * 1024 / T,
         "rank_giant_points_per_s": my_pts_s,
         "build_seconds": build_s,
-        "candidates": eng.bsgs_candidates(),
+        "candidates": sum(e.bsgs_candidates() for e in W.engs),
         "info": info,
         "roofline": roof,
         "sustained": quarters(t0, recs, B, two_n, clock),
@@ -427,15 +479,27 @@ def _valu_mix(kname: str) -> dict:
     return {}
 
 
-def walk_roofline(kname: str, pts_launch: float, ms_launch: float, algo_bytes_per_point: float, launches: int) -> dict:
+def chip_ms_per_launch(walks: int, event_ms: float, launches: int, wall_s: float) -> float:
+    """The chip's time per launch of a leg's walk kernel.  One context: the mean of the HIP events
+    around its launches (what rocprofv3 reports per dispatch).  Several contexts in flight: their
+    launches overlap, so an event spans its own launch and part of the others'; the chip's time per
+    launch is then the timed region's wall time / all contexts' launches (host gaps included)."""
+    return event_ms / launches if walks == 1 else wall_s * 1e3 / launches
+
+
+def walk_roofline(kname: str, pts_launch: float, ms_launch: float, algo_bytes_per_point: float, launches: int,
+                  walks: int = 1, event_ms: float | None = None) -> dict:
     """The roofline object of one walk kernel (see the module docstring): VALU issue bound, with the
     HBM side alongside.  Counter-derived figures come from the newest profiles/r*_pmc_summary.json
-    holding this kernel and are scaled to this run's points per launch."""
+    holding this kernel and are scaled to this run's points per launch.  ms_launch is the chip's time
+    per launch (chip_ms_per_launch); with walks > 1 the overlapping launches' own event mean is
+    reported beside it (event_mean_launch_ms, which a rocprofv3 trace of the same run agrees with)."""
     d = pmc_entry(kname)
     secs = ms_launch / 1e3
     roof = {"bound": "valu", "achieved": None, "peak": VALU_PEAK_GIPS, "unit": "G VALU wave-instr/s", "frac": None,
             "peak_hw": VALU_PEAK_HW_GIPS, "frac_hw": None, "frac_mix": None,
             "traffic": None, "kernel": kname, "launches": launches, "mean_launch_ms": ms_launch,
+            "walks_in_flight": walks, "event_mean_launch_ms": event_ms if event_ms is not None else ms_launch,
             "points_per_launch": pts_launch, "source": d.get("source")}
     if "valu_wave_instructions_per_dispatch" in d:
         wipp = d["valu_wave_instructions_per_dispatch"] / d["points_per_dispatch"]
@@ -485,53 +549,61 @@ def pmc_entry(kernel: str) -> dict:
     return {}
 
 
-def address_leg(D: Dist, eng, args, clock, mode: int, kname: str, keys_per_point: int, base0: int, ka):
-    """-m rmd160 -l compress / -m xpoint: steps of C chunks of 2^32 keys from the rank's region."""
+def address_leg(D: Dist, W: Walks, args, clock, mode: int, kname: str, keys_per_point: int, base0: int, ka):
+    """-m rmd160 -l compress / -m xpoint: steps of C chunks of 2^32 keys from the rank's region (C / S
+    per context, each in its own part of the region)."""
     import keyhunt_amd as K
     kind = K.engine.TIME_ADDRESS if mode == K.KH_MODE_ADDRESS else K.engine.TIME_XPOINT
+    S = len(W)
     origin = base0 + rank_origin(D.rank, RANK_SPAN_CHUNKS) * CHUNK
     walked = 0
 
     def run(nc):
         nonlocal walked
-        assert walked + nc <= RANK_SPAN_CHUNKS, "rank region exhausted"
-        for c in range(nc):
-            hits = eng.scan(origin + (walked + c) * CHUNK, CHUNK, mode, K.KH_SEARCH_COMPRESS)
-            assert not hits  # the puzzle keys lie far from the start of the range
-        walked += nc
+        per = nc // S
+        assert walked + per <= RANK_SPAN_CHUNKS // S, "rank region exhausted"
+
+        def chunks(i, e):
+            o = walk_origin(origin, i, S, RANK_SPAN_CHUNKS, CHUNK)
+            for c in range(per):
+                hits = e.scan(o + (walked + c) * CHUNK, CHUNK, mode, K.KH_SEARCH_COMPRESS)
+                assert not hits  # the puzzle keys lie far from the start of the range
+        W.each(chunks)
+        walked += per
 
     last = 0.0
     for s in range(args.warmup_rmd):
         t = time.perf_counter()
-        run(1)
+        run(S)
         last = time.perf_counter() - t
-    C = int(D.max(batch_for(args.seconds_secondary, args.steps_rmd, last, 1, 1) if args.warmup_rmd else 1))
-    T, t0, _, recs = timed(D, eng, args.steps_rmd, lambda s: run(C), C, kind, clock)
-    la, ms, pts = eng.kernel_time(kind)
+    C = int(D.max(batch_for(args.seconds_secondary, args.steps_rmd, last / S, S, S) if args.warmup_rmd else S))
+    T, t0, t1, recs = timed(D, W, args.steps_rmd, lambda s: run(C), C, kind, clock)
+    la, ms, pts = W.kernel_time(kind)
     ka_lo, ka_n, ka_key = ka
-    ka_hits = eng.scan(ka_lo, ka_n, mode, K.KH_SEARCH_COMPRESS)
+    ka_hits = W.engs[0].scan(ka_lo, ka_n, mode, K.KH_SEARCH_COMPRESS)
     keys = D.world * args.steps_rmd * C * CHUNK * keys_per_point
+    ms_launch = chip_ms_per_launch(S, ms, la, t1 - t0)
     return {"value": keys / T / 1e6, "ms_per_step": T / args.steps_rmd * 1e3, "seconds_timed": T,
             "chunks_per_step": C, "steps": args.steps_rmd,
-            "points_per_s_in_kernel": pts / (ms / 1e3),
-            "roofline": walk_roofline(kname, pts / la, ms / la, 0, la),
+            "points_per_s_in_kernel": pts / (ms_launch * la / 1e3),
+            "roofline": walk_roofline(kname, pts / la, ms_launch, 0, la, walks=S, event_ms=ms / la),
             "sustained": quarters(t0, recs, C, CHUNK * keys_per_point, clock),
             "known_answer": {"window": f"{ka_lo:x}:{ka_lo + ka_n - 1:x}", "expected": f"{ka_key:x}",
                              "found": [f"{h.key:x}" for h in ka_hits], "match": [h.key for h in ka_hits] == [ka_key]}}
 
 
-def rmd160_leg(D: Dist, eng, args, clock):
+def rmd160_leg(D: Dist, W: Walks, args, clock):
     import keyhunt_amd as K
-    eng.set_targets([bytes.fromhex(PUZZLE66_RMD)], bloom_items=1)
+    W.each(lambda i, e: e.set_targets([bytes.fromhex(PUZZLE66_RMD)], bloom_items=1))
     # algorithmic HBM bytes ~0 per key: the 16-B target filter block is L2-resident
-    return address_leg(D, eng, args, clock, K.KH_MODE_ADDRESS, "k_walk<11, 2048>", 2, 1 << 65, KA_RMD160)
+    return address_leg(D, W, args, clock, K.KH_MODE_ADDRESS, "k_walk<11, 2048>", 2, 1 << 65, KA_RMD160)
 
 
-def xpoint_leg(D: Dist, eng, args, clock):
+def xpoint_leg(D: Dist, W: Walks, args, clock):
     """-m xpoint -f tests/63.pub -b 63 (BASELINE configs[2]): X[0..20) probes, one key per point."""
     import keyhunt_amd as K
-    eng.set_targets([PUZZLE63_X.to_bytes(32, "big")[:20]], bloom_items=1)
-    return address_leg(D, eng, args, clock, K.KH_MODE_XPOINT, "k_walk<10, 2048>", 1, 1 << 62, KA_XPOINT)
+    W.each(lambda i, e: e.set_targets([PUZZLE63_X.to_bytes(32, "big")[:20]], bloom_items=1))
+    return address_leg(D, W, args, clock, K.KH_MODE_XPOINT, "k_walk<10, 2048>", 1, 1 << 62, KA_XPOINT)
 
 
 def cpu_host() -> dict:
@@ -687,6 +759,8 @@ def main():
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--rehearse", action="store_true",
                     help="allow more ranks than visible GPUs (ranks share devices; the line reports it)")
+    ap.add_argument("--walks", type=int, default=1, choices=(1, 2, 4),
+                    help="contexts per GPU, each on its own stream and host thread (walk launches in flight)")
     ap.add_argument("--layer1", type=int, default=1, help="BSGS layer-1 layout: 1 blocked (default), 0 reference")
     args = ap.parse_args()
     args.steps_rmd = args.steps if args.steps_rmd is None else args.steps_rmd
@@ -697,20 +771,20 @@ def main():
     if args.gpus != D.world:
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={D.world}: launch one rank per GPU")
     dev = device_plan(D.world, D.local, D.local_world, K.device_count(), args.rehearse)
-    eng = K.Engine(dev)
+    W = Walks(K, dev, args.walks)
     bdf = pci_bus_id(dev)
     clock = ClockSampler(bdf).start()
-    prim = bsgs_leg(D, eng, args, clock)
-    sec = None if args.no_secondary else rmd160_leg(D, eng, args, clock)
-    ter = None if args.no_secondary else xpoint_leg(D, eng, args, clock)
+    prim = bsgs_leg(D, W, args, clock)
+    sec = None if args.no_secondary else rmd160_leg(D, W, args, clock)
+    ter = None if args.no_secondary else xpoint_leg(D, W, args, clock)
     clock.stop()
     cpu_b = cpu_r = cpu_x = None
     if D.rank == 0 and D.world == 1 and not args.no_cpu_baseline:
-        cpu_b = cpu_baseline_bsgs(eng, BSGS_CONFIGS[args.config], args.cpu_seconds)
+        cpu_b = cpu_baseline_bsgs(W.engs[0], BSGS_CONFIGS[args.config], args.cpu_seconds)
         if not args.no_secondary:
             cpu_r = cpu_baseline_rmd160(args.cpu_seconds)
             cpu_x = cpu_baseline_xpoint(args.cpu_seconds)
-    eng.close()
+    W.close()
     ranks = D.gather({"rank": D.rank, "host": os.uname().nodename, "device": dev, "pci_bus_id": bdf,
                       "giant_points_per_s": prim["rank_giant_points_per_s"]})
     kas = [prim["known_answer"]] + [x["known_answer"] for x in (sec, ter) if x]
@@ -728,6 +802,7 @@ def main():
                        "layer1_layout": "blocked" if info.layer1_layout == 1 else "reference",
                        "bases_per_step": prim["bases_per_step"],
                        "giant_points_per_step": prim["bases_per_step"] * info.cycles * 1024,
+                       "walks_in_flight_per_gpu": args.walks,
                        "parallelism": f"keyspace split x{D.world} (no collective)"},
             "devices_used": len(devices),
             "rehearsal": len(devices) < D.world,

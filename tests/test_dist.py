@@ -71,6 +71,28 @@ def test_rank_regions_disjoint_and_inside_the_range(world):
         assert lo + regions[-1][1] * unit_keys <= key < 2 * lo
 
 
+@pytest.mark.parametrize("walks", [1, 2, 4])
+def test_walk_parts_tile_the_rank_region(walks):
+    """bench.py --walks S cuts each rank region into S contiguous parts, one per context: the parts
+    are disjoint, lie inside the rank's region and, walked as far as the part allows, end at the next
+    part's start."""
+    import bench
+    for span, unit_keys in ((bench.RANK_SPAN_BASES, 2 << 44), (bench.RANK_SPAN_CHUNKS, 1 << 32)):
+        for rank in range(8):
+            origin = (1 << 124) + bench.rank_origin(rank, span) * unit_keys
+            starts = [bench.walk_origin(origin, i, walks, span, unit_keys) for i in range(walks)]
+            ends = [s + (span // walks) * unit_keys for s in starts]
+            assert starts[0] == origin and ends[-1] == origin + span * unit_keys
+            assert all(e == s for e, s in zip(ends, starts[1:]))
+
+
+def test_chip_ms_per_launch():
+    """One context: the launches' own event mean; several in flight: wall time over all launches."""
+    import bench
+    assert bench.chip_ms_per_launch(1, 280.0, 10, 9.9) == 28.0
+    assert bench.chip_ms_per_launch(2, 520.0, 20, 5.0) == 250.0  # 5 s / 20 launches
+
+
 @pytest.mark.parametrize("seconds,steps,unit_s,quantum,expect", [
     (60, 10, 56.5e-3 / 65536, 65536, 65536 * 107),   # BSGS: 10 steps of ~6 s
     (60, 20, 56.5e-3 / 65536, 65536, 65536 * 54),    # the driver's --steps 20
