@@ -195,6 +195,12 @@ class Walks:
     def __len__(self):
         return len(self.engs)
 
+    def head(self, n: int) -> "Walks":
+        """The first n contexts as a set of their own (same threads), for a leg that walks fewer."""
+        v = Walks.__new__(Walks)
+        v.engs, v.pool = self.engs[:n], self.pool if n > 1 else None
+        return v
+
     def each(self, fn) -> list:
         """fn(i, engine) on every context, concurrently; results in context order."""
         if self.pool is None:
@@ -219,6 +225,14 @@ class Walks:
             e.close()
         if self.pool:
             self.pool.shutdown()
+
+
+# walk launches in flight per GPU, per leg (bench.py --walks / --walks-secondary; same-box A/B of 25 s /
+# 8 s windows, profiles/r03u_walks_ab.json): the BSGS walk lost 3 % with two contexts (one launch of
+# 2^18 lanes already holds every SIMD at its 4-wave VGPR limit), the hash walks gained (rmd160 +4.5 %,
+# xpoint +17 %: their launches' inversion and pad phases leave issue slots the other context fills)
+WALKS_BSGS = 1
+WALKS_ADDRESS = 2
 
 
 def batch_for(seconds: float, steps: int, unit_s: float, quantum: int, floor: int) -> int:
@@ -759,8 +773,10 @@ def main():
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--rehearse", action="store_true",
                     help="allow more ranks than visible GPUs (ranks share devices; the line reports it)")
-    ap.add_argument("--walks", type=int, default=1, choices=(1, 2, 4),
-                    help="contexts per GPU, each on its own stream and host thread (walk launches in flight)")
+    ap.add_argument("--walks", type=int, default=WALKS_BSGS, choices=(1, 2, 4),
+                    help="BSGS leg: contexts per GPU, each on its own stream and host thread (walk launches in flight)")
+    ap.add_argument("--walks-secondary", type=int, default=WALKS_ADDRESS, choices=(1, 2, 4),
+                    help="the same for the rmd160 and xpoint legs")
     ap.add_argument("--layer1", type=int, default=1, help="BSGS layer-1 layout: 1 blocked (default), 0 reference")
     args = ap.parse_args()
     args.steps_rmd = args.steps if args.steps_rmd is None else args.steps_rmd
@@ -771,12 +787,13 @@ def main():
     if args.gpus != D.world:
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={D.world}: launch one rank per GPU")
     dev = device_plan(D.world, D.local, D.local_world, K.device_count(), args.rehearse)
-    W = Walks(K, dev, args.walks)
+    W = Walks(K, dev, max(args.walks, 1 if args.no_secondary else args.walks_secondary))
     bdf = pci_bus_id(dev)
     clock = ClockSampler(bdf).start()
-    prim = bsgs_leg(D, W, args, clock)
-    sec = None if args.no_secondary else rmd160_leg(D, W, args, clock)
-    ter = None if args.no_secondary else xpoint_leg(D, W, args, clock)
+    prim = bsgs_leg(D, W.head(args.walks), args, clock)
+    Wa = W.head(args.walks_secondary)
+    sec = None if args.no_secondary else rmd160_leg(D, Wa, args, clock)
+    ter = None if args.no_secondary else xpoint_leg(D, Wa, args, clock)
     clock.stop()
     cpu_b = cpu_r = cpu_x = None
     if D.rank == 0 and D.world == 1 and not args.no_cpu_baseline:
@@ -823,7 +840,7 @@ def main():
         for key, leg, wl in (("secondary", sec, "-m rmd160 -f tests/66.rmd -b 66 -l compress"),
                              ("tertiary", ter, "-m xpoint -f tests/63.pub -b 63")):
             if leg:
-                line[key] = {"workload": wl, "value": leg["value"], "unit": "Mkeys/s", "ms_per_step": leg["ms_per_step"],
+                line[key] = {"workload": wl, "value": leg["value"], "walks_in_flight_per_gpu": args.walks_secondary, "unit": "Mkeys/s", "ms_per_step": leg["ms_per_step"],
                              "steps": leg["steps"], "chunks_per_step": leg["chunks_per_step"],
                              "seconds_timed": leg["seconds_timed"],
                              "points_per_s_in_kernel": leg["points_per_s_in_kernel"],
