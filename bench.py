@@ -31,6 +31,13 @@ used and every rank's own rate.  The table build is replicated per GPU and not t
 reported.  torch.distributed (gloo, CPU tensors) provides the barrier and the max over ranks; the
 engine owns the GPU through its own HIP stream, synchronised on both sides of the timed region.
 
+Walks in flight (--walks, --walks-secondary; Walks): each leg may drive S contexts on its GPU, each
+with its own stream and host thread, walking its own contiguous part of the rank region
+(walk_origin).  Defaults from a same-box A/B: S = 1 for BSGS, 2 for rmd160 / xpoint.  With S > 1 the
+launches overlap, so the roofline prices the chip's time per launch (timed wall / all launches,
+chip_ms_per_launch) and reports the launches' own event mean beside it (event_mean_launch_ms, which
+a rocprofv3 kernel trace of the run agrees with).
+
 roofline: dominant kernel of each leg (the giant-step walk k_walk<7, 2048>; k_walk<11, 2048> and
 k_walk<10, 2048> for rmd160 / xpoint), from HIP events the engine records on its own stream around
 its launches.  The walks are bound by VALU issue, so "bound" is "valu":
