@@ -303,59 +303,91 @@ def pci_bus_id(device: int) -> str | None:
         return None
 
 
-class ClockSampler:
-    """Samples the board's gfx clock (amdsmi, MHz) of the device with bus id `bdf` every `period`
-    seconds in a thread.  Board readings run a few % above the in-kernel clock (MI355X_MICROARCH.md,
-    DVFS give-back): a trend indicator beside the kernel times, not a cycle count."""
+def _num(v) -> float | None:
+    return float(v) if isinstance(v, (int, float)) and not isinstance(v, bool) and v != 0xFFFF else None
+
+
+class BoardSampler:
+    """The board's own view of a run (amdsmi, device with bus id `bdf`; the only device when there is
+    one): gfx clock (MHz, mean over the XCDs' current_gfxclks) and socket power (W) sampled every
+    `period` s in a thread, plus counter snapshots (`snapshot`) whose differences (`between`) give
+
+      * mean socket power from the energy accumulator (amdsmi_get_energy_count, its own resolution);
+      * the share of the interval spent at the package power limit (PPT), at a thermal limit
+        (socket / HBM / VR) and under PROCHOT, from the firmware's residency accumulators over its
+        accumulation counter (gpu_metrics ppt_residency_acc etc.): 1.0 = limited the whole time;
+      * the power cap in force (amdsmi_get_power_cap_info, W).
+
+    Board clocks run a few % above the in-kernel clock (MI355X_MICROARCH.md, DVFS give-back): a
+    trend indicator beside the kernel times, not a cycle count."""
+
+    RESIDENCY = ("ppt_residency_acc", "socket_thm_residency_acc", "hbm_thm_residency_acc", "vr_thm_residency_acc",
+                 "prochot_residency_acc")
 
     def __init__(self, bdf: str | None, period: float = 0.25):
-        self.samples: list[tuple[float, float]] = []
+        self.samples: list[tuple[float, float]] = []        # (t, gfx MHz)
+        self.power_samples: list[tuple[float, float]] = []  # (t, socket W)
         self.error = None
         self._stop = threading.Event()
         self._h = None
         self._period = period
+        self._lock = threading.Lock()
         try:
             import amdsmi
             self._amdsmi = amdsmi
             amdsmi.amdsmi_init()
-            for h in amdsmi.amdsmi_get_processor_handles():
+            hs = amdsmi.amdsmi_get_processor_handles()
+            for h in hs:
                 b = str(amdsmi.amdsmi_get_gpu_device_bdf(h)).lower()
                 if bdf and (b == bdf or b.endswith(bdf.split(":", 1)[-1]) or bdf.endswith(b.split(":", 1)[-1])):
                     self._h = h
                     break
+            if self._h is None and len(hs) == 1:
+                self._h = hs[0]
             if self._h is None:
                 self.error = f"no amdsmi device with bus id {bdf}"
         except Exception as e:  # amdsmi absent or not permitted: the line says why
             self.error = f"amdsmi: {e!r}"[:200]
         self._t = None
 
-    def _read(self) -> float | None:
-        a = self._amdsmi
-        try:
-            ci = a.amdsmi_get_clock_info(self._h, a.AmdSmiClkType.GFX)
-            v = ci.get("clk") if isinstance(ci, dict) else None
-            if v:
-                return float(v)
-        except Exception:
-            pass
-        m = a.amdsmi_get_gpu_metrics_info(self._h)
-        for key in ("current_gfxclk", "average_gfxclk_frequency"):
-            v = m.get(key)
-            if isinstance(v, (int, float)) and 0 < v < 10000:
-                return float(v)
+    def _metrics(self) -> dict:
+        with self._lock:
+            return self._amdsmi.amdsmi_get_gpu_metrics_info(self._h)
+
+    @staticmethod
+    def _clock_of(m: dict) -> float | None:
         v = m.get("current_gfxclks")
         if isinstance(v, list):
             vals = [x for x in v if isinstance(x, (int, float)) and 0 < x < 10000]
             if vals:
                 return sum(vals) / len(vals)
+        for key in ("current_gfxclk", "average_gfxclk_frequency"):
+            x = _num(m.get(key))
+            if x and 0 < x < 10000:
+                return x
         return None
+
+    def _energy(self) -> tuple[float, float] | None:
+        """(joules, resolution in J) from the energy accumulator."""
+        try:
+            with self._lock:
+                e = self._amdsmi.amdsmi_get_energy_count(self._h)
+            res = float(e["counter_resolution"]) * 1e-6  # µJ per count
+            return float(e["energy_accumulator"]) * res, res
+        except Exception:
+            return None
 
     def _run(self):
         while not self._stop.is_set():
             try:
-                v = self._read()
-                if v:
-                    self.samples.append((time.perf_counter(), v))
+                m = self._metrics()
+                t = time.perf_counter()
+                c = self._clock_of(m)
+                if c:
+                    self.samples.append((t, c))
+                p = _num(m.get("current_socket_power"))
+                if p:
+                    self.power_samples.append((t, p))
             except Exception as e:
                 self.error = f"amdsmi read: {e!r}"[:200]
                 return
@@ -375,6 +407,71 @@ class ClockSampler:
     def mean(self, t0: float, t1: float) -> float | None:
         v = [c for t, c in self.samples if t0 <= t <= t1]
         return sum(v) / len(v) if v else None
+
+    def mean_power(self, t0: float, t1: float) -> float | None:
+        v = [c for t, c in self.power_samples if t0 <= t <= t1]
+        return sum(v) / len(v) if v else None
+
+    def snapshot(self) -> dict | None:
+        """Counter values now (perf_counter time, energy, residency accumulators)."""
+        if self._h is None:
+            return None
+        try:
+            m = self._metrics()
+        except Exception as e:
+            self.error = f"amdsmi read: {e!r}"[:200]
+            return None
+        s = {"t": time.perf_counter(), "acc": _num(m.get("accumulation_counter"))}
+        for k in self.RESIDENCY:
+            s[k] = _num(m.get(k))
+        en = self._energy()
+        s["energy_j"], s["energy_res_j"] = en if en else (None, None)
+        return s
+
+    def between(self, a: dict | None, b: dict | None) -> dict | None:
+        """Mean power, power-limit residency and board clock between two snapshots."""
+        if not a or not b:
+            return None
+        dt = b["t"] - a["t"]
+        out = {"seconds": dt, "board_gfxclk_mhz": self.mean(a["t"], b["t"]),
+               "socket_power_w_sampled": self.mean_power(a["t"], b["t"])}
+        if a.get("energy_j") is not None and b.get("energy_j") is not None and dt > 0:
+            out["socket_power_w"] = (b["energy_j"] - a["energy_j"]) / dt
+        if a.get("acc") is not None and b.get("acc") is not None and b["acc"] > a["acc"]:
+            da = b["acc"] - a["acc"]
+            out["accumulation_counts"] = da
+            for k in self.RESIDENCY:
+                if a.get(k) is not None and b.get(k) is not None:
+                    out[k.replace("_acc", "_frac")] = (b[k] - a[k]) / da
+        cap = self.power_cap_w()
+        if cap:
+            out["power_cap_w"] = cap
+            if out.get("socket_power_w"):
+                out["power_over_cap"] = out["socket_power_w"] / cap
+        return out
+
+    def power_cap_w(self) -> float | None:
+        try:
+            with self._lock:
+                c = self._amdsmi.amdsmi_get_power_cap_info(self._h)
+            v = _num(c.get("power_cap"))
+            return v / 1e6 if v and v > 1e5 else v  # reported in µW
+        except Exception:
+            return None
+
+    def info(self) -> dict:
+        out = {"error": self.error, "samples": len(self.samples), "power_samples": len(self.power_samples)}
+        if self._h is not None:
+            try:
+                with self._lock:
+                    out["power_cap_info"] = self._amdsmi.amdsmi_get_power_cap_info(self._h)
+                    out["power_info"] = self._amdsmi.amdsmi_get_power_info(self._h)
+            except Exception as e:
+                out["power_cap_error"] = repr(e)[:200]
+        return out
+
+
+ClockSampler = BoardSampler
 
 
 def timed(D: Dist, eng, steps: int, step_fn, units_per_step: int, kind: int, clock: ClockSampler | None):

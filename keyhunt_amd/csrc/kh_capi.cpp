@@ -314,8 +314,11 @@ struct kh_ctx {
   comb_table comb;
   uint32_t *d_comb = nullptr;
 
-  // lanes
+  // lanes: lanes_max for the 1024-point-group walks and the BSGS giant walk; lanes_hb for the
+  // address family's 4096-point groups (several waves per SIMD slot in one launch, DESIGN.md §2
+  // "Launch geometry").  kh_set_geometry(lanes != 0) sets both.
   uint32_t lanes_max = 1u << 18;
+  uint32_t lanes_hb = KH_LANES_HB;
   uint32_t groups_per_launch = 0;
   uint32_t lanes_alloc = 0;
   int scratch_h = 0;  // inversion-pad entries per lane in d_scratch
@@ -562,9 +565,10 @@ struct job_geom {
   uint64_t gpl;  // groups per lane in the job
 };
 // lanes cover total_groups groups; gpl must divide `gpl_divides` when non-zero
-job_geom plan(kh_ctx *c, uint64_t total_groups, uint64_t gpl_divides) {
+job_geom plan(kh_ctx *c, uint64_t total_groups, uint64_t gpl_divides, uint32_t lanes = 0) {
   job_geom g;
-  uint64_t gpl = (total_groups + c->lanes_max - 1) / c->lanes_max;
+  if (!lanes) lanes = c->lanes_max;
+  uint64_t gpl = (total_groups + lanes - 1) / lanes;
   if (gpl == 0) gpl = 1;
   if (gpl_divides) {
     while (gpl < gpl_divides && gpl_divides % gpl) gpl++;
@@ -705,6 +709,7 @@ int kh_close(kh_ctx *ctx) {
 int kh_set_geometry(kh_ctx *ctx, uint32_t lanes, uint32_t groups_per_launch) {
   if (!ctx) return KH_E_ARG;
   ctx->lanes_max = lanes ? lanes : (1u << 18);
+  ctx->lanes_hb = lanes ? lanes : KH_LANES_HB;
   ctx->groups_per_launch = groups_per_launch;
   return KH_OK;
 }
@@ -822,6 +827,14 @@ int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride_be[32], u
   }
   if (!ctx->d_tbloom) return KH_E_STATE;
   (void)hipSetDevice(ctx->device);
+  if (zg && reaches_order(sc_reduce(u256_from_be(start)),
+                          stride_be ? sc_reduce(u256_from_be(stride_be)) : u256_u64(1), n_keys + 2 * (uint64_t)zg)) {
+    // k_walk_zinv advances each lane's centre by C += G*stride*D; where a centre meets -that (the
+    // next centre is the point at infinity, keys at the group order) the reference's own group is
+    // built from its infinity representation, which this engine does not restate
+    ctx->err = "--rmd-batch-size below 1024 on a chunk that reaches the group order";
+    return KH_E_RANGE;
+  }
   int km = mode == KH_MODE_XPOINT ? KM_XPOINT
          : mode == KH_MODE_ETH ? KM_ETH
          : search == KH_SEARCH_COMPRESS ? KM_H160C
@@ -858,7 +871,7 @@ int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride_be[32], u
   // multiple of the group overshoots its end
   uint64_t total_groups = (n_keys + 2 * H - 1) / (2 * H);
   const uint64_t n_points = total_groups * 2 * H;
-  job_geom jg = plan(ctx, total_groups, 0);
+  job_geom jg = plan(ctx, total_groups, 0, H == KH_WALK_HB ? ctx->lanes_hb : 0);
   // large-group modes interleave lanes (lane g walks groups g, g + L, ...) when the lanes divide
   // the chunk: after the call every lane sits on its group of the chunk that follows, so a call
   // starting there continues them without a lane setup

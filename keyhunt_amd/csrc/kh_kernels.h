@@ -19,6 +19,15 @@ static_assert(KH_WALK_H >= 64 && KH_WALK_H <= 512 && (512 % KH_WALK_H) == 0,
 #ifndef KH_WALK_HB
 #define KH_WALK_HB 2048
 #endif
+// Lanes of the address family's 4096-point-group walks (xpoint, compressed address/rmd160): 2^20, so
+// one 2^32-key chunk is one launch of 16384 waves -- four per wave slot of the xpoint walk (128 VGPRs,
+// 4 waves/SIMD) and 5.3 per slot of the hash walk (168 VGPRs, 3 waves/SIMD).  Waves that start as
+// others end run out of phase with them, so the pad and inversion phases of some overlap the field
+// math of others; with 2^18 lanes (one wave per slot, all in phase) xpoint ran 50.5 vs 57.9 G points/s
+// and rmd160 7.66 vs 8.00 (profiles/r04a_geom_ab.json).  Pad: 2^20 x 4096 x 32 B / 2 = 64 GB.
+#ifndef KH_LANES_HB
+#define KH_LANES_HB (1u << 20)
+#endif
 
 // minimum waves per SIMD requested for the walk kernel: XPOINT/BSGS/BUILD modes (KH_WALK_LB) and
 // the hash160 modes (KH_WALK_LB_HASH).  256 / LB VGPRs per lane at most; see DESIGN.md.

@@ -788,6 +788,17 @@ __global__ void __launch_bounds__(256, KH_WALK_LB_HASH) k_walk_zinv(walk_args A)
     load_fe_k(t2x, T + H * 16);
     load_fe_k(t2y, T + H * 16 + 8);
     fe_sub(dx, t2x, cx);
+    // rare: C = +-T[H].  The reference computes the next centre from its key (3350-3354), so
+    // C = T[H] -- a group centred on key G*stride, e.g. -r 100: with G = 512 -- doubles instead.
+    // C = -T[H] (the next centre is the point at infinity) lies at the group order, which kh_scan
+    // keeps away from this kernel (reaches_order).
+    const bool dbl = fe_is_zero(dx);
+    ge c2;
+    if (dbl) {  // the wave skips this block unless one of its lanes needs it
+      const ge c{cx, cy};
+      ge_double(c2, c);
+      dx.d[0] = 1;  // any non-zero value: this lane's common-path result is replaced
+    }
     fe_inv(dx, dx);
     fe_sub(dy, t2y, cy);
     fe_mul(s, dy, dx);
@@ -797,8 +808,8 @@ __global__ void __launch_bounds__(256, KH_WALK_LB_HASH) k_walk_zinv(walk_args A)
     fe_sub(t, t2x, nx);
     fe_mul(ny, s, t);
     fe_sub(ny, ny, t2y);
-    cx = nx;
-    cy = ny;
+    cx = dbl ? c2.x : nx;
+    cy = dbl ? c2.y : ny;
   }
   store_soa(A.cx, A.L, g, cx);
   store_soa(A.cy, A.L, g, cy);

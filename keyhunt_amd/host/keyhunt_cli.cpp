@@ -449,9 +449,11 @@ void print_stats(uint64_t secs, const U &total) {
     lim[i] = l;
     l = u_mul_u64(l, 1000);
   }
+  // -M (FLAGMATRIX) prints the line as a line of its own; otherwise it overwrites itself in place
+  const char *lead = opt.matrix ? "" : "\r", *tail = opt.matrix ? "\n" : "\r";
   if (u_cmp(per, lim[0]) < 0) {
-    printf("\r[+] Total %s keys in %llu seconds: %s keys/s\r", u_dec(total).c_str(), (unsigned long long)secs,
-           u_dec(per).c_str());
+    printf("%s[+] Total %s keys in %llu seconds: %s keys/s%s", lead, u_dec(total).c_str(), (unsigned long long)secs,
+           u_dec(per).c_str(), tail);
   } else {
     int i = 0;
     while (i < 6 && u_cmp(per, lim[i + 1]) >= 0) i++;
@@ -460,8 +462,8 @@ void print_stats(uint64_t secs, const U &total) {
     U d = per;
     for (int k = 0; k < i; k++) d = u_divmod_u64(d, 1000, nullptr);
     d = u_divmod_u64(d, 1000000, nullptr);
-    printf("\r[+] Total %s keys in %llu seconds: ~%s %s (%s keys/s)\r", u_dec(total).c_str(),
-           (unsigned long long)secs, u_dec(d).c_str(), pfx[i], u_dec(per).c_str());
+    printf("%s[+] Total %s keys in %llu seconds: ~%s %s (%s keys/s)%s", lead, u_dec(total).c_str(),
+           (unsigned long long)secs, u_dec(d).c_str(), pfx[i], u_dec(per).c_str(), tail);
   }
   fflush(stdout);
 }
@@ -484,6 +486,7 @@ U keys_done(const U &twoN) {
 // ---------------------------------------------------------------------------------------------
 struct addr_job {
   int device;
+  int index = 0;  // worker number (the reference's thread_number)
   const std::vector<uint8_t> *rows;
   uint64_t bloom_items;
   uint64_t nseq;
@@ -552,7 +555,15 @@ void addr_worker(addr_job *j) {
         g_cursor = u_add(g_cursor, span);
       }
     }
-    if (opt.matrix) printf("Base key: %s gpu %d\n", u_hex(base).c_str(), j->device);
+    // the chunk's progress line (thread_process, keyhunt.cpp:3333-3346): one line per chunk with -M,
+    // else (without -q) overwritten in place; "thread" is this worker's index, as the reference's
+    if (opt.matrix) {
+      printf("Base key: %s thread %i\n", u_hex(base).c_str(), j->index);
+      fflush(stdout);
+    } else if (!opt.quiet) {
+      printf("\rBase key: %s     \r", u_hex(base).c_str());
+      fflush(stdout);
+    }
     u_to_be32(base, st_be);
     uint32_t nh = 0;
     r = kh_scan(ctx, st_be, stride_be, j->nseq,
@@ -589,7 +600,9 @@ struct bsgs_job {
   const std::vector<fe> *tx, *ty;
   const std::vector<bool> *comp;
   uint64_t n, k;
-  uint64_t bases_per_call;
+  uint64_t bases_per_call;       // consecutive bases of 2N (one counted progression per call)
+  uint64_t list_bases_per_call;  // listed bases (-B backward|both|random|dance, ggsb): the host lists,
+                                 // sorts and uploads each one, so calls stay at ~2^31 giant points
   bool first = false;  // the first GPU's worker (writes the -S files)
   int rc = 0;
 };
@@ -856,49 +869,128 @@ int bsgs_tables(kh_ctx *ctx, const kh_bsgs_info &info, bool first) {
   return KH_OK;
 }
 
-// the targets a call found, printed and recorded as the reference's sequential worker does
-// (keyhunt.cpp:4790-4830); the run ends when every target is found
-void report_found(kh_ctx *ctx, const bsgs_job *j, const std::vector<kh_bsgs_found> &found, uint32_t nf) {
-  for (uint32_t i = 0; i < nf; i++) {
-    uint32_t t = found[i].target;
+// One found target, printed and recorded as the reference's worker does (keyhunt.cpp:4790-4830);
+// returns true when every target is now found (the run then ends, 4811-4814)
+bool print_found(kh_ctx *ctx, const bsgs_job *j, const kh_bsgs_found &fd) {
+  uint32_t t = fd.target;
+  {
     std::lock_guard<std::mutex> lk(g_found_mtx);
-    if (g_found[t]) continue;
+    if (g_found[t]) return false;
     g_found[t] = 1;
-    std::string k = u_hex(u_from_be32(found[i].key));
-    uint8_t pxy[64];
-    kh_pubkeys(ctx, found[i].key, 1, pxy);
-    std::string pub;
-    if ((*j->comp)[t]) {
-      uint8_t p = (pxy[63] & 1) ? 3 : 2;
-      pub = hex(&p, 1) + hex(pxy, 32);
-    } else {
-      uint8_t p = 4;
-      pub = hex(&p, 1) + hex(pxy, 64);
+  }
+  std::string k = u_hex(u_from_be32(fd.key));
+  uint8_t pxy[64];
+  kh_pubkeys(ctx, fd.key, 1, pxy);
+  std::string pub;
+  if ((*j->comp)[t]) {
+    uint8_t p = (pxy[63] & 1) ? 3 : 2;
+    pub = hex(&p, 1) + hex(pxy, 32);
+  } else {
+    uint8_t p = 4;
+    pub = hex(&p, 1) + hex(pxy, 64);
+  }
+  {
+    std::lock_guard<std::mutex> lk2(g_keys_mtx);
+    // each BSGS worker of the reference has its own format: the sequential one (also -B ggsb and
+    // angrygiant) continues its string over a backslash-newline, so no newline is printed
+    // (keyhunt.cpp:4826-4827); random 5079, dance 5885, backward 6144, both 6429
+    const int bm = opt.bsgs_mode;
+    printf(bm == BM_SEQUENTIAL || bm == BM_GGSB || bm == BM_ANGRYGIANT ? "[+] Thread Key found privkey %s   "
+           : bm == BM_RANDOM                                          ? "[+] Thread Key found privkey %s    \n"
+                                                                      : "[+] Thread Key found privkey %s   \n",
+           k.c_str());
+    printf("[+] Publickey %s\n", pub.c_str());
+    FILE *f = fopen("KEYFOUNDKEYFOUND.txt", "a");
+    if (f) {
+      fprintf(f, "Key found privkey %s\nPublickey %s\n", k.c_str(), pub.c_str());
+      fclose(f);
     }
-    {
-      std::lock_guard<std::mutex> lk2(g_keys_mtx);
-      // each BSGS worker of the reference has its own format: the sequential one (also -B ggsb and
-      // angrygiant) continues its string over a backslash-newline, so no newline is printed
-      // (keyhunt.cpp:4826-4827); random 5079, dance 5885, backward 6144, both 6429
-      const int bm = opt.bsgs_mode;
-      printf(bm == BM_SEQUENTIAL || bm == BM_GGSB || bm == BM_ANGRYGIANT ? "[+] Thread Key found privkey %s   "
-             : bm == BM_RANDOM                                          ? "[+] Thread Key found privkey %s    \n"
-                                                                        : "[+] Thread Key found privkey %s   \n",
-             k.c_str());
-      printf("[+] Publickey %s\n", pub.c_str());
-      FILE *f = fopen("KEYFOUNDKEYFOUND.txt", "a");
-      if (f) {
-        fprintf(f, "Key found privkey %s\nPublickey %s\n", k.c_str(), pub.c_str());
-        fclose(f);
+    fflush(stdout);
+  }
+  std::lock_guard<std::mutex> lk(g_found_mtx);
+  return std::all_of(g_found.begin(), g_found.end(), [](uint8_t v) { return v != 0; });
+}
+
+// The per-base progress lines of the reference's BSGS workers, each printed as the worker takes the
+// base (keyhunt.cpp:4618-4633; random 4955-4968, dance 5762-5774, backward 6023-6035, both
+// 6308-6320): "[+] Thread 0x%s \n" with -M, else, unless -q, "\r[+] Thread 0x%s   \r" overwritten in
+// place (the random worker pads with two spaces).  A call walks many bases: with -M every base's
+// line is printed in the reference's order, each before the keys found in that base; otherwise the
+// lines of a run of bases would overwrite one another, so the run's overlay is printed once -- what
+// they leave on the terminal (the last line, completed by any longer earlier line).
+struct base_lines {
+  const bool on = opt.matrix || !opt.quiet;
+  const char *sp = opt.bsgs_mode == BM_RANDOM ? "  " : opt.matrix ? " " : "   ";
+  std::string overlay;  // the pending in-place lines, rendered
+  void add(const U &base) {
+    if (!on) return;
+    const std::string ln = "[+] Thread 0x" + u_hex(base) + sp;
+    if (opt.matrix) {
+      printf("%s\n", ln.c_str());
+      return;
+    }
+    if (ln.size() >= overlay.size())
+      overlay = ln;
+    else
+      overlay.replace(0, ln.size(), ln);
+  }
+  void flush() {
+    if (!overlay.empty()) printf("\r%s\r", overlay.c_str());
+    overlay.clear();
+    fflush(stdout);
+  }
+};
+
+// The bases of one call, in the order the reference's worker takes them: `count` bases from `start`
+// `step` apart, or an explicit list.  Each found key is reported after the progress line of the
+// first base whose window (base, base + 2M * cycles * 1024] holds it -- the base a single reference
+// thread finds it in.  Exits (status 1) when every target is found.
+void report_call(kh_ctx *ctx, const bsgs_job *j, const kh_bsgs_info &info, const U &start, const U &step,
+                 uint64_t count, const std::vector<U> *list, const std::vector<kh_bsgs_found> &found, uint32_t nf) {
+  const uint64_t W = 2 * info.m * info.cycles * 1024;
+  auto base_at = [&](uint64_t i) { return list ? (*list)[i] : u_add(start, u_mul_u64(step, i)); };
+  std::vector<std::pair<uint64_t, uint32_t>> at;  // (base position, found index)
+  for (uint32_t f = 0; f < nf && f < found.size(); f++) {
+    const U key = u_from_be32(found[f].key);
+    uint64_t pos = count ? count - 1 : 0;
+    if (list) {
+      for (uint64_t i = 0; i < count; i++) {
+        const U b = (*list)[i];
+        if (u_cmp(key, b) > 0 && u_cmp(u_sub(key, b), u_from_u64(W)) <= 0) {
+          pos = i;
+          break;
+        }
       }
-      fflush(stdout);
+    } else if (u_cmp(key, start) > 0 && step.v[1] == 0 && step.v[2] == 0 && step.v[3] == 0 && step.v[4] == 0 &&
+               step.v[0]) {
+      const U rel = u_sub(key, start);  // smallest b with rel <= b * step + W
+      if (u_cmp(rel, u_from_u64(W)) > 0) {
+        uint64_t rem = 0;
+        const U q = u_divmod_u64(u_sub(rel, u_from_u64(W)), step.v[0], &rem);
+        if (u_bitlen(q) < 63) pos = std::min<uint64_t>(pos, q.v[0] + (rem ? 1 : 0));
+      } else {
+        pos = 0;
+      }
     }
-    bool all = std::all_of(g_found.begin(), g_found.end(), [](uint8_t v) { return v != 0; });
-    if (all) {
+    at.push_back({pos, f});
+  }
+  std::sort(at.begin(), at.end());
+  base_lines bl;
+  uint64_t next = 0;
+  for (auto &p : at) {
+    if (bl.on) {
+      for (; next <= p.first && next < count; next++) bl.add(base_at(next));
+      bl.flush();
+    }
+    if (print_found(ctx, j, found[p.second])) {
       printf("All points were found\n");
       fflush(stdout);
       _exit(EXIT_FAILURE);  // keyhunt.cpp:4811-4814
     }
+  }
+  if (bl.on) {
+    for (; next < count; next++) bl.add(base_at(next));
+    bl.flush();
   }
 }
 
@@ -924,14 +1016,15 @@ void bsgs_worker(bsgs_job *j) {
   if (!r) r = kh_bsgs_set_targets(ctx, xy.data(), (uint32_t)nt);
   const U twoN = u_mul_u64(u_from_u64(info.n), 2);
   std::vector<kh_bsgs_found> found(nt + 1);
-  std::vector<U> bases;
+  std::vector<U> bases, drawn;
   std::vector<uint8_t> list_be;
   const bool progression = opt.bsgs_mode == BM_SEQUENTIAL || opt.bsgs_mode == BM_ANGRYGIANT || opt.bsgs_mode == BM_GGSB;
   while (!r) {
     if (progression) {
       U st;
       uint64_t nb = 0;
-      if (!take_progression(g_step, j->bases_per_call, st, nb)) break;
+      if (!take_progression(g_step, u_cmp(g_step, twoN) == 0 ? j->bases_per_call : j->list_bases_per_call, st, nb))
+        break;
       bases.assign(1, st);
       uint8_t st_be[32];
       u_to_be32(st, st_be);
@@ -949,11 +1042,12 @@ void bsgs_worker(bsgs_job *j) {
         break;
       }
       g_bases_done += nb;
-      report_found(ctx, j, found, nf);
+      report_call(ctx, j, info, st, g_step, nb, nullptr, found, nf);
       continue;
     }
-    if (!take_bases(g_step, j->bases_per_call, bases)) break;
+    if (!take_bases(g_step, j->list_bases_per_call, bases)) break;
     const uint64_t nb = bases.size();
+    drawn = bases;  // the reference's order, for the progress lines
     // consecutive ascending bases go through kh_bsgs_scan (one progression), others as a list
     std::sort(bases.begin(), bases.end(), [](const U &a, const U &b) { return u_cmp(a, b) < 0; });
     bool consecutive = true;
@@ -973,7 +1067,7 @@ void bsgs_worker(bsgs_job *j) {
       break;
     }
     g_bases_done += nb;
-    report_found(ctx, j, found, nf);
+    report_call(ctx, j, info, U{}, g_step, nb, &drawn, found, nf);
   }
   j->rc = r;
   kh_close(ctx);
@@ -1351,6 +1445,7 @@ int main(int argc, char **argv) {
     g_running = gpus;
     for (int d = 0; d < gpus; d++) {
       aj[d].device = d % ndev;
+      aj[d].index = d;
       aj[d].rows = &rows;
       // initBloomFilter (keyhunt.cpp:7608): max(10000, items), times -z above the floor
       const uint64_t nitems = items ? items : rows.size() / 20;
@@ -1450,6 +1545,7 @@ int main(int argc, char **argv) {
       {
         uint64_t aux = Nr / M, pts = ((aux + 1023) / 1024) * 1024;
         bj[d].bases_per_call = std::max<uint64_t>(1, (1ULL << 35) / pts);
+        bj[d].list_bases_per_call = std::max<uint64_t>(1, (1ULL << 31) / pts);
         const U span = u_sub(opt.end, opt.start);
         if (g_step.v[1] == 0 && g_step.v[2] == 0 && g_step.v[3] == 0 && g_step.v[4] == 0) {
           uint64_t rem = 0;
@@ -1457,6 +1553,7 @@ int main(int argc, char **argv) {
           if (u_bitlen(nb) <= 40) {
             const uint64_t bases = nb.v[0] + (rem ? 1 : 0), share = (bases + gpus - 1) / gpus;
             bj[d].bases_per_call = std::max<uint64_t>(1, std::min(bj[d].bases_per_call, share));
+            bj[d].list_bases_per_call = std::max<uint64_t>(1, std::min(bj[d].list_bases_per_call, share));
           }
         }
       }

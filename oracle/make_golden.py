@@ -21,7 +21,10 @@ TEST INFRASTRUCTURE.  Runs in the development container only (needs /root/refere
                                  request of BSGSD_REQUESTS with the raw reply bytes and the lines the
                                  daemon printed for it, plus its KEYFOUNDKEYFOUND.txt.
 
-Usage:  python oracle/make_golden.py [--vectors] [--e2e] [--tables] [--data] [--bsgsd]
+  tests/golden/ref_stdout.json   the reference CLI's whole stdout of single-thread runs with -M and
+                                 without -q (progress lines), and its stats lines with and without -M.
+
+Usage:  python oracle/make_golden.py [--vectors] [--e2e] [--tables] [--data] [--bsgsd] [--stdout]
 """
 from __future__ import annotations
 
@@ -581,8 +584,64 @@ def gen_mapped() -> None:
         json.dump(res, f, indent=1)
 
 
+# The reference's own stdout of single-thread runs (-t 1, so its print order is deterministic), for the
+# output contract: the per-chunk "Base key" lines (keyhunt.cpp:3333-3346), the BSGS per-base
+# "[+] Thread 0x..." lines (4618-4633, backward 6023-6035), with -M (FLAGMATRIX: one line each) and
+# without -q (overwritten in place with \r), and the hit / "All points were found" / "End" text
+# between them.  -s 0: no stats line.  tests/golden/data/bsgs_two_targets.txt = 63.pub + 125.txt (one
+# target is never found, so the run walks every base and ends with "End").
+STDOUT_RUNS = [
+    ("rmd160_M", ["-m", "rmd160", "-f", "1to32.rmd", "-l", "compress", "-r", "1:300000", "-n", "0x100000", "-M"]),
+    ("rmd160_verbose", ["-m", "rmd160", "-f", "1to32.rmd", "-l", "compress", "-r", "1:300000", "-n", "0x100000"]),
+    ("rmd160_M_quiet", ["-m", "rmd160", "-f", "1to32.rmd", "-l", "compress", "-r", "1:300000", "-n", "0x100000", "-M", "-q"]),
+    ("rmd160_quiet", ["-m", "rmd160", "-f", "1to32.rmd", "-l", "compress", "-r", "1:300000", "-n", "0x100000", "-q"]),
+    ("address_M", ["-m", "address", "-f", "1to32.txt", "-r", "1:300000", "-n", "0x100000", "-M"]),
+    ("xpoint_M", ["-m", "xpoint", "-f", "1to63_65.txt", "-r", "1:300000", "-n", "0x100000", "-M"]),
+    ("xpoint_verbose", ["-m", "xpoint", "-f", "1to63_65.txt", "-r", "1:300000", "-n", "0x100000"]),
+    ("bsgs_63_M", ["-m", "bsgs", "-f", "63.pub", "-r", "7cce5a0000000000:7cce9a0000000000", "-M"]),
+    ("bsgs_63_verbose", ["-m", "bsgs", "-f", "63.pub", "-r", "7cce5a0000000000:7cce9a0000000000"]),
+    ("bsgs_63_bases_M", ["-m", "bsgs", "-f", "63.pub", "-n", "0x100000", "-r", "7cce5efdac000000:7cce5efdad000000", "-M"]),
+    ("bsgs_63_bases_verbose", ["-m", "bsgs", "-f", "63.pub", "-n", "0x100000", "-r", "7cce5efdac000000:7cce5efdad000000"]),
+    ("bsgs_63_bases_quiet", ["-m", "bsgs", "-f", "63.pub", "-n", "0x100000", "-r", "7cce5efdac000000:7cce5efdad000000", "-q"]),
+    ("bsgs_63_backward_M", ["-m", "bsgs", "-f", "63.pub", "-n", "0x100000", "-B", "backward", "-r", "7cce5efdac000000:7cce5efdad000000", "-M"]),
+    ("bsgs_63_backward_verbose", ["-m", "bsgs", "-f", "63.pub", "-n", "0x100000", "-B", "backward", "-r", "7cce5efdac000000:7cce5efdad000000"]),
+    ("bsgs_two_M", ["-m", "bsgs", "-f", "bsgs_two_targets.txt", "-n", "0x100000", "-r", "7cce5efdac000000:7cce5efdad000000", "-M"]),
+    ("bsgs_two_verbose", ["-m", "bsgs", "-f", "bsgs_two_targets.txt", "-n", "0x100000", "-r", "7cce5efdac000000:7cce5efdad000000"]),
+]
+# the stats line (keyhunt.cpp:2904-2950) with and without -M: runs stopped after a few seconds; the
+# fixture keeps the lines, the test compares their shape (numbers are the run's)
+STATS_RUNS = [
+    ("rmd160_stats_M", ["-m", "rmd160", "-f", "1to32.rmd", "-l", "compress", "-r", "1:400000000", "-s", "1", "-M", "-q"], 4),
+    ("rmd160_stats", ["-m", "rmd160", "-f", "1to32.rmd", "-l", "compress", "-r", "1:400000000", "-s", "1", "-q"], 4),
+]
+STATS_LINE = re.compile(rb"\r?\[\+\] Total \d+ keys in \d+ seconds: [^\r\n]*[\r\n]")
+
+
+def gen_stdout():
+    subprocess.run(["make", "-s", "-C", HERE, "-f", "Makefile.ref", "-j8"], check=True)
+    res = {"_generator": "oracle/make_golden.py --stdout running oracle/_ref/keyhunt -t 1 -s 0"}
+    for name, argv in STDOUT_RUNS:
+        with tempfile.TemporaryDirectory() as td:
+            for fn in os.listdir(DATA):
+                shutil.copy(os.path.join(DATA, fn), td)
+            p = subprocess.run(["timeout", "300", REF_BIN] + argv + ["-t", "1", "-s", "0"], cwd=td, capture_output=True)
+        res[name] = {"argv": argv, "exit": p.returncode, "stdout": p.stdout.decode("latin-1")}
+        print(name, p.returncode, len(p.stdout), flush=True)
+    for name, argv, secs in STATS_RUNS:
+        with tempfile.TemporaryDirectory() as td:
+            for fn in os.listdir(DATA):
+                shutil.copy(os.path.join(DATA, fn), td)
+            p = subprocess.run(["timeout", str(secs), REF_BIN] + argv + ["-t", "1"], cwd=td, capture_output=True)
+        lines = [m.decode("latin-1") for m in STATS_LINE.findall(p.stdout)]
+        res[name] = {"argv": argv, "stats_lines": lines}
+        print(name, lines, flush=True)
+    with open(os.path.join(REPO, "tests", "golden", "ref_stdout.json"), "w") as f:
+        json.dump(res, f, indent=1)
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
+    ap.add_argument("--stdout", action="store_true")
     ap.add_argument("--vectors", action="store_true")
     ap.add_argument("--e2e", action="store_true")
     ap.add_argument("--tables", action="store_true")
@@ -592,8 +651,8 @@ if __name__ == "__main__":
     ap.add_argument("--bsgsd-mapped", action="store_true")
     ap.add_argument("--only", nargs="*")
     a = ap.parse_args()
-    if not (a.vectors or a.e2e or a.tables or a.data or a.bsgsd or a.mapped or a.bsgsd_mapped):
-        a.vectors = a.e2e = a.tables = a.data = a.bsgsd = a.mapped = a.bsgsd_mapped = True
+    if not (a.vectors or a.e2e or a.tables or a.data or a.bsgsd or a.mapped or a.bsgsd_mapped or a.stdout):
+        a.vectors = a.e2e = a.tables = a.data = a.bsgsd = a.mapped = a.bsgsd_mapped = a.stdout = True
     if a.vectors:
         gen_vectors()
     if a.e2e:
@@ -608,3 +667,5 @@ if __name__ == "__main__":
         gen_mapped()
     if a.bsgsd_mapped:
         gen_bsgsd_mapped()
+    if a.stdout:
+        gen_stdout()

@@ -22,6 +22,38 @@ STDERR_NOTE = re.compile(r"^\[[IE]\] (?:Ommiting|Omiting|Ignoring)[^\n]*$", re.M
 STDOUT_NOTE = re.compile(r"^(?:ParsePublicKeyHex: |Invalid length: )[^\n]*$", re.M)
 
 
+# where the run section of a CLI's stdout starts: the first progress line (keyhunt.cpp:3333-3346 per
+# chunk, 4618-4633 per BSGS base), hit block or found line, or the final "End"
+RUN_START = re.compile(r"\r?Base key: |\r?\[\+\] Thread 0x|\nHit! |\n Hit!!!! |\nVanity Private|\[\+\] Thread Key found"
+                       r"|\nEnd\n")
+
+
+def run_section(text: str) -> str:
+    """stdout from the first progress line, hit or "End" on (the header before it is not compared)."""
+    m = RUN_START.search(text)
+    return text[m.start():] if m else ""
+
+
+def render(text: str) -> str:
+    """What a terminal shows for `text`: \\r returns to the start of the line, later characters
+    overwrite earlier ones, \\n ends the line."""
+    lines, cur, col = [], [], 0
+    for ch in text:
+        if ch == "\n":
+            lines.append("".join(cur))
+            cur, col = [], 0
+        elif ch == "\r":
+            col = 0
+        else:
+            if col < len(cur):
+                cur[col] = ch
+            else:
+                cur.append(ch)
+            col += 1
+    lines.append("".join(cur))
+    return "\n".join(lines)
+
+
 def parse_keyfound(text: str, ordered: bool = False) -> list[dict]:
     """The records of KEYFOUNDKEYFOUND.txt / VANITYKEYFOUND.txt, sorted by key (or, with ordered, in
     file order per record kind, as oracle/make_golden.py stores "hits_in_order")."""

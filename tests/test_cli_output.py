@@ -1,0 +1,60 @@
+"""CPU checks of the output-contract fixtures (tests/golden/ref_stdout.json) and of the rule the CLI
+uses for in-place progress lines: a run of "\\r<line>\\r" writes shows on a terminal as their overlay,
+so printing the overlay once per engine call (keyhunt_cli.cpp base_lines) renders exactly what the
+reference's per-base writes render (keyhunt.cpp:4626-4631, 3340-3345)."""
+import json
+import os
+import re
+
+from conftest import GOLDEN
+from _cli import render, run_section
+
+REF = json.load(open(os.path.join(GOLDEN, "ref_stdout.json")))
+
+
+def overlay(lines: list[str]) -> str:
+    out = ""
+    for ln in lines:
+        out = ln if len(ln) >= len(out) else ln + out[len(ln):]
+    return out
+
+
+def collapse(text: str) -> str:
+    """Every run of consecutive in-place lines replaced by one write of their overlay."""
+    def sub(m):
+        return "\r" + overlay(re.findall(r"\r([^\r\n]*)\r", m.group(0))) + "\r"
+    return re.sub(r"(?:\r[^\r\n]*\r)+", sub, text)
+
+
+def test_fixtures_present():
+    names = {k for k in REF if not k.startswith("_")}
+    for n in ("rmd160_M", "rmd160_verbose", "bsgs_63_M", "bsgs_63_verbose", "bsgs_two_verbose", "rmd160_stats_M"):
+        assert n in names
+
+
+def test_overlay_renders_like_every_line():
+    for name, ref in REF.items():
+        if name.startswith("_") or "stdout" not in ref:
+            continue
+        sec = run_section(ref["stdout"])
+        assert sec, name
+        assert render(collapse(sec)) == render(sec), name
+
+
+def test_overlay_of_shrinking_lines():
+    s = "\r[+] Thread 0x10000   \r\r[+] Thread 0xffff   \r"
+    assert render(collapse(s)) == render(s) == "[+] Thread 0xffff    "
+
+
+def test_matrix_lines_one_per_base():
+    """-M: one "[+] Thread 0x<base> \\n" per base up to the one holding the key, then the key."""
+    sec = run_section(REF["bsgs_63_bases_M"]["stdout"])
+    bases = re.findall(r"\[\+\] Thread 0x([0-9a-f]+) \n", sec)
+    assert [int(b, 16) for b in bases] == [0x7cce5efdac000000 + i * 0x200000 for i in range(7)]
+    assert sec.endswith("[+] Thread Key found privkey 7cce5efdaccf6808   [+] Publickey "
+                        "0365ec2994b8cc0a20d40dd69edfe55ca32a54bcbbaa6b0ddcff36049301a54579\nAll points were found\n")
+
+
+def test_stats_fixture_terminators():
+    assert all(l.endswith("\n") and not l.startswith("\r") for l in REF["rmd160_stats_M"]["stats_lines"])
+    assert all(l.startswith("\r") and l.endswith("\r") for l in REF["rmd160_stats"]["stats_lines"])

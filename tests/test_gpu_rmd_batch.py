@@ -13,6 +13,7 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 P = 2**256 - 2**32 - 977
+ORDER_N = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141
 
 
 def _point_rows(oracle, pts, rng):
@@ -89,5 +90,37 @@ def test_engine_rmd_batch_refuses_bad_sizes_and_xpoint(engine, oracle):
     try:
         with pytest.raises(KhError):
             engine.scan(1, 4096, mode=1, search=2)
+    finally:
+        engine.set_rmd_batch(1024)
+
+
+@pytest.mark.parametrize("G", [8, 512])
+def test_engine_rmd_batch_centre_on_the_jump(engine, oracle, G):
+    """A group centred on key G (start = G/2) is the lane's jump T[H] itself: the next centre is 2C,
+    a doubling, which the reference gets by recomputing the centre from its key (keyhunt.cpp:3350-3354).
+    Few lanes, so each walks many groups past that one."""
+    rng = random.Random(G)
+    start, n_keys = G // 2, 64 * G
+    rows = _targets(oracle, start, n_keys, G, rng, n=24)
+    engine.set_targets(rows)
+    engine.set_geometry(4, 0)
+    engine.set_rmd_batch(G)
+    try:
+        got = engine.scan(start, n_keys, mode=0, search=2)
+    finally:
+        engine.set_rmd_batch(1024)
+        engine.set_geometry(0, 0)
+    ref = oracle.scan_chunk(0, 2, start, n_keys, rows, group=G)
+    assert ref
+    assert sorted((h.key, h.compressed, h.kind) for h in got) == sorted(ref)
+
+
+def test_engine_rmd_batch_refuses_chunks_reaching_the_order(engine, oracle):
+    from keyhunt_amd.engine import KhError
+    engine.set_targets([bytes(20)])
+    engine.set_rmd_batch(512)
+    try:
+        with pytest.raises(KhError):
+            engine.scan(ORDER_N - 1000, 4096, mode=0, search=0)
     finally:
         engine.set_rmd_batch(1024)
