@@ -16,8 +16,10 @@ Metric (BASELINE.json): "Mkeys/s at 1/2/4/8 GPU (BSGS b125; addr b66); HBM GB/s 
 Sustained measurement (throughput runs of >= 60 s after warm-up): the batch of a step
 (B bases, C chunks) is sized from the last warm-up step so that the K timed steps last --seconds
 (primary, default 60) and --seconds-secondary (default 20) per address-family leg; the line reports
-the rate of the first and the last quarter of the timed steps, each with its kernel time per launch
-and the board's gfx clock sampled through amdsmi while they ran.
+the rate of the first and the last quarter of the timed steps, each with its kernel time per launch,
+the board's gfx clock and socket power (amdsmi), and over the whole timed region the board's own
+counters (BoardSampler): mean socket power from the energy accumulator, the power cap, the share of
+the time spent at the package power limit (ppt_residency_frac, "power_capped") and points per joule.
 
 Parity at full size: after each leg's timed loop (outside it), the same engine with the same tables
 scans the SURVEY.md 8c known-answer window of that workload and must find the reference's key
@@ -33,34 +35,34 @@ engine owns the GPU through its own HIP stream, synchronised on both sides of th
 
 Walks in flight (--walks, --walks-secondary; Walks): each leg may drive S contexts on its GPU, each
 with its own stream and host thread, walking its own contiguous part of the rank region
-(walk_origin).  Defaults from a same-box A/B: S = 1 for BSGS, 2 for rmd160 / xpoint.  With S > 1 the
-launches overlap, so the roofline prices the chip's time per launch (timed wall / all launches,
-chip_ms_per_launch) and reports the launches' own event mean beside it (event_mean_launch_ms, which
-a rocprofv3 kernel trace of the run agrees with).
+(walk_origin).  Default S = 1 for every leg: the configuration the CLI and the INTEGRATION.md binding
+run.  With S > 1 the launches overlap, so the roofline prices the chip's time per launch (timed wall /
+all launches, chip_ms_per_launch) and reports the launches' own event mean beside it
+(event_mean_launch_ms, which a rocprofv3 kernel trace of the run agrees with).
 
 roofline: dominant kernel of each leg (the giant-step walk k_walk<7, 2048>; k_walk<11, 2048> and
 k_walk<10, 2048> for rmd160 / xpoint), from HIP events the engine records on its own stream around
 its launches.  The walks are bound by VALU issue, so "bound" is "valu":
 achieved = VALU wave-instructions per launch (rocprofv3 SQ_INSTS_VALU per point, committed under
-profiles/, x this run's points per launch) / mean launch time.  Three ceilings:
-  peak / frac        1024 SIMDs x 2.4 GHz / 4 cycles: one wave64 VALU instruction per SIMD per
-                     quad-cycle (the SQ's issue unit and the cost of the multiply-add and carry ops);
-  peak_hw / frac_hw  1024 SIMDs x 2.4 GHz / 2 cycles: the guide's wave64 issue on a SIMD-32
-                     (MI355X_MICROARCH.md), which only full-rate ops reach;
-  frac_mix           the kernel's own class-weighted ceiling: sum over instruction classes of its
-                     dynamic count per point x the class's measured SIMD cycles (tools/ubench_cost.hip,
-                     in shader cycles), s_nop included (profiles/r03_valu_mix.json, tools/valu_mix.py),
-                     at 2.4 GHz; frac_mix_clock is the same at the profiled dispatch's own clock.
+profiles/, x this run's points per launch) / mean launch time.  Two ceilings, both upper bounds:
+  peak / frac   1024 SIMDs x 2.4 GHz / 2 cycles: the hardware's wave64 VALU issue on a SIMD-32
+                (MI355X_MICROARCH.md), which only full-rate instructions reach;
+  frac_mix      the kernel's own instruction mix per point at the issue floor of each instruction
+                (2 / 4 cycles per full- / half-rate wave64 instruction, s_nop at its measured in-situ
+                cost, dual-issued instructions free; tools/valu_mix.py -> profiles/r*_valu_mix.json)
+                at the clock the board reported over the leg's timed region.
 The HBM side is reported too ("hbm"): algorithmic bytes (BSGS: 64 B per giant point, one random line
 of the blocked layer 1; the reference layout's is 128 B) / launch time against 8 TB/s,
 and traffic = HBM bytes per launch from the PMC counters with the guide's gfx950 corrections
 (tools/pmc_summary.py), or null.
 cpu_baseline: rank 0 at N=1 only, on every leg the reference binary built from its own sources with
-its own optimisation flags (oracle/_ref/keyhunt_fast, oracle/Makefile.ref; kind "reference") run for
---cpu-seconds on the job's CPU share (cpu_threads), its own last stats line parsed; "all_cpus" scales
-its per-thread rate to every CPU of the host.  BSGS skips the reference's baby-step build: the engine
-writes the -S table files in the reference's format (kh_bsgs_save, byte-identical) and the reference
-reads them (-S -6).
+its own optimisation flags (oracle/_ref/keyhunt_fast, oracle/Makefile.ref; kind "reference"), run for
+--cpu-seconds of its own stats clock twice: on the job's CPU share (cpu_threads: "value", "threads")
+and with -t 1 ("per_core"), its own last stats line parsed each time; the host's sockets, physical
+cores and threads per core come from lscpu.  "long_sample" quotes the newest >= 60-s measurement
+(bench.py --cpu-only --cpu-seconds 60, profiles/r*_cpu_baseline_*.json).  BSGS skips the reference's
+baby-step build: the engine writes the -S table files in the reference's format (kh_bsgs_save,
+byte-identical) and the reference reads them (-S -6).
 """
 from __future__ import annotations
 
@@ -85,11 +87,10 @@ ALGO_BYTES_PER_GIANT_POINT = {0: 128, 1: 64}      # by layer-1 layout (reference
 WALK_KERNEL = {0: "k_walk<4, 2048>", 1: "k_walk<7, 2048>"}    # KM_BSGS, KM_BSGSB on 4096-point groups
 SIMDS = 256 * 4
 NOMINAL_GHZ = 2.4
-# 1024 SIMDs x 2.4 GHz / 4 cycles per wave64 VALU instruction (SQ quad-cycle; measured issue cost of
-# v_mad_u64_u32 / v_add_co / v_addc_co / v_bitop3 at 4 waves per SIMD, profiles/r03_ubench_cost.txt)
-VALU_ISSUE_CYCLES = 4
-VALU_PEAK_GIPS = SIMDS * NOMINAL_GHZ / VALU_ISSUE_CYCLES
-VALU_PEAK_HW_GIPS = SIMDS * NOMINAL_GHZ / 2          # wave64 over 2 cycles on a SIMD-32 (guide)
+# the hardware's VALU issue peak: 1024 SIMDs x 2.4 GHz / 2 cycles per wave64 instruction on a SIMD-32
+# (MI355X_MICROARCH.md); only full-rate instructions reach it, the walks' multiply-adds and carry ops
+# take 4 cycles (profiles/r04_valu_mix.json prices the mix: frac_mix)
+VALU_PEAK_GIPS = SIMDS * NOMINAL_GHZ / 2
 RANDOM16_CEILING_GPS = 51.36   # measured random 16-B nontemporal loads/s, 24 GB footprint (profiles/)
 PUZZLE125 = "0233709eb11e0d4439a729f21c2c443dedb727528229713f0065721ba8fa46f00e"
 PUZZLE130 = "03633cbe3ec02b9401c5effa144c5b4d22f87940259634858fc7e59b1c09937852"
@@ -234,12 +235,12 @@ class Walks:
             self.pool.shutdown()
 
 
-# walk launches in flight per GPU, per leg (bench.py --walks / --walks-secondary; same-box A/B of 25 s /
-# 8 s windows, profiles/r03u_walks_ab.json): the BSGS walk lost 3 % with two contexts (one launch of
-# 2^18 lanes already holds every SIMD at its 4-wave VGPR limit), the hash walks gained (rmd160 +4.5 %,
-# xpoint +17 %: their launches' inversion and pad phases leave issue slots the other context fills)
+# walk contexts per GPU, per leg (bench.py --walks / --walks-secondary): one, as the CLI and the
+# INTEGRATION.md binding open.  Round 3 ran the address legs on two contexts, whose launches filled each
+# other's phases (xpoint +17 %); since round 4 one context's launch holds 2^20 lanes, four waves per
+# wave slot, which gets the same (kh_kernels.h KH_LANES_HB, profiles/r04a_geom_ab.json)
 WALKS_BSGS = 1
-WALKS_ADDRESS = 2
+WALKS_ADDRESS = 1
 
 
 def batch_for(seconds: float, steps: int, unit_s: float, quantum: int, floor: int) -> int:
@@ -474,13 +475,15 @@ class BoardSampler:
 ClockSampler = BoardSampler
 
 
-def timed(D: Dist, eng, steps: int, step_fn, units_per_step: int, kind: int, clock: ClockSampler | None):
-    """K timed steps bracketed by barrier + synchronize; returns (max-over-ranks seconds, per-step
-    records (wall end, cumulative kernel ms and launches)) for the quarter analysis."""
+def timed(D: Dist, eng, steps: int, step_fn, units_per_step: int, kind: int, clock: BoardSampler | None):
+    """K timed steps bracketed by barrier + synchronize; returns (max-over-ranks seconds, t0, t1,
+    per-step records (wall end, cumulative kernel ms and launches) for the quarter analysis, the
+    board's counters between t0 and t1 (BoardSampler.between: power, power-limit residency, clock))."""
     eng.synchronize()
     D.barrier()
     eng.kernel_time_reset()
     recs = []
+    b0 = clock.snapshot() if clock else None
     t0 = time.perf_counter()
     for s in range(steps):
         step_fn(s)
@@ -488,13 +491,17 @@ def timed(D: Dist, eng, steps: int, step_fn, units_per_step: int, kind: int, clo
         recs.append((time.perf_counter(), ms, la))
     eng.synchronize()
     t1 = time.perf_counter()
+    b1 = clock.snapshot() if clock else None
     D.barrier()
-    return D.max(t1 - t0), t0, t1, recs
+    return D.max(t1 - t0), t0, t1, recs, (clock.between(b0, b1) if clock else None)
 
 
-def quarters(t0: float, recs: list, units_per_step: int, keys_per_unit: float, clock: ClockSampler | None) -> dict | None:
+def quarters(t0: float, recs: list, units_per_step: int, keys_per_unit: float, clock: BoardSampler | None,
+             board: dict | None = None, points_per_s: float | None = None) -> dict | None:
     """Rate of the first and the last quarter of the timed steps (keys/s from their wall time), their
-    kernel ms per launch, and the mean board clock while they ran."""
+    kernel ms per launch, the mean board clock and socket power while they ran; and over the whole
+    timed region (`board`, BoardSampler.between) the mean power, the share of it spent at the package
+    power limit (ppt_residency_frac) and the points per joule."""
     K = len(recs)
     if K < 4:
         return None
@@ -506,9 +513,20 @@ def quarters(t0: float, recs: list, units_per_step: int, keys_per_unit: float, c
         te, ms1, la1 = recs[b - 1]
         out[name] = {"steps": [a, b], "mkeys_per_s": (b - a) * units_per_step * keys_per_unit / (te - ts) / 1e6,
                      "kernel_ms_per_launch": (ms1 - ms0) / max(1, la1 - la0),
-                     "board_gfxclk_mhz": clock.mean(ts, te) if clock else None}
+                     "board_gfxclk_mhz": clock.mean(ts, te) if clock else None,
+                     "socket_power_w": clock.mean_power(ts, te) if clock else None}
     f, l = out["first_quarter"], out["last_quarter"]
     out["last_over_first"] = l["mkeys_per_s"] / f["mkeys_per_s"]
+    if board:
+        out["board"] = board
+        if points_per_s and board.get("socket_power_w"):
+            out["points_per_joule"] = points_per_s / board["socket_power_w"]
+        ppt = board.get("ppt_residency_frac")
+        if ppt is not None:
+            out["power_capped"] = {"ppt_residency_frac": ppt, "socket_power_w": board.get("socket_power_w"),
+                                   "power_cap_w": board.get("power_cap_w"),
+                                   "verdict": "power-capped" if ppt >= 0.5 else "partly power-capped" if ppt >= 0.1
+                                   else "not power-capped"}
     return out
 
 
@@ -551,7 +569,7 @@ def bsgs_leg(D: Dist, W: Walks, args, clock):
         last = time.perf_counter() - t
     B = int(D.max(batch_for(args.seconds, args.steps, last / B0, B0, B0) if args.warmup else B0))
     progress(f"BSGS warm-up done; timing {args.steps} steps of {B} bases")
-    T, t0, t1, recs = timed(D, W, args.steps, lambda s: run(B), B, K.engine.TIME_BSGS, clock)
+    T, t0, t1, recs, board = timed(D, W, args.steps, lambda s: run(B), B, K.engine.TIME_BSGS, clock)
     progress(f"BSGS timed region {T:.1f} s; known-answer window next")
     la, ms, pts = W.kernel_time(K.engine.TIME_BSGS)
     my_pts_s = args.steps * B * info.cycles * 1024 / (recs[-1][0] - t0)
@@ -563,7 +581,8 @@ def bsgs_leg(D: Dist, W: Walks, args, clock):
     ms_launch = chip_ms_per_launch(S, ms, la, t1 - t0)
     bpp = ALGO_BYTES_PER_GIANT_POINT[info.layer1_layout]
     kname = WALK_KERNEL[info.layer1_layout]
-    roof = walk_roofline(kname, pts_launch, ms_launch, bpp, la, walks=S, event_ms=ms / la)
+    roof = walk_roofline(kname, pts_launch, ms_launch, bpp, la, walks=S, event_ms=ms / la,
+                         clock_mhz=(board or {}).get("board_gfxclk_mhz"))
     # the probe is one random 16-B load per giant point: its own ceiling is the chip's random-load
     # rate at this footprint (tools/ubench_random2.hip, profiles/r01l_random16B.txt: 24 GB, nt loads)
     rand = {"achieved": pts_launch / (ms_launch / 1e3) / 1e9, "ceiling": RANDOM16_CEILING_GPS, "unit": "G loads/s",
@@ -581,7 +600,7 @@ def bsgs_leg(D: Dist, W: Walks, args, clock):
         "candidates": sum(e.bsgs_candidates() for e in W.engs),
         "info": info,
         "roofline": roof,
-        "sustained": quarters(t0, recs, B, two_n, clock),
+        "sustained": quarters(t0, recs, B, two_n, clock, board, my_pts_s),
         "known_answer": {"window": f"{ka_lo:x}:{ka_hi:x}", "expected": f"{ka_key:x}",
                          "found": [f"{k:x}" for _, k in ka_found], "match": [k for _, k in ka_found] == [ka_key]},
     }
@@ -606,42 +625,44 @@ def chip_ms_per_launch(walks: int, event_ms: float, launches: int, wall_s: float
 
 
 def walk_roofline(kname: str, pts_launch: float, ms_launch: float, algo_bytes_per_point: float, launches: int,
-                  walks: int = 1, event_ms: float | None = None) -> dict:
+                  walks: int = 1, event_ms: float | None = None, clock_mhz: float | None = None) -> dict:
     """The roofline object of one walk kernel (see the module docstring): VALU issue bound, with the
     HBM side alongside.  Counter-derived figures come from the newest profiles/r*_pmc_summary.json
     holding this kernel and are scaled to this run's points per launch.  ms_launch is the chip's time
     per launch (chip_ms_per_launch); with walks > 1 the overlapping launches' own event mean is
-    reported beside it (event_mean_launch_ms, which a rocprofv3 trace of the same run agrees with)."""
+    reported beside it (event_mean_launch_ms, which a rocprofv3 trace of the same run agrees with).
+    clock_mhz: the board's mean gfx clock over this leg's timed region, which frac_mix's ceiling uses."""
     d = pmc_entry(kname)
     secs = ms_launch / 1e3
     roof = {"bound": "valu", "achieved": None, "peak": VALU_PEAK_GIPS, "unit": "G VALU wave-instr/s", "frac": None,
-            "peak_hw": VALU_PEAK_HW_GIPS, "frac_hw": None, "frac_mix": None,
-            "traffic": None, "kernel": kname, "launches": launches, "mean_launch_ms": ms_launch,
+            "frac_mix": None, "traffic": None, "kernel": kname, "launches": launches, "mean_launch_ms": ms_launch,
             "walks_in_flight": walks, "event_mean_launch_ms": event_ms if event_ms is not None else ms_launch,
             "points_per_launch": pts_launch, "source": d.get("source")}
     if "valu_wave_instructions_per_dispatch" in d:
         wipp = d["valu_wave_instructions_per_dispatch"] / d["points_per_dispatch"]
         a = wipp * pts_launch / secs / 1e9
-        roof.update(achieved=a, frac=a / VALU_PEAK_GIPS, frac_hw=a / VALU_PEAK_HW_GIPS,
+        roof.update(achieved=a, frac=a / VALU_PEAK_GIPS,
                     valu_wave_instructions_per_point=wipp, valu_lane_instructions_per_point=wipp * 64)
         if d.get("valu_issue_frac"):
-            # the profiled dispatch's issue-slot occupancy, in cycles (clock-free; DVFS moves the
-            # clock between runs, so frac above is at the nominal 2.4 GHz)
-            roof.update(pmc_valu_issue_frac=d["valu_issue_frac"], pmc_clock_ghz=d["effective_clock_ghz"])
+            # the profiled dispatch's issue-slot occupancy at 4 cycles per instruction (clock-free)
+            roof.update(pmc_valu_issue_frac_4cyc=d["valu_issue_frac"], pmc_clock_ghz=d["effective_clock_ghz"])
         for key in ("valu_dual_issue_frac", "wave_time_split", "valu_thread_cycles_per_instruction"):
             if key in d:
                 roof["pmc_" + key] = d[key]
     mix = _valu_mix(kname)
-    if mix.get("simd_cycles_per_point"):
-        # class-weighted ceiling: points/s if every SIMD issued this kernel's instruction mix back to
-        # back at the measured class costs (s_nop included), at 2.4 GHz and at the profiled clock
-        cyc = mix["simd_cycles_per_point"]
-        ceil_pts = SIMDS * NOMINAL_GHZ * 1e9 / cyc
+    if mix.get("simd_cycles_per_point_floor"):
+        # the kernel's own ceiling: its instruction mix per point at the hardware's issue floor (2 / 4
+        # cycles per full- / half-rate wave64 instruction, s_nop at its in-situ cost, dual-issued
+        # instructions free: tools/valu_mix.py), on every SIMD back to back, at the clock the board
+        # reported over this leg (2.4 GHz if none) -- no order of these instructions issues faster
+        cyc = mix["simd_cycles_per_point_floor"]
+        ghz = clock_mhz / 1e3 if clock_mhz else NOMINAL_GHZ
+        ceil_pts = SIMDS * ghz * 1e9 / cyc
         got_pts = pts_launch / secs
-        roof.update(frac_mix=got_pts / ceil_pts, mix_simd_cycles_per_point=cyc,
-                    mix_ceiling_points_per_s=ceil_pts, mix_source=mix["source"])
-        if roof.get("pmc_clock_ghz"):
-            roof["frac_mix_clock"] = got_pts / (SIMDS * roof["pmc_clock_ghz"] * 1e9 / cyc)
+        roof.update(frac_mix=got_pts / ceil_pts, mix_floor_simd_cycles_per_point=cyc, mix_clock_ghz=ghz,
+                    mix_clock_source="board gfx clock over the timed region" if clock_mhz else "nominal",
+                    mix_ceiling_points_per_s=ceil_pts, mix_source=mix["source"],
+                    mix_measured_cost_simd_cycles_per_point=mix.get("simd_cycles_per_point"))
     hbm = {"achieved": pts_launch * algo_bytes_per_point / secs / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "algorithmic_bytes_per_point": algo_bytes_per_point}
     hbm["frac"] = hbm["achieved"] / HBM_PEAK_GBS
@@ -695,7 +716,7 @@ def address_leg(D: Dist, W: Walks, args, clock, mode: int, kname: str, keys_per_
         run(S)
         last = time.perf_counter() - t
     C = int(D.max(batch_for(args.seconds_secondary, args.steps_rmd, last / S, S, S) if args.warmup_rmd else S))
-    T, t0, t1, recs = timed(D, W, args.steps_rmd, lambda s: run(C), C, kind, clock)
+    T, t0, t1, recs, board = timed(D, W, args.steps_rmd, lambda s: run(C), C, kind, clock)
     la, ms, pts = W.kernel_time(kind)
     ka_lo, ka_n, ka_key = ka
     ka_hits = W.engs[0].scan(ka_lo, ka_n, mode, K.KH_SEARCH_COMPRESS)
@@ -704,8 +725,10 @@ def address_leg(D: Dist, W: Walks, args, clock, mode: int, kname: str, keys_per_
     return {"value": keys / T / 1e6, "ms_per_step": T / args.steps_rmd * 1e3, "seconds_timed": T,
             "chunks_per_step": C, "steps": args.steps_rmd,
             "points_per_s_in_kernel": pts / (ms_launch * la / 1e3),
-            "roofline": walk_roofline(kname, pts / la, ms_launch, 0, la, walks=S, event_ms=ms / la),
-            "sustained": quarters(t0, recs, C, CHUNK * keys_per_point, clock),
+            "roofline": walk_roofline(kname, pts / la, ms_launch, 0, la, walks=S, event_ms=ms / la,
+                                      clock_mhz=(board or {}).get("board_gfxclk_mhz")),
+            "sustained": quarters(t0, recs, C, CHUNK * keys_per_point, clock, board,
+                                  args.steps_rmd * C * CHUNK / (recs[-1][0] - t0)),
             "known_answer": {"window": f"{ka_lo:x}:{ka_lo + ka_n - 1:x}", "expected": f"{ka_key:x}",
                              "found": [f"{h.key:x}" for h in ka_hits], "match": [h.key for h in ka_hits] == [ka_key]}}
 
@@ -725,10 +748,9 @@ def xpoint_leg(D: Dist, W: Walks, args, clock):
 
 
 def cpu_host() -> dict:
-    """The host the CPU baseline ran on: model and CPU count (lscpu), the CPUs this process may use,
-    and the threads the baseline used.  On the pool's GPU boxes a one-GPU job's CPU share is 16
-    threads (OMP_NUM_THREADS, set by the box) of a much larger machine, so the baseline uses that
-    share; `per_thread` values let the reader scale it to any core count."""
+    """The host the CPU baseline ran on (lscpu): model, sockets, physical cores and threads per core,
+    and the logical CPUs this process may use.  On the pool's GPU boxes a one-GPU job's CPU share is 16
+    logical CPUs (OMP_NUM_THREADS, set by the box) of a much larger machine."""
     info = {"machine_cpus": os.cpu_count()}
     try:
         out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
@@ -737,13 +759,18 @@ def cpu_host() -> dict:
             m = re.search(rf"^{re.escape(key)}:\s*(.+)$", out, re.M)
             if m:
                 info[name] = m.group(1).strip()
+        if str(info.get("sockets", "")).isdigit() and str(info.get("cores_per_socket", "")).isdigit():
+            info["physical_cores"] = int(info["sockets"]) * int(info["cores_per_socket"])
     except Exception:
         pass
     try:
         info["affinity_cpus"] = len(os.sched_getaffinity(0))
     except Exception:
         info["affinity_cpus"] = os.cpu_count()
-    info["threads_used"] = cpu_threads()
+    tpc = info.get("threads_per_core")
+    if str(tpc).isdigit() and int(tpc) > 1:
+        info["job_share"] = (f"{cpu_threads()} logical CPUs = {cpu_threads() // int(tpc)} physical cores at "
+                             f"{tpc} threads per core (if the share takes whole cores)")
     return info
 
 
@@ -765,85 +792,119 @@ REF_BIN = next((p for p in (os.path.join(REPO, "oracle", "_ref", b) for b in ("k
 REF_FLAGS = os.path.join(REPO, "oracle", "_ref", "build_flags.txt")
 
 
-def run_reference(argv: list[str], files: list[str], seconds: float, setup=None):
-    """Run the reference CLI (oracle/_ref/keyhunt, built from /root/reference's sources by
-    oracle/Makefile.ref) in a scratch directory under /tmp for `seconds` after its tables are ready,
-    with every thread of the job's CPU share, and parse its own last stats line
-    ("Total N keys in S seconds", keyhunt.cpp:2906-2946).  `setup(dir)` may write table files first."""
+def run_reference_once(argv: list[str], td: str, threads: int, seconds: float) -> tuple[int, int] | None:
+    """One run of the reference CLI in `td` with `threads` threads until its own stats line covers
+    `seconds` (its clock starts once its tables are ready): (keys, seconds) of the last such line
+    ("Total N keys in S seconds", keyhunt.cpp:2906-2946), keys counted as the reference counts them."""
+    cmd = [REF_BIN] + argv + ["-t", str(threads), "-s", "5", "-q"]
+    p = subprocess.Popen(cmd, cwd=td, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL)
+    out = b""
+    t0 = time.time()
+    os.set_blocking(p.stdout.fileno(), False)
+    last = None
+    tick = t0
+    while time.time() - t0 < seconds + 120:
+        time.sleep(0.5)
+        if time.time() - tick >= 30:
+            tick = time.time()
+            progress(f"CPU baseline running ({tick - t0:.0f} s, -t {threads})")
+        try:
+            chunk = p.stdout.read()
+        except Exception:
+            chunk = None
+        if chunk:
+            out += chunk
+        rates = re.findall(rb"Total (\d+) keys in (\d+) seconds", out)
+        if rates:
+            last = tuple(map(int, rates[-1]))
+            if last[1] >= seconds:
+                break
+        if p.poll() is not None:
+            break
+    if p.poll() is None:
+        p.terminate()
+        try:
+            p.wait(timeout=10)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.wait()
+    return last if last and last[1] else None
+
+
+def run_reference(argv: list[str], files: list[str], seconds: float, setup=None, per_core_seconds: float | None = None):
+    """The reference CLI (built from /root/reference's sources by oracle/Makefile.ref) on this leg's
+    workload in a scratch directory under /tmp: once with every thread of the job's CPU share (the
+    baseline's value) and once with -t 1 (its per-core rate), each for `seconds` of its own stats
+    clock.  `setup(dir)` may write table files first."""
     if not os.path.exists(REF_BIN):
         return None
     thr = cpu_threads()
+    pcs = seconds if per_core_seconds is None else per_core_seconds
     with tempfile.TemporaryDirectory(dir="/tmp") as td:
         for f in files:
             shutil.copy(os.path.join(REPO, "tests", "golden", "data", f), td)
         if setup:
             progress("CPU baseline: writing the tables for the reference")
             setup(td)
-        progress(f"CPU baseline: oracle/_ref/{os.path.basename(REF_BIN)} {' '.join(argv)}")
-        cmd = [REF_BIN] + argv + ["-t", str(thr), "-s", "5", "-q"]
-        p = subprocess.Popen(cmd, cwd=td, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL)
-        out = b""
-        t0 = time.time()
-        os.set_blocking(p.stdout.fileno(), False)
-        last = None
-        tick = t0
-        while time.time() - t0 < seconds + 120:
-            time.sleep(0.5)
-            if time.time() - tick >= 60:
-                tick = time.time()
-                progress(f"CPU baseline running ({tick - t0:.0f} s)")
-            try:
-                chunk = p.stdout.read()
-            except Exception:
-                chunk = None
-            if chunk:
-                out += chunk
-            rates = re.findall(rb"Total (\d+) keys in (\d+) seconds", out)
-            if rates:
-                last = tuple(map(int, rates[-1]))
-                if last[1] >= seconds:
-                    break
-            if p.poll() is not None:
-                break
-        if p.poll() is None:
-            p.terminate()
-            try:
-                p.wait(timeout=10)
-            except subprocess.TimeoutExpired:
-                p.kill()
-                p.wait()
-    if not last or last[1] == 0:
+        progress(f"CPU baseline: oracle/_ref/{os.path.basename(REF_BIN)} {' '.join(argv)} -t {thr}, then -t 1")
+        many = run_reference_once(argv, td, thr, seconds)
+        one = run_reference_once(argv, td, 1, pcs) if pcs > 0 else None
+    if not many:
         return None
-    keys, secs = last
     host = cpu_host()
-    per_thread = keys / secs / 1e6 / thr
     flags = (open(REF_FLAGS).read().strip() if os.path.exists(REF_FLAGS) and REF_BIN.endswith("_fast")
              else "oracle/_ref/keyhunt: g++ -m64 -march=x86-64-v3 -mssse3 -O3 (the fixtures' build)")
-    return {"value": keys / secs / 1e6, "unit": "Mkeys/s", "cores": thr, "kind": "reference",
-            "per_thread": per_thread, "host": host, "build_flags": flags,
-            "all_cpus": {"value": per_thread * (host.get("machine_cpus") or thr), "cpus": host.get("machine_cpus"),
-                         "how": "per-thread rate of this run x every CPU of the host (extrapolated: the job's share "
-                                "of the box is its GPU's 16 CPUs, so the other CPUs are not used)"},
-            "sample": f"oracle/_ref/{os.path.basename(REF_BIN)} {' '.join(argv)} -t {thr}: {keys} keys in {secs} s (the reference's "
-                      f"own stats line, keys counted as it counts them)"}
+    name = f"oracle/_ref/{os.path.basename(REF_BIN)} {' '.join(argv)}"
+    out = {"value": many[0] / many[1] / 1e6, "unit": "Mkeys/s", "cores": thr, "kind": "reference",
+           "threads": {"value": many[0] / many[1] / 1e6, "threads": thr, "seconds": many[1], "keys": many[0],
+                       "measured": True},
+           "per_core": ({"value": one[0] / one[1] / 1e6, "threads": 1, "seconds": one[1], "keys": one[0],
+                         "measured": True} if one else None),
+           "host": host, "build_flags": flags,
+           "sample": f"{name} -t {thr}: {many[0]} keys in {many[1]} s" +
+                     (f"; -t 1: {one[0]} keys in {one[1]} s" if one else "") +
+                     " (the reference's own stats lines, keys counted as it counts them; 'cores' = logical CPUs used)"}
+    if one and host.get("physical_cores"):
+        # labelled estimate, not a measurement: the -t 1 rate times the host's physical cores
+        out["all_physical_cores_extrapolated"] = {"value": out["per_core"]["value"] * host["physical_cores"],
+                                                  "cores": host["physical_cores"], "measured": False}
+    return out
 
 
-def cpu_baseline_bsgs(eng, C: dict, seconds: float):
+def cpu_baseline_bsgs(eng, C: dict, seconds: float, per_core_seconds: float | None = None):
     """The reference's BSGS giant-step loop (thread_process_bsgs, keyhunt.cpp:4549-4888) on the host,
     on the same workload (-b bits -k K from 2^(bits-1)).  Its 120-s-per-core baby-step build is
     skipped: the engine writes the four -S table files (kh_bsgs_save: the reference's format, byte
     for byte, tests/test_gpu_tables.py) and the reference reads them (-S -6, keyhunt.cpp:1983-2240)."""
     pub = {125: "125.txt", 130: "130.txt"}[C["bits"]]
     return run_reference(["-m", "bsgs", "-f", pub, "-b", str(C["bits"]), "-k", str(C["k"]), "-S", "-6"], [pub],
-                         seconds, setup=lambda d: eng.bsgs_save(d))
+                         seconds, setup=lambda d: eng.bsgs_save(d), per_core_seconds=per_core_seconds)
 
 
-def cpu_baseline_rmd160(seconds: float):
-    return run_reference(["-m", "rmd160", "-f", "66.rmd", "-b", "66", "-l", "compress"], ["66.rmd"], seconds)
+def cpu_baseline_rmd160(seconds: float, per_core_seconds: float | None = None):
+    return run_reference(["-m", "rmd160", "-f", "66.rmd", "-b", "66", "-l", "compress"], ["66.rmd"], seconds,
+                         per_core_seconds=per_core_seconds)
 
 
-def cpu_baseline_xpoint(seconds: float):
-    return run_reference(["-m", "xpoint", "-f", "63.pub", "-b", "63"], ["63.pub"], seconds)
+def cpu_baseline_xpoint(seconds: float, per_core_seconds: float | None = None):
+    return run_reference(["-m", "xpoint", "-f", "63.pub", "-b", "63"], ["63.pub"], seconds,
+                         per_core_seconds=per_core_seconds)
+
+
+def long_cpu_baseline() -> dict | None:
+    """The newest profiles/r*_cpu_baseline_*.json (bench.py --cpu-only --cpu-seconds 60 on a GPU box):
+    the reference's rates over >= 60 s of its own clock, at the job's threads and at -t 1 (SURVEY.md
+    8d), quoted beside this run's shorter samples; their per-leg objects, without the host block."""
+    import glob
+    fs = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_cpu_baseline_*.json")), reverse=True)
+    if not fs:
+        return None
+    d = json.load(open(fs[0]))
+    out = {"source": os.path.relpath(fs[0], REPO)}
+    for k in ("bsgs", "rmd160", "xpoint"):
+        if d.get(k):
+            out[k] = {kk: d[k].get(kk) for kk in ("threads", "per_core", "sample")}
+    return out
 
 
 def main():
@@ -872,7 +933,11 @@ def main():
                     help="the same for each address-family leg (0: one 2^32-key chunk per step)")
     ap.add_argument("--steps-rmd", type=int, default=None)
     ap.add_argument("--warmup-rmd", type=int, default=None)
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-seconds", type=float, default=20.0,
+                    help="CPU baseline: seconds of the reference's own stats clock per run (threads run, then -t 1)")
+    ap.add_argument("--cpu-only", action="store_true",
+                    help="only the CPU baselines of the three legs (the BSGS one still needs the GPU to write the "
+                         "-S tables); prints one JSON object")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--rehearse", action="store_true",
@@ -893,14 +958,25 @@ def main():
     dev = device_plan(D.world, D.local, D.local_world, K.device_count(), args.rehearse)
     W = Walks(K, dev, max(args.walks, 1 if args.no_secondary else args.walks_secondary))
     bdf = pci_bus_id(dev)
-    clock = ClockSampler(bdf).start()
+    clock = BoardSampler(bdf).start()
+    if args.cpu_only:  # the reference's rates alone (profiles/r04*_cpu_baseline_*.json)
+        C = BSGS_CONFIGS[args.config]
+        W.engs[0].bsgs_setup(1 << 44, C["k"], layer1=args.layer1)
+        W.engs[0].bsgs_build()
+        res = {"bsgs": cpu_baseline_bsgs(W.engs[0], C, args.cpu_seconds),
+               "rmd160": cpu_baseline_rmd160(args.cpu_seconds), "xpoint": cpu_baseline_xpoint(args.cpu_seconds),
+               "cpu_seconds": args.cpu_seconds, "workload": C["workload"]}
+        W.close()
+        json_out.write(json.dumps(res) + "\n")
+        json_out.flush()
+        return
     prim = bsgs_leg(D, W.head(args.walks), args, clock)
     Wa = W.head(args.walks_secondary)
     sec = None if args.no_secondary else rmd160_leg(D, Wa, args, clock)
     ter = None if args.no_secondary else xpoint_leg(D, Wa, args, clock)
     clock.stop()
     cpu_b = cpu_r = cpu_x = None
-    if D.rank == 0 and D.world == 1 and not args.no_cpu_baseline:
+    if D.rank == 0 and D.world == 1 and not args.no_cpu_baseline and not args.cpu_only:
         cpu_b = cpu_baseline_bsgs(W.engs[0], BSGS_CONFIGS[args.config], args.cpu_seconds)
         if not args.no_secondary:
             cpu_r = cpu_baseline_rmd160(args.cpu_seconds)
@@ -937,8 +1013,7 @@ def main():
             "sustained": prim["sustained"],
             "roofline": prim["roofline"],
             "random_access": prim["random_access"],
-            "clock_sampler": {"source": "amdsmi gfx clock of the rank-0 device", "samples": len(clock.samples),
-                              "error": clock.error},
+            "board_sampler": dict(clock.info(), source="amdsmi gpu_metrics / energy counter of the rank-0 device"),
             "cpu_baseline": cpu_b,
         }
         for key, leg, wl in (("secondary", sec, "-m rmd160 -f tests/66.rmd -b 66 -l compress"),
@@ -951,6 +1026,14 @@ def main():
                              "known_answer": leg["known_answer"], "sustained": leg["sustained"],
                              "roofline": leg["roofline"],
                              "cpu_baseline": cpu_r if key == "secondary" else cpu_x}
+        long_cpu = long_cpu_baseline()
+        if long_cpu:
+            for k, leg in (("cpu_baseline", line), ("secondary", line.get("secondary")), ("tertiary", line.get("tertiary"))):
+                tgt = leg if k == "cpu_baseline" else (leg or {})
+                cb = tgt.get("cpu_baseline")
+                key = {"cpu_baseline": "bsgs", "secondary": "rmd160", "tertiary": "xpoint"}[k]
+                if cb is not None and long_cpu.get(key):
+                    cb["long_sample"] = dict(long_cpu[key], source=long_cpu["source"])
         json_out.write(json.dumps(line) + "\n")
         json_out.flush()
     D.close()

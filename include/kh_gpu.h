@@ -152,8 +152,10 @@ int kh_set_rmd_batch(kh_ctx *ctx, uint32_t group);
 int kh_bsgs_set_layer1(kh_ctx *ctx, uint32_t layout);
 int kh_bsgs_setup(kh_ctx *ctx, uint64_t n, uint64_t k, kh_bsgs_info *info);
 /* after kh_bsgs_setup: the device bytes this context holds once its tables are built and it scans
- * (the three layers, the bP rows, the inversion pad of the giant walk, lane state), and how many of
- * them it holds already */
+ * (the three layers, the bP rows, the inversion pad of the giant walk, lane state, candidate buffers
+ * at their current size, a kh_bsgs_scan_list of up to 2^16 bases), and how many of them it holds
+ * already.  A lower bound: longer lists (32 B per base) and candidate buffers grown on overflow come
+ * on top */
 int kh_bsgs_memory(kh_ctx *ctx, uint64_t *needed_bytes, uint64_t *held_bytes);
 int kh_bsgs_build(kh_ctx *ctx);                  /* baby-step blooms + sorted bP table on the GPU */
 /* -S table files in the reference's formats (keyhunt.cpp:2504-2652 write, 1983-2230 read), in dir

@@ -1226,10 +1226,14 @@ int kh_bsgs_memory(kh_ctx *ctx, uint64_t *needed_bytes, uint64_t *held_bytes) {
   uint64_t layers = 0;
   for (int l = 0; l < 3; l++) layers += 256 * ctx->bd[l].stride + 4;
   const uint64_t L = ctx->lanes_max;
-  // the giant walk's pad (L x KH_WALK_HB entries of 32 B), lane centres and scalars, the comb,
-  // candidate buffers, and the build's transient row keys (m3 x 12 B)
+  // the giant walk's pad (L x KH_WALK_HB entries of 32 B), lane centres and scalars, the comb, the two
+  // rounds' candidate buffers at their current size (16 B per entry, plus the first list's copy), the
+  // base list of a kh_bsgs_scan_list call of up to 2^16 bases (32 B each: bsgsd's batch; a longer
+  // list adds 32 B per base), and the build's transient row keys (m3 x 12 B).  A round whose
+  // candidates overflow doubles its buffers on demand (up to 2^28 entries), which this figure cannot
+  // foresee.
   const uint64_t walk = L * (uint64_t)KH_WALK_HB * 32 + L * 32 * 3 + (512u << 10) + 4ull * ctx->cand_cap * 16 +
-                        ctx->info.m3 * 12;
+                        (1ull << 16) * 32 + ctx->info.m3 * 12;
   if (needed_bytes) *needed_bytes = layers + walk;
   if (held_bytes)
     *held_bytes = layers + (uint64_t)ctx->lanes_alloc * ctx->scratch_h * 32 + (uint64_t)ctx->lanes_alloc * 32 * 3;

@@ -651,6 +651,12 @@ int main(int argc, char **argv) {
     }
     if (!r && d == 0) {
       r = first_tables(g, ptable_rows, present);
+    } else if (!r && opt.mapped) {
+      // --mapped skips the -S files (bsgsd.cpp:1465, 1991): the first context built its tables and
+      // the shard files; the others build theirs too rather than read any -S file left in the
+      // directory by an earlier run
+      r = kh_bsgs_build(g.ctx);
+      if (!r && opt.load_ptable) r = kh_bsgs_set_table(g.ctx, ptable_rows.data(), g.info.m3);
     } else if (!r) {  // the first context left the four files (or the --ptable rows) for the others
       r = kh_bsgs_load(g.ctx, ".", opt.skip_checksum ? KH_LOAD_SKIP_CHECKSUM : 0);
       if (r == KH_E_IO) r = kh_bsgs_build(g.ctx);  // --load-ptable without a .tbl

@@ -184,6 +184,61 @@ __global__ __launch_bounds__(256) void k_pat(stamp *out, uint32_t seed) {
                    : "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s53",
                      "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71", "s72", "s73",
                      "s74", "s75", "s76", "s77", "s78", "s79", "s80", "s81", "s82", "s83", "s84", "s85", "scc");
+    // --- round 4: rotate encodings for the hash walks (SHA-256 / RIPEMD-160) and mixed-rate streams
+    if (P == 29)  // byte-multiple rotates: v_alignbyte_b32
+      asm volatile(R8("v_alignbyte_b32 %0, %0, %0, 1\n v_alignbyte_b32 %1, %1, %1, 1\n v_alignbyte_b32 %2, %2, %2, 1\n"
+                      "v_alignbyte_b32 %3, %3, %3, 1\n")
+                   : "+v"(u0), "+v"(u1), "+v"(u2), "+v"(u3));
+    if (P == 30)  // shift-or fused: (x << n) | y
+      asm volatile(R8("v_lshl_or_b32 %0, %0, 7, %1\n v_lshl_or_b32 %1, %1, 7, %2\n v_lshl_or_b32 %2, %2, 7, %3\n"
+                      "v_lshl_or_b32 %3, %3, 7, %0\n")
+                   : "+v"(u0), "+v"(u1), "+v"(u2), "+v"(u3));
+    if (P == 31)  // a rotate as a shift pair: t = x >> 25; r = (x << 7) | t  (16 rotates per trip)
+      asm volatile(R4("v_lshrrev_b32 %4, 25, %0\n v_lshrrev_b32 %5, 25, %1\n v_lshl_or_b32 %0, %0, 7, %4\n"
+                      "v_lshl_or_b32 %1, %1, 7, %5\n v_lshrrev_b32 %4, 25, %2\n v_lshrrev_b32 %5, 25, %3\n"
+                      "v_lshl_or_b32 %2, %2, 7, %4\n v_lshl_or_b32 %3, %3, 7, %5\n")
+                   : "+v"(u0), "+v"(u1), "+v"(u2), "+v"(u3), "=&v"(a), "=&v"(b));
+    if (P == 32)
+      asm volatile(R8("v_or3_b32 %0, %0, %4, %1\n v_or3_b32 %1, %1, %4, %2\n v_or3_b32 %2, %2, %4, %3\n"
+                      "v_or3_b32 %3, %3, %4, %0\n")
+                   : "+v"(u0), "+v"(u1), "+v"(u2), "+v"(u3) : "v"(a));
+    if (P == 33)
+      asm volatile(R8("v_xad_u32 %0, %0, %4, %1\n v_xad_u32 %1, %1, %4, %2\n v_xad_u32 %2, %2, %4, %3\n"
+                      "v_xad_u32 %3, %3, %4, %0\n")
+                   : "+v"(u0), "+v"(u1), "+v"(u2), "+v"(u3) : "v"(a));
+    if (P == 34)  // 16 alignbit + 16 v_add_u32, interleaved: does a full-rate op fill a half-rate op's slot?
+      asm volatile(R8("v_alignbit_b32 %0, %0, %0, 7\n v_add_u32 %1, %1, %4\n v_alignbit_b32 %2, %2, %2, 7\n"
+                      "v_add_u32 %3, %3, %4\n")
+                   : "+v"(u0), "+v"(u1), "+v"(u2), "+v"(u3) : "v"(a));
+    if (P == 35)  // 16 alignbit + 16 bitop3, interleaved
+      asm volatile(R8("v_alignbit_b32 %0, %0, %0, 7\n v_bitop3_b32 %1, %1, %4, %3 bitop3:0x96\n"
+                      "v_alignbit_b32 %2, %2, %2, 7\n v_bitop3_b32 %3, %3, %4, %1 bitop3:0x96\n")
+                   : "+v"(u0), "+v"(u1), "+v"(u2), "+v"(u3) : "v"(a));
+    if (P == 36)
+      asm volatile(R8("v_lshl_add_u32 %0, %0, 3, %1\n v_lshl_add_u32 %1, %1, 3, %2\n v_lshl_add_u32 %2, %2, 3, %3\n"
+                      "v_lshl_add_u32 %3, %3, 3, %0\n")
+                   : "+v"(u0), "+v"(u1), "+v"(u2), "+v"(u3));
+    if (P == 37)  // 16 add3 + 16 bitop3, interleaved
+      asm volatile(R8("v_add3_u32 %0, %0, %4, %1\n v_bitop3_b32 %1, %1, %4, %3 bitop3:0x96\n"
+                      "v_add3_u32 %2, %2, %4, %3\n v_bitop3_b32 %3, %3, %4, %0 bitop3:0x96\n")
+                   : "+v"(u0), "+v"(u1), "+v"(u2), "+v"(u3) : "v"(a));
+    if (P == 38)  // 16 mads + 16 bitop3, interleaved (the field math beside logic)
+      asm volatile(R8("v_mad_u64_u32 %0, %4, %5, %6, %0\n v_bitop3_b32 %7, %7, %5, %8 bitop3:0x96\n"
+                      "v_mad_u64_u32 %1, %4, %5, %6, %1\n v_bitop3_b32 %8, %8, %6, %7 bitop3:0x96\n")
+                   : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3), "=s"(s0), "+v"(a), "+v"(b), "+v"(u0), "+v"(u1));
+    if (P == 39)  // 16 add_u32 + 16 v_add_u32 writing... two full-rate streams (control for 34/35)
+      asm volatile(R8("v_add_u32 %0, %0, %4\n v_xor_b32 %1, %1, %4\n v_add_u32 %2, %2, %4\n v_xor_b32 %3, %3, %4\n")
+                   : "+v"(u0), "+v"(u1), "+v"(u2), "+v"(u3) : "v"(a));
+    if (P == 40)  // rotate by 16 with SDWA word selects: t = x << 16 (dst WORD_1), r = (x >> 16) | t
+      asm volatile(R4("v_mov_b32_sdwa %4, %0 dst_sel:WORD_1 dst_unused:UNUSED_PAD src0_sel:WORD_0\n"
+                      "v_mov_b32_sdwa %5, %1 dst_sel:WORD_1 dst_unused:UNUSED_PAD src0_sel:WORD_0\n"
+                      "v_or_b32_sdwa %0, %0, %4 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD\n"
+                      "v_or_b32_sdwa %1, %1, %5 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD\n"
+                      "v_mov_b32_sdwa %4, %2 dst_sel:WORD_1 dst_unused:UNUSED_PAD src0_sel:WORD_0\n"
+                      "v_mov_b32_sdwa %5, %3 dst_sel:WORD_1 dst_unused:UNUSED_PAD src0_sel:WORD_0\n"
+                      "v_or_b32_sdwa %2, %2, %4 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD\n"
+                      "v_or_b32_sdwa %3, %3, %5 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD\n")
+                   : "+v"(u0), "+v"(u1), "+v"(u2), "+v"(u3), "=&v"(a), "=&v"(b));
     if (P == 24)  // 16 mads + 16 v_mov (the product-scanning column shift), interleaved
       asm volatile(R8("v_mad_u64_u32 %0, %4, %5, %6, %0\n v_mov_b32 %7, %5\n v_mad_u64_u32 %1, %4, %5, %6, %1\n"
                       "v_mov_b32 %8, %6\n")
@@ -204,7 +259,8 @@ typedef void (*kfn)(stamp *, uint32_t);
 #define K(n) k_pat<n>
 static const kfn kernels[] = {K(0),  K(1),  K(2),  K(3),  K(4),  K(5),  K(6),  K(7),  K(8),  K(9),  K(10), K(11), K(12),
                               K(13), K(14), K(15), K(16), K(17), K(18), K(19), K(20), K(21), K(22), K(23), K(24),
-                              K(25), K(26), K(27), K(28)};
+                              K(25), K(26), K(27), K(28), K(29), K(30), K(31), K(32), K(33), K(34), K(35), K(36),
+                              K(37), K(38), K(39), K(40)};
 static const char *names[] = {
     "mad_u64_u32 acc, 4 chains",      "mad,nop,addc,nop (as hipcc)",  "mad+addc, hazards scheduled", "addc_e32 vcc chain + s_nop 1",
     "add_co/addc, 4 sgpr chains",     "v_mov_b32",                    "v_add_u32",                   "v_and_b32",
@@ -213,7 +269,10 @@ static const char *names[] = {
     "v_add_co_u32_e32 (vcc) indep",   "v_lshrrev_b64",                "v_lshl_add_u64",              "v_mov_b64",
     "v_mul_lo/hi_u32",                "s_nop 0 only",                 "v_add_u32 + s_nop 0",         "mad + s_nop 0 (no hazard)",
     "mad + v_mov interleaved",        "mad + SALU interleaved",       "SALU only (s_xor/and/or_b64)", "7-col: 7 addc (+2 add)",
-    "7-col: SALU count (+3 add)"};
+    "7-col: SALU count (+3 add)",     "v_alignbyte_b32",              "v_lshl_or_b32",               "rotate = lshrrev + lshl_or",
+    "v_or3_b32",                      "v_xad_u32 (xor-add)",                   "alignbit + v_add_u32 mix",    "alignbit + bitop3 mix",
+    "v_lshl_add_u32",                 "add3 + bitop3 mix",            "mad + bitop3 mix",            "v_add_u32 + v_xor_b32 mix",
+    "rot16 = 2 sdwa ops"};
 
 int main(int argc, char **argv) {
   // optional: the pattern numbers to run (default all)

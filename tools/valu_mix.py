@@ -26,6 +26,14 @@ rates: ~2.2 cycles (32-bit add / logic / shifts / v_mov_b32 / v_bitop3: a wave64
 ~4.2 (v_mad_u64_u32, every carry-in/out op, v_alignbit, v_add3, v_perm, packed 16-bit ops, compares,
 v_cndmask, 64-bit ALU ops, 32-bit multiplies); an s_nop stream issues at ~1.1 cycles per wait state.
 
+Floor (round 4; what bench.py's frac_mix divides by, so that it is a bound): every class at the
+hardware's own issue floor instead of its measured single-class cost -- 2 cycles for a full-rate
+wave64 instruction (MI355X_MICROARCH.md: 32 lanes per cycle), 4 for a half-rate one -- an s_nop wait
+state at its in-situ cost (ubench "mad,nop,addc,nop" against "mad+addc, hazards scheduled": the
+cycles the pads add when other waves issue beside them, ~0.3), and the share of VALU instructions
+the PMC saw dual-issued (SQ_ACTIVE_INST_VALU2 / SQ_INSTS_VALU) taken as free.  A kernel cannot issue
+its instructions faster than that at a given clock, whatever their order.
+
 usage: python tools/valu_mix.py LISTING.s PMC_SUMMARY.json OUT.json [COST.txt]
 """
 import json
@@ -98,6 +106,25 @@ def costs(path: str) -> dict:
     half = sorted(v for k, v in c.items() if k in ("mad64", "carry", "cmp", "alignbit", "add3", "perm", "alu64"))
     c["other"] = half[len(half) // 2]
     return c
+
+
+FULL_RATE = ("mov", "full", "bitop3")  # 2-cycle wave64 issue; every other VALU class is half rate
+
+
+def nop_in_situ(path: str) -> float:
+    """SIMD cycles an s_nop wait state adds between half-rate instructions at 4 waves/SIMD: 16 of the
+    32 instructions of "mad,nop,addc,nop" are pads, "mad+addc, hazards scheduled" has none."""
+    span = {}
+    for line in open(path):
+        m = re.match(r"^(.*?)\s+W1 span\s+([\d.]+).*W4 span\s+([\d.]+)", line)
+        if m:
+            span[m.group(1).strip()] = float(m.group(3))
+    padded, plain = span["mad,nop,addc,nop (as hipcc)"], span["mad+addc, hazards scheduled"]
+    return max(0.0, (32 * padded - 16 * plain) / 16)
+
+
+def floor_costs(classes, nop: float) -> dict:
+    return {k: (nop if k == "s_nop" else 2.0 if k in FULL_RATE else 4.0) for k in classes}
 
 
 def function(lines, sym):
@@ -222,6 +249,7 @@ def main():
     listing, pmc, out = sys.argv[1:4]
     cost_path = sys.argv[4] if len(sys.argv) > 4 else "profiles/r03e_ubench_cost.txt"
     cost = costs(cost_path)
+    nop = nop_in_situ(cost_path)
     pm = json.load(open(pmc))
     res = {}
     for name, (sym, ppl, fpt) in KERNELS.items():
@@ -238,18 +266,30 @@ def main():
                                       for k, v in sorted(pp.items(), key=lambda x: -x[1] * cost[x[0]])},
              "listing": listing, "costs": cost_path,
              "recompute": "simd_cycles_per_point = sum(lane_instructions_per_point[c] * class_cost_simd_cycles[c]) / 64 * pmc_over_static"}
+        fl = floor_costs(pp, nop)
+        cyc_floor = sum(v * fl[k] for k, v in pp.items()) / 64
+        e.update(class_floor_simd_cycles=fl, s_nop_in_situ_cycles=nop)
+        dual = 0.0
+        f = 1.0
         if name in pm and "valu_lane_instructions_per_point" in pm[name]:
             e["valu_per_point_pmc"] = pm[name]["valu_lane_instructions_per_point"]
             # scale the static mix to the measured dynamic VALU count (inversion, centre step)
             f = pm[name]["valu_lane_instructions_per_point"] / valu
             e["pmc_over_static"] = f
             e["simd_cycles_per_point"] = cyc * f
+            c = pm[name].get("counters_per_dispatch", {})
+            if c.get("SQ_ACTIVE_INST_VALU2") and c.get("SQ_INSTS_VALU"):
+                dual = c["SQ_ACTIVE_INST_VALU2"] / c["SQ_INSTS_VALU"]
+        e["dual_issue_share"] = dual
+        e["simd_cycles_per_point_floor"] = cyc_floor * f * (1 - dual)
+        e["recompute_floor"] = ("simd_cycles_per_point_floor = sum(lane_instructions_per_point[c] * "
+                                "class_floor_simd_cycles[c]) / 64 * pmc_over_static * (1 - dual_issue_share)")
         res[name] = e
     json.dump(res, open(out, "w"), indent=1)
     for k, e in res.items():
-        print(k, "static VALU/pt %.1f  PMC %.1f  s_nop states/pt %.1f  SIMD cycles/pt %.3f" % (
+        print(k, "static VALU/pt %.1f  PMC %.1f  s_nop states/pt %.1f  SIMD cycles/pt %.3f (floor %.3f)" % (
             e["valu_per_point_static"], e.get("valu_per_point_pmc", 0), e["s_nop_states_per_point"],
-            e["simd_cycles_per_point"]))
+            e["simd_cycles_per_point"], e["simd_cycles_per_point_floor"]))
         print("   ", e["simd_cycles_by_class"])
 
 
