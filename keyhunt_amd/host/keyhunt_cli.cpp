@@ -155,6 +155,8 @@ struct options {
   long double mapped_error = 0;  // mapped_error_override
   uint32_t mapped_chunks = 1;
   int rmd_batch = 1024;  // --rmd-batch-size (keyhunt.cpp:301, 815-829), -m rmd160 only
+  bool crypto_given = false;      // -c (FLAGCRYPTO set): no "Setting search for btc" line
+  std::string range_start_str, range_end_str;  // -r as typed (BSGS prints them so, keyhunt.cpp:1529-1531)
 } opt;
 // keyhunt.cpp:419; ggsb and angrygiant walk like sequential (ggsb with BSGS_STEP = 2 x block size)
 const char *BSGS_MODES[7] = {"sequential", "backward", "both", "random", "dance", "ggsb", "angrygiant"};
@@ -286,6 +288,16 @@ bool read_vanity(const char *fn) {
   return true;
 }
 
+// initBloomFilter's lines (keyhunt.cpp:7605-7626): the item count it was given and the size of the
+// filter it makes, bloom_init2(max(10000, items) (x -z above the floor), 1e-6).  The --mapped path
+// prints its own (kh_mapped.h).
+void print_bloom_init(uint64_t items) {
+  if (opt.mapped) return;
+  const uint64_t total = items <= 10000 ? 10000 : (uint64_t)opt.bloom_mult * items;
+  printf("[+] Bloom filter for %llu elements.\n", (unsigned long long)items);
+  printf("[+] Loading data to the bloomfilter total: %.2f MB\n", (double)mapped::bytes_for(total, 0.000001L) / 1048576.0);
+}
+
 // forceReadFileAddressEth (keyhunt.cpp:7312-7384): 40 hex digits, or 0x and 40 hex digits
 bool read_targets_eth(const char *fn, std::vector<uint8_t> &rows, uint64_t &bloom_items,
                       std::vector<uint8_t> *adds = nullptr) {
@@ -306,6 +318,7 @@ bool read_targets_eth(const char *fn, std::vector<uint8_t> &rows, uint64_t &bloo
   bloom_items = counted;
   printf("[+] Allocating memory for %llu elements: %.2f MB\n", (unsigned long long)counted,
          (double)(counted * 20) / 1048576.0);
+  print_bloom_init(counted);
   for (auto &ln : lines) {
     uint8_t raw[20];
     const size_t r = ln.size();
@@ -360,6 +373,7 @@ bool read_targets(const char *fn, int mode, std::vector<uint8_t> &rows, uint64_t
   bloom_items = counted;
   printf("[+] Allocating memory for %llu elements: %.2f MB\n", (unsigned long long)counted,
          (double)(counted * 20) / 1048576.0);
+  print_bloom_init(counted);
   uint8_t raw[100] = {0};
   size_t next = 0;
   if (xp) {
@@ -1196,7 +1210,7 @@ int main(int argc, char **argv) {
           return EXIT_FAILURE;
         }
         opt.mode = m;
-        printf("[+] Mode %s\n", optarg);
+        if (m != MODE_BSGS) printf("[+] Mode %s\n", optarg);  // BSGS: "[+] Mode BSGS <schedule>" later
         break;
       }
       case 'f': opt.file = optarg; break;
@@ -1211,9 +1225,10 @@ int main(int argc, char **argv) {
         }
         break;
       case 'l':
-        if (!strcmp(optarg, "compress")) opt.search = KH_SEARCH_COMPRESS;
-        else if (!strcmp(optarg, "uncompress")) opt.search = KH_SEARCH_UNCOMPRESS;
-        else if (!strcmp(optarg, "both")) opt.search = KH_SEARCH_BOTH;
+        // keyhunt.cpp:945-960
+        if (!strcmp(optarg, "compress")) { opt.search = KH_SEARCH_COMPRESS; printf("[+] Search compress only\n"); }
+        else if (!strcmp(optarg, "uncompress")) { opt.search = KH_SEARCH_UNCOMPRESS; printf("[+] Search uncompress only\n"); }
+        else if (!strcmp(optarg, "both")) { opt.search = KH_SEARCH_BOTH; printf("[+] Search both compress and uncompress\n"); }
         else { fprintf(stderr, "[E] Unknow search type %s\n", optarg); return EXIT_FAILURE; }
         break;
       case 'r': {  // keyhunt.cpp:1024-1055: START[:END]; START alone runs to the group order
@@ -1227,6 +1242,8 @@ int main(int argc, char **argv) {
           fprintf(stderr, "[E] Invalid hexstring : %s\n", b.c_str());
         } else {
           opt.have_range = true;
+          opt.range_start_str = a;
+          opt.range_end_str = p == std::string::npos ? std::string() : b;  // empty: the order
         }
         break;
       }
@@ -1240,10 +1257,22 @@ int main(int argc, char **argv) {
         break;
       case 'k': opt.kfactor = strtoull(optarg, nullptr, 10); if (!opt.kfactor) opt.kfactor = 1; printf("[+] K factor %llu\n", (unsigned long long)opt.kfactor); break;
       case 'n': opt.flag_n = true; opt.str_n = optarg; break;
-      case 't': break;  // host threads: one per GPU here (see -g)
+      case 't': {  // host threads: one per GPU context here (see -g); echoed as keyhunt.cpp:1076-1082 does
+        long t = strtol(optarg, NULL, 10);
+        if (t <= 0) t = 1;
+        printf(t > 1 ? "[+] Threads : %u\n" : "[+] Thread : %u\n", (unsigned)t);
+        break;
+      }
       case 'g': opt.gpus = atoi(optarg); break;
       case 'q': opt.quiet = true; printf("[+] Quiet thread output\n"); break;
-      case 's': opt.seconds = atoi(optarg); break;
+      case 's':  // keyhunt.cpp:1059-1072
+        opt.seconds = atoi(optarg);
+        if (opt.seconds < 0) opt.seconds = 30;
+        if (opt.seconds == 0)
+          printf("[+] Turn off stats output\n");
+        else
+          printf("[+] Stats output every %d seconds\n", opt.seconds);
+        break;
       case 'I': {
         U s;
         bool ok = (optarg[0] == '0' && optarg[1] == 'x') ? u_from_hex(optarg, s) : u_from_dec(optarg, s);
@@ -1252,7 +1281,7 @@ int main(int argc, char **argv) {
         opt.stride_set = true;
         break;
       }
-      case 'M': opt.matrix = true; break;
+      case 'M': opt.matrix = true; printf("[+] Matrix screen\n"); break;  // keyhunt.cpp:960-963
       case 'L':  // BSGS layer-1 layout on the GPU (engine option; the reference has one layout)
         if (!strcmp(optarg, "reference")) opt.layer1 = KH_LAYER1_REFERENCE;
         else if (!strcmp(optarg, "blocked")) opt.layer1 = KH_LAYER1_BLOCKED;
@@ -1285,6 +1314,7 @@ int main(int argc, char **argv) {
         fprintf(stderr, "[W] Skipping checksums on files\n");
         break;
       case 'c':  // keyhunt.cpp:874-891
+        opt.crypto_given = true;
         if (!strcmp(optarg, "btc")) {
           opt.eth = false;
         } else if (!strcmp(optarg, "eth")) {
@@ -1320,7 +1350,6 @@ int main(int argc, char **argv) {
   mapped::cfg.error = opt.mapped_error;
   mapped::cfg.bloom_mult = opt.bloom_mult;
   if (opt.create_mapped) return mapped::create();  // keyhunt.cpp:1131-1172: make the file(s) and exit
-  if (opt.mode == MODE_BSGS) printf("[+] Mode BSGS %s\n", BSGS_MODES[opt.bsgs_mode]);  // keyhunt.cpp:1209-1211
   if (!opt.file && !(opt.mode == MODE_VANITY && opt.vanity.targets)) {
     fprintf(stderr, "[E] -f FILE is required\n");
     return EXIT_FAILURE;
@@ -1339,12 +1368,14 @@ int main(int argc, char **argv) {
     fprintf(stderr, "[E] Stride doesn't work with BSGS\n");
     return EXIT_FAILURE;
   }
+  if (opt.stride_set) printf("[+] Stride : %s\n", u_dec(opt.stride).c_str());  // keyhunt.cpp:1195-1203
+  if (opt.mode == MODE_BSGS) printf("[+] Mode BSGS %s\n", BSGS_MODES[opt.bsgs_mode]);  // keyhunt.cpp:1209-1211
+  if (opt.mode == MODE_ADDRESS && !opt.crypto_given) printf("[+] Setting search for btc adddress\n");  // 1217-1220
   // ranges (keyhunt.cpp:854-873, 1221-1269)
   if (opt.have_bits) {
     opt.start = u_shl1(opt.bits - 1);
     opt.end = u_shl1(opt.bits);
     if (u_cmp(opt.end, order) > 0) opt.end = order;
-    printf("[+] Bit Range %d\n", opt.bits);
   } else if (opt.have_range) {
     if (u_is_zero(opt.start)) opt.start = u_from_u64(1);
     if (u_cmp(opt.start, opt.end) == 0) {
@@ -1358,7 +1389,6 @@ int main(int argc, char **argv) {
         fprintf(stderr, "[W] Opps, start range can't be great than end range. Swapping them\n");
         std::swap(opt.start, opt.end);
       }
-      printf("[+] Range \n");
     }
   }
   if (!opt.have_bits && !opt.have_range) {
@@ -1367,25 +1397,42 @@ int main(int argc, char **argv) {
     opt.start = opt.mode == MODE_BSGS ? u_rand_range(u_from_u64(1), order) : u_from_u64(1);
     opt.end = order;
   }
-  printf("[+] -- from : 0x%s\n[+] -- to   : 0x%s\n", u_hex(opt.start).c_str(), u_hex(opt.end).c_str());
-  int ndev = 0;
-  kh_device_count(&ndev);
-  if (ndev < 1) {
-    fprintf(stderr, "[E] no GPU found\n");
-    return EXIT_FAILURE;
-  }
+  // the range lines: the address family prints them after "[+] N =" with the range as used
+  // (keyhunt.cpp:1325-1339); BSGS after reading its targets, with -r's strings as typed and nothing
+  // for a random start (1517-1540)
+  auto print_range = [&]() {
+    if (opt.mode == MODE_BSGS && !opt.have_bits && !opt.have_range) return;
+    printf(opt.have_bits ? "[+] Bit Range %d\n" : "[+] Range \n", opt.bits);
+    if (opt.mode == MODE_BSGS && !opt.have_bits)
+      printf("[+] -- from : 0x%s\n[+] -- to   : 0x%s\n", opt.range_start_str.c_str(),
+             opt.range_end_str.empty() ? u_hex(order).c_str() : opt.range_end_str.c_str());
+    else
+      printf("[+] -- from : 0x%s\n[+] -- to   : 0x%s\n", u_hex(opt.start).c_str(), u_hex(opt.end).c_str());
+  };
   // -g contexts: one host thread + kh_ctx each, on device d % ndev.  More contexts than devices
   // share a device (as the reference's -t threads share the host's cores); each keeps its own
   // tables and lanes, and they all take work from the one cursor (keyhunt.cpp:3321-3324, 4600-4617).
-  int gpus = opt.gpus > 0 ? opt.gpus : ndev;
-  printf("[+] GPUs : %d (%d context%s)\n", std::min(gpus, ndev), gpus, gpus == 1 ? "" : "s");
+  // The devices are counted once the targets are read, so the reference's lines come first.
+  int ndev = 0, gpus = 0;
+  std::vector<addr_job> aj;
+  std::vector<bsgs_job> bj;
+  auto open_devices = [&]() {
+    kh_device_count(&ndev);
+    if (ndev < 1) {
+      fprintf(stderr, "[E] no GPU found\n");
+      return false;
+    }
+    gpus = opt.gpus > 0 ? opt.gpus : ndev;
+    printf("[+] GPUs : %d (%d context%s)\n", std::min(gpus, ndev), gpus, gpus == 1 ? "" : "s");
+    aj.resize(gpus);
+    bj.resize(gpus);
+    return true;
+  };
   g_cursor = opt.start;
   g_end = opt.end;
   g_top = opt.end;
   U twoN;
   std::vector<std::thread> th;
-  std::vector<addr_job> aj(gpus);
-  std::vector<bsgs_job> bj(gpus);
   std::vector<uint8_t> rows;
   std::string data_file;  // -S target cache (outlives the GPU threads)
   std::vector<fe> tx, ty;
@@ -1398,6 +1445,7 @@ int main(int argc, char **argv) {
       if (nseq < 1024 || nseq % 1024) nseq = 0x100000000ULL;
     }
     printf("[+] N = %p\n", (void *)nseq);
+    print_range();
     uint64_t items = 0;
     // -S: read the target cache if it exists (FLAGREADEDFILE1), else read the file and write it
     bool have_data = false;
@@ -1442,6 +1490,7 @@ int main(int argc, char **argv) {
     }
     if (!have_data)
       printf("[+] Sorting data ... done! %llu values were loaded and sorted\n", (unsigned long long)(rows.size() / 20));
+    if (!open_devices()) return EXIT_FAILURE;
     g_running = gpus;
     for (int d = 0; d < gpus; d++) {
       aj[d].device = d % ndev;
@@ -1499,6 +1548,7 @@ int main(int argc, char **argv) {
       return EXIT_FAILURE;
     }
     printf("[+] Added %zu points from file\n", tx.size());
+    print_range();
     g_found.assign(tx.size(), 0);
     // BSGS N: -n or 2^44 (keyhunt.cpp:1454-1471); the library validates sqrt / 1024 and derives M
     uint64_t n = nk_n;
@@ -1528,6 +1578,7 @@ int main(int argc, char **argv) {
       fprintf(stderr, "[i] BSGS table build: %s layout, creating %llu block(s) of %llu babies each.\n",
               bc > 1 ? "GGSB" : "classic", (unsigned long long)bc, (unsigned long long)bs);
     }
+    if (!open_devices()) return EXIT_FAILURE;
     g_running = gpus;
     for (int d = 0; d < gpus; d++) {
       bj[d].device = d % ndev;

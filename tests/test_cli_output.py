@@ -58,3 +58,36 @@ def test_matrix_lines_one_per_base():
 def test_stats_fixture_terminators():
     assert all(l.endswith("\n") and not l.startswith("\r") for l in REF["rmd160_stats_M"]["stats_lines"])
     assert all(l.startswith("\r") and l.endswith("\r") for l in REF["rmd160_stats"]["stats_lines"])
+
+
+def _header_lines(text: str, bsgs: bool) -> list[str]:
+    """The lines before the run section, without the version line (the engine's own); for BSGS up
+    to "[+] N = ..." (the table-build lines after it are the reference's CPU build's)."""
+    m = __import__("_cli").RUN_START.search(text)
+    lines = [l for l in (text[:m.start()] if m else text).split("\n") if l and not l.startswith("[+] Version")]
+    if bsgs:
+        lines = lines[:next(i for i, l in enumerate(lines) if l.startswith("[+] N = ")) + 1]
+    return lines
+
+
+def test_cli_header_matches_reference():
+    """keyhunt-amd prints the reference's header lines (option echoes, mode, N, range, target loading)
+    in the reference's order, before it looks for a GPU: run here with no device, it stops right after
+    them ("[E] no GPU found")."""
+    import shutil
+    import subprocess
+    import tempfile
+    from conftest import DATA
+    from _cli import CLI
+    env = dict(os.environ, HIP_VISIBLE_DEVICES="-1", ROCR_VISIBLE_DEVICES="-1")
+    for name, ref in REF.items():
+        if name.startswith("_") or "stdout" not in ref:
+            continue
+        with tempfile.TemporaryDirectory() as td:
+            for fn in os.listdir(DATA):
+                shutil.copy(os.path.join(DATA, fn), td)
+            p = subprocess.run([CLI] + ref["argv"] + ["-t", "1", "-s", "0"], cwd=td, capture_output=True, text=True,
+                               timeout=60, env=env)
+        bsgs = "bsgs" in ref["argv"]
+        got = _header_lines(p.stdout, bsgs)
+        assert got == _header_lines(ref["stdout"], bsgs), name

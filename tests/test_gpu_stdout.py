@@ -19,6 +19,7 @@ import pytest
 
 from conftest import DATA, GOLDEN
 from _cli import CLI, render, run_section
+from test_cli_output import _header_lines
 
 pytestmark = pytest.mark.gpu
 REF = json.load(open(os.path.join(GOLDEN, "ref_stdout.json")))
@@ -39,14 +40,20 @@ def run_raw(argv: list[str], kill_after: int | None = None, timeout: int = 300) 
 @pytest.mark.parametrize("name", RUNS)
 def test_run_section_matches_reference(name):
     ref = REF[name]
-    p = run_raw(ref["argv"] + ["-g", "1", "-s", "0"])
+    p = run_raw(ref["argv"] + ["-t", "1", "-s", "0", "-g", "1"])
     assert p.returncode == ref["exit"], p.stdout[-2000:] + p.stderr[-2000:]
-    got = run_section(p.stdout.decode("latin-1"))
+    out = p.stdout.decode("latin-1")
+    got = run_section(out)
     want = run_section(ref["stdout"])
     assert want, name
     assert render(got) == render(want)
     if "-M" in ref["argv"]:  # one line per chunk / base: the bytes themselves
         assert got == want
+    # the header too (tests/test_cli_output.py checks it without a GPU): the engine's own lines are
+    # its version and the device count; BSGS compares up to "[+] N = " (then the tables are built)
+    bsgs = "bsgs" in ref["argv"]
+    head = [l for l in _header_lines(out, bsgs) if not l.startswith("[+] GPUs : ")]
+    assert head == _header_lines(ref["stdout"], bsgs)
 
 
 def _shape(line: str) -> str:
