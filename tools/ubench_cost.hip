@@ -37,6 +37,7 @@ __global__ __launch_bounds__(256) void k_pat(stamp *out, uint32_t seed) {
   uint64_t x0 = t * 3 + seed, x1 = t * 5, x2 = t * 7, x3 = t * 11;
   uint32_t a = t * 2654435761u + seed, b = a ^ 0x5bd1e995u, u0 = t, u1 = t + 1, u2 = t + 2, u3 = t + 3;
   uint64_t s0 = seed, s1 = seed + 1, s2 = seed + 2, s3 = seed + 3;
+  uint32_t v0 = t * 13, v1 = t * 17, v2 = t * 19, v3 = t * 23;  // 32-bit operands of the run patterns
   __syncthreads();
   const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
   for (int it = 0; it < TRIPS; it++) {
@@ -239,6 +240,21 @@ __global__ __launch_bounds__(256) void k_pat(stamp *out, uint32_t seed) {
                       "v_or_b32_sdwa %2, %2, %4 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD\n"
                       "v_or_b32_sdwa %3, %3, %5 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD\n")
                    : "+v"(u0), "+v"(u1), "+v"(u2), "+v"(u3), "=&v"(a), "=&v"(b));
+    if (P == 41)  // runs of 4: 4 alignbit then 4 v_add_u32 (does grouping let full-rate ops pair up?)
+      asm volatile(R4("v_alignbit_b32 %0, %0, %0, 7\n v_alignbit_b32 %1, %1, %1, 7\n v_alignbit_b32 %2, %2, %2, 7\n"
+                      "v_alignbit_b32 %3, %3, %3, 7\n v_add_u32 %4, %4, %8\n v_add_u32 %5, %5, %8\n"
+                      "v_add_u32 %6, %6, %8\n v_add_u32 %7, %7, %8\n")
+                   : "+v"(u0), "+v"(u1), "+v"(u2), "+v"(u3), "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3) : "v"(a));
+    if (P == 42)  // runs of 16: 16 alignbit then 16 bitop3
+      asm volatile(R4("v_alignbit_b32 %0, %0, %0, 7\n v_alignbit_b32 %1, %1, %1, 7\n v_alignbit_b32 %2, %2, %2, 7\n"
+                      "v_alignbit_b32 %3, %3, %3, 7\n")
+                   R4("v_bitop3_b32 %4, %4, %8, %5 bitop3:0x96\n v_bitop3_b32 %5, %5, %8, %6 bitop3:0x96\n"
+                      "v_bitop3_b32 %6, %6, %8, %7 bitop3:0x96\n v_bitop3_b32 %7, %7, %8, %4 bitop3:0x96\n")
+                   : "+v"(u0), "+v"(u1), "+v"(u2), "+v"(u3), "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3) : "v"(a));
+    if (P == 43)  // pairs: 2 alignbit then 2 v_add_u32
+      asm volatile(R8("v_alignbit_b32 %0, %0, %0, 7\n v_alignbit_b32 %1, %1, %1, 7\n v_add_u32 %2, %2, %4\n"
+                      "v_add_u32 %3, %3, %4\n")
+                   : "+v"(u0), "+v"(u1), "+v"(u2), "+v"(u3) : "v"(a));
     if (P == 24)  // 16 mads + 16 v_mov (the product-scanning column shift), interleaved
       asm volatile(R8("v_mad_u64_u32 %0, %4, %5, %6, %0\n v_mov_b32 %7, %5\n v_mad_u64_u32 %1, %4, %5, %6, %1\n"
                       "v_mov_b32 %8, %6\n")
@@ -248,7 +264,7 @@ __global__ __launch_bounds__(256) void k_pat(stamp *out, uint32_t seed) {
   if ((threadIdx.x & 63) == 0) {
     stamp s;
     s.t0 = t0;
-    s.t1 = t1 + (x0 ^ x1 ^ x2 ^ x3 ^ u0 ^ u1 ^ u2 ^ u3 ^ s0 ^ s1 ^ s2 ^ s3 ^ a ^ b) * 0;  // keep results live
+    s.t1 = t1 + (x0 ^ x1 ^ x2 ^ x3 ^ u0 ^ u1 ^ u2 ^ u3 ^ s0 ^ s1 ^ s2 ^ s3 ^ a ^ b ^ v0 ^ v1 ^ v2 ^ v3) * 0;  // keep results live
     s.r0 = r0;
     s.r1 = r1;
     out[t >> 6] = s;
@@ -260,7 +276,7 @@ typedef void (*kfn)(stamp *, uint32_t);
 static const kfn kernels[] = {K(0),  K(1),  K(2),  K(3),  K(4),  K(5),  K(6),  K(7),  K(8),  K(9),  K(10), K(11), K(12),
                               K(13), K(14), K(15), K(16), K(17), K(18), K(19), K(20), K(21), K(22), K(23), K(24),
                               K(25), K(26), K(27), K(28), K(29), K(30), K(31), K(32), K(33), K(34), K(35), K(36),
-                              K(37), K(38), K(39), K(40)};
+                              K(37), K(38), K(39), K(40), K(41), K(42), K(43)};
 static const char *names[] = {
     "mad_u64_u32 acc, 4 chains",      "mad,nop,addc,nop (as hipcc)",  "mad+addc, hazards scheduled", "addc_e32 vcc chain + s_nop 1",
     "add_co/addc, 4 sgpr chains",     "v_mov_b32",                    "v_add_u32",                   "v_and_b32",
@@ -272,7 +288,7 @@ static const char *names[] = {
     "7-col: SALU count (+3 add)",     "v_alignbyte_b32",              "v_lshl_or_b32",               "rotate = lshrrev + lshl_or",
     "v_or3_b32",                      "v_xad_u32 (xor-add)",                   "alignbit + v_add_u32 mix",    "alignbit + bitop3 mix",
     "v_lshl_add_u32",                 "add3 + bitop3 mix",            "mad + bitop3 mix",            "v_add_u32 + v_xor_b32 mix",
-    "rot16 = 2 sdwa ops"};
+    "rot16 = 2 sdwa ops",             "runs: 4 alignbit, 4 add",      "runs: 16 alignbit, 16 bitop3", "runs: 2 alignbit, 2 add"};
 
 int main(int argc, char **argv) {
   // optional: the pattern numbers to run (default all)
