@@ -1137,15 +1137,9 @@ int kh_bsgs_setup(kh_ctx *ctx, uint64_t n, uint64_t k, kh_bsgs_info *info) {
     (void)hipFree(ctx->d_bl[l]);
     ctx->d_bl[l] = nullptr;
     size_t bytes = 256 * ctx->bd[l].stride + 4;
-    // A/B hook (round 4): KH_L1_ALLOC=fine|uncached allocates layer 1 with hipExtMallocWithFlags
-    // (fine-grained / uncached memory types), to see whether the probes' fabric requests shrink
-    const char *al = l == 0 ? getenv("KH_L1_ALLOC") : nullptr;
-    if (al && (!strcmp(al, "fine") || !strcmp(al, "uncached"))) {
-      HIPCHK(ctx, hipExtMallocWithFlags((void **)&ctx->d_bl[l], bytes,
-                                        !strcmp(al, "fine") ? hipDeviceMallocFinegrained : hipDeviceMallocUncached));
-    } else {
-      HIPCHK(ctx, hipMalloc(&ctx->d_bl[l], bytes));
-    }
+    // (fine-grained and uncached memory types for layer 1 were measured in round 4: no gain, the
+    // probes still cost the same power, profiles/r04e_alloc_ab.json)
+    HIPCHK(ctx, hipMalloc(&ctx->d_bl[l], bytes));
     HIPCHK(ctx, hipMemset(ctx->d_bl[l], 0, bytes));
   }
   // AMP2[i] = -(M2 + 2i*M2)G, AMP3[i] = -(M3 + 2i*M3)G  (keyhunt.cpp:1818-1842)

@@ -1,5 +1,6 @@
 """Small fixed workload for rocprofv3 counter passes: one BSGS launch (2^30 giant points), one
-rmd160 and one xpoint launch (2^30 points each) -- one dispatch of each dominant kernel."""
+rmd160 and one xpoint launch (one 2^32-key chunk each: 2^20 lanes x one 4096-point group, the
+address family's launch geometry since round 4) -- one dispatch of each dominant kernel."""
 import os
 import sys
 
@@ -13,8 +14,8 @@ e.bsgs_build()
 e.bsgs_set_targets([bench.decompress(bench.PUZZLE125)])
 e.bsgs_scan(1 << 124, 32768)          # one launch: 2^18 lanes x 1 group of 4096 = 2^30 giant points
 e.set_targets([bytes.fromhex(bench.PUZZLE66_RMD)], bloom_items=1)
-e.scan(1 << 65, 1 << 30, K.KH_MODE_ADDRESS, K.KH_SEARCH_COMPRESS)
+e.scan(1 << 65, 1 << 32, K.KH_MODE_ADDRESS, K.KH_SEARCH_COMPRESS)
 e.set_targets([bench.PUZZLE63_X.to_bytes(32, "big")[:20]], bloom_items=1)
-e.scan(1 << 62, 1 << 30, K.KH_MODE_XPOINT, K.KH_SEARCH_COMPRESS)
+e.scan(1 << 62, 1 << 32, K.KH_MODE_XPOINT, K.KH_SEARCH_COMPRESS)
 e.synchronize()
 print("done", e.kernel_time(2), e.kernel_time(0), e.kernel_time(1))

@@ -34,6 +34,15 @@ cycles the pads add when other waves issue beside them, ~0.3), and the share of 
 the PMC saw dual-issued (SQ_ACTIVE_INST_VALU2 / SQ_INSTS_VALU) taken as free.  A kernel cannot issue
 its instructions faster than that at a given clock, whatever their order.
 
+Quad model (round 4, what the walks actually meet): on gfx950 a full-rate instruction only issues in
+2 cycles when another full-rate one shares its 4-cycle quad; streams that mix full- and half-rate
+instructions -- alternating, or in runs of 2, 4 or 16 -- issue at ~4 cycles per instruction whatever
+their classes (profiles/r04d_ubench_cost.txt "alignbit + v_add_u32 mix" 4.04, "alignbit + bitop3 mix"
+3.86, r04e_ubench_runs.txt "runs" 4.00-4.04 at 4 waves/SIMD).  simd_cycles_per_point_quad prices
+every VALU instruction at one quad, the dual-issued share (SQ_ACTIVE_INST_VALU2 / SQ_INSTS_VALU) free
+and s_nop at its in-situ cost.  It is a model of the mixed kernels, not a hardware bound: pure
+full-rate stretches issued by several waves at once would beat it.
+
 usage: python tools/valu_mix.py LISTING.s PMC_SUMMARY.json OUT.json [COST.txt]
 """
 import json
@@ -282,14 +291,17 @@ def main():
                 dual = c["SQ_ACTIVE_INST_VALU2"] / c["SQ_INSTS_VALU"]
         e["dual_issue_share"] = dual
         e["simd_cycles_per_point_floor"] = cyc_floor * f * (1 - dual)
+        e["simd_cycles_per_point_quad"] = (valu * f * 4.0 * (1 - dual) + pp.get("s_nop", 0.0) * nop) / 64
+        e["recompute_quad"] = ("simd_cycles_per_point_quad = (valu_per_point_pmc * 4 * (1 - dual_issue_share) + "
+                               "s_nop_states_per_point * s_nop_in_situ_cycles) / 64")
         e["recompute_floor"] = ("simd_cycles_per_point_floor = sum(lane_instructions_per_point[c] * "
                                 "class_floor_simd_cycles[c]) / 64 * pmc_over_static * (1 - dual_issue_share)")
         res[name] = e
     json.dump(res, open(out, "w"), indent=1)
     for k, e in res.items():
-        print(k, "static VALU/pt %.1f  PMC %.1f  s_nop states/pt %.1f  SIMD cycles/pt %.3f (floor %.3f)" % (
+        print(k, "static VALU/pt %.1f  PMC %.1f  s_nop states/pt %.1f  SIMD cycles/pt %.3f (floor %.3f, quad %.3f)" % (
             e["valu_per_point_static"], e.get("valu_per_point_pmc", 0), e["s_nop_states_per_point"],
-            e["simd_cycles_per_point"], e["simd_cycles_per_point_floor"]))
+            e["simd_cycles_per_point"], e["simd_cycles_per_point_floor"], e["simd_cycles_per_point_quad"]))
         print("   ", e["simd_cycles_by_class"])
 
 
