@@ -28,4 +28,5 @@ def _argv(name: str, contexts: int) -> list[str]:
 @pytest.mark.parametrize("name", CASES)
 def test_cli_contexts_match_reference(name, contexts):
     p = check_against_reference(E2E[name], _argv(name, contexts), name)
-    assert f"({contexts} contexts)" in p.stdout
+    if E2E[name]["exit"] != 255:  # the run got as far as opening its contexts (not a refused target file)
+        assert f"({contexts} contexts)" in p.stdout
