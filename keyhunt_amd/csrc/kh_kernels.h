@@ -111,6 +111,11 @@ KH_HD void kh_blk_masks(uint32_t s0, uint32_t s1, uint32_t s2, uint32_t m[4]) {
 #ifndef KH_SPARSE_ALL
 #define KH_SPARSE_ALL 0
 #endif
+//   KH_PAD_PLANES  the two 16-B halves of every inversion-pad entry in separate planes (kh_kernels.hip
+//                  pad_idx): one wave access covers 1 KB contiguously instead of 2 KB with holes
+#ifndef KH_PAD_PLANES
+#define KH_PAD_PLANES 0
+#endif
 //   KH_XPOINT_DEFER -m xpoint against the blocked target filter walks like the BSGS giant walk: a
 //                pair's two 16-B filter loads are issued one step later and tested after that
 //                step's field math (k_walk<KM_XPOINTB>), and -(dy) = T.y + C.y replaces the negation

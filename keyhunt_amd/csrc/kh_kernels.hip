@@ -56,12 +56,21 @@ __device__ __forceinline__ void store_soa(uint32_t *__restrict__ base, uint32_t 
 #pragma unroll
   for (int i = 0; i < 8; i++) base[(size_t)i * L + g] = r.d[i];
 }
-__device__ __forceinline__ void scr_store(uint4 *__restrict__ scr, size_t slot, const fe &a) {
-  scr[2 * slot] = make_uint4(a.d[0], a.d[1], a.d[2], a.d[3]);
-  scr[2 * slot + 1] = make_uint4(a.d[4], a.d[5], a.d[6], a.d[7]);
+// Pad entry `slot` = row * L + g (lane g) as two 16-B halves.  KH_PAD_PLANES: the halves of a row
+// live in two planes of L entries each, so one 16-B access of a wave covers 1 KB contiguously
+// (16 lines) instead of 2 KB with 16-B holes (32 lines, each touched again by the other half)
+__device__ __forceinline__ size_t pad_idx(size_t slot, uint32_t g, size_t L, int h) {
+  if constexpr (KH_PAD_PLANES) return 2 * slot - g + (h ? L : 0);
+  (void)g;
+  (void)L;
+  return 2 * slot + h;
 }
-__device__ __forceinline__ void scr_load(fe &a, const uint4 *__restrict__ scr, size_t slot) {
-  uint4 u = scr[2 * slot], v = scr[2 * slot + 1];
+__device__ __forceinline__ void scr_store(uint4 *__restrict__ scr, size_t slot, const fe &a, uint32_t g, size_t L) {
+  scr[pad_idx(slot, g, L, 0)] = make_uint4(a.d[0], a.d[1], a.d[2], a.d[3]);
+  scr[pad_idx(slot, g, L, 1)] = make_uint4(a.d[4], a.d[5], a.d[6], a.d[7]);
+}
+__device__ __forceinline__ void scr_load(fe &a, const uint4 *__restrict__ scr, size_t slot, uint32_t g, size_t L) {
+  uint4 u = scr[pad_idx(slot, g, L, 0)], v = scr[pad_idx(slot, g, L, 1)];
   a.d[0] = u.x; a.d[1] = u.y; a.d[2] = u.z; a.d[3] = u.w;
   a.d[4] = v.x; a.d[5] = v.y; a.d[6] = v.z; a.d[7] = v.w;
 }
@@ -574,9 +583,9 @@ __global__ void __launch_bounds__((walk_threads<MODE, H>()), (walk_blocks_per_cu
           acc = dx0;
         else
           fe_mul(acc, acc, dx0);
-        scr_store(scr, slot(i), acc);
+        scr_store(scr, slot(i), acc, g, L);
         fe_mul(acc, acc, dx1);
-        if (!SPARSE) scr_store(scr, slot(i + 1), acc);
+        if (!SPARSE) scr_store(scr, slot(i + 1), acc, g, L);
       }
     } else {
 #pragma unroll 1
@@ -588,7 +597,7 @@ __global__ void __launch_bounds__((walk_threads<MODE, H>()), (walk_blocks_per_cu
           acc = dx;
         else
           fe_mul(acc, acc, dx);
-        if (!SPARSE || (i & 1) == 0) scr_store(scr, slot(i), acc);
+        if (!SPARSE || (i & 1) == 0) scr_store(scr, slot(i), acc, g, L);
       }
     }
     fe t2x, t2y, dxn;
@@ -630,7 +639,7 @@ __global__ void __launch_bounds__((walk_threads<MODE, H>()), (walk_blocks_per_cu
     if constexpr (MODE == KM_XPOINTB && KH_FULL_GROUPS) wfull = !kh_any(cidx + H > A.n_points);
 #endif
     fe pre;
-    scr_load(pre, scr, slot(H - 2));
+    scr_load(pre, scr, slot(H - 2), g, L);
 #pragma unroll 1
     for (int i = H - 1; i >= 0; i--) {
       fe tx, ty, di;
@@ -650,7 +659,7 @@ __global__ void __launch_bounds__((walk_threads<MODE, H>()), (walk_blocks_per_cu
         }
         fe_mul(di, inv, pre);
         // refill `pre` for the next step right after its last use (no register copy)
-        if (i > 1) scr_load(pre, scr, slot(i - 2));
+        if (i > 1) scr_load(pre, scr, slot(i - 2), g, L);
         fe_sub(dx, tx, cx);
         fe_mul(inv, inv, dx);
       } else {
