@@ -111,10 +111,24 @@ KH_HD void kh_blk_masks(uint32_t s0, uint32_t s1, uint32_t s2, uint32_t m[4]) {
 #ifndef KH_SPARSE_ALL
 #define KH_SPARSE_ALL 0
 #endif
+//   KH_SPARSE_KEEP the sparse pad's backward pass keeps the loaded even row as loaded for the two
+//                  steps it serves (one read per row; the load lands in place and flies for a step)
+#ifndef KH_SPARSE_KEEP
+#define KH_SPARSE_KEEP 1
+#endif
 //   KH_PAD_PLANES  the two 16-B halves of every inversion-pad entry in separate planes (kh_kernels.hip
 //                  pad_idx): one wave access covers 1 KB contiguously instead of 2 KB with holes
 #ifndef KH_PAD_PLANES
 #define KH_PAD_PLANES 0
+#endif
+//   KH_PAD_NT      the inversion pad's stores (bit 0) / loads (bit 1) with the nontemporal hint
+#ifndef KH_PAD_NT
+#define KH_PAD_NT 0
+#endif
+//   KH_PROBE_EARLY the deferred walks issue the previous pair's block loads at the top of a step,
+//                  before its inverse, instead of after it
+#ifndef KH_PROBE_EARLY
+#define KH_PROBE_EARLY 0
 #endif
 //   KH_XPOINT_DEFER -m xpoint against the blocked target filter walks like the BSGS giant walk: a
 //                pair's two 16-B filter loads are issued one step later and tested after that

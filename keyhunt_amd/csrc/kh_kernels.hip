@@ -65,14 +65,37 @@ __device__ __forceinline__ size_t pad_idx(size_t slot, uint32_t g, size_t L, int
   (void)L;
   return 2 * slot + h;
 }
+typedef uint32_t pad4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void scr_store(uint4 *__restrict__ scr, size_t slot, const fe &a, uint32_t g, size_t L) {
+  if constexpr (KH_PAD_NT & 1) {
+    pad4 *p = reinterpret_cast<pad4 *>(scr);
+    __builtin_nontemporal_store(pad4{a.d[0], a.d[1], a.d[2], a.d[3]}, p + pad_idx(slot, g, L, 0));
+    __builtin_nontemporal_store(pad4{a.d[4], a.d[5], a.d[6], a.d[7]}, p + pad_idx(slot, g, L, 1));
+    return;
+  }
   scr[pad_idx(slot, g, L, 0)] = make_uint4(a.d[0], a.d[1], a.d[2], a.d[3]);
   scr[pad_idx(slot, g, L, 1)] = make_uint4(a.d[4], a.d[5], a.d[6], a.d[7]);
 }
-__device__ __forceinline__ void scr_load(fe &a, const uint4 *__restrict__ scr, size_t slot, uint32_t g, size_t L) {
-  uint4 u = scr[pad_idx(slot, g, L, 0)], v = scr[pad_idx(slot, g, L, 1)];
+// a pad entry as its two loaded 16-B halves (kept as loaded across a loop edge, see k_walk)
+__device__ __forceinline__ void scr_load_raw(pad4 &u, pad4 &v, const uint4 *__restrict__ scr, size_t slot, uint32_t g,
+                                             size_t L) {
+  const pad4 *p = reinterpret_cast<const pad4 *>(scr);
+  if constexpr (KH_PAD_NT & 2) {
+    u = __builtin_nontemporal_load(p + pad_idx(slot, g, L, 0));
+    v = __builtin_nontemporal_load(p + pad_idx(slot, g, L, 1));
+  } else {
+    u = p[pad_idx(slot, g, L, 0)];
+    v = p[pad_idx(slot, g, L, 1)];
+  }
+}
+__device__ __forceinline__ void pad_unpack(fe &a, const pad4 &u, const pad4 &v) {
   a.d[0] = u.x; a.d[1] = u.y; a.d[2] = u.z; a.d[3] = u.w;
   a.d[4] = v.x; a.d[5] = v.y; a.d[6] = v.z; a.d[7] = v.w;
+}
+__device__ __forceinline__ void scr_load(fe &a, const uint4 *__restrict__ scr, size_t slot, uint32_t g, size_t L) {
+  pad4 u, v;
+  scr_load_raw(u, v, scr, slot, g, L);
+  pad_unpack(a, u, v);
 }
 
 // bloom_check (bloom/bloom.cpp:189-212) on one filter at `bf`
@@ -553,7 +576,20 @@ __global__ void __launch_bounds__((walk_threads<MODE, H>()), (walk_blocks_per_cu
   // BSGS walks keep only the even prefix products in the pad and rebuild each odd one with one
   // multiplication in the backward pass: half the pad traffic for +1/2 multiplication per pair
   constexpr bool SPARSE = KH_SPARSE_ALL || (KH_SPARSE_BSGS && (MODE == KM_BSGSB || MODE == KM_BSGS));
+#ifdef KH_TIMING_PAD_ROWS_LOG2
+  // timing-only build: the pad's stores (KH_TIMING_PAD_FOLD & 1) and/or loads (& 2) folded onto its
+  // first 2^LOG2 rows (8 MB each at 2^18 lanes), which stay on die -- those accesses without their
+  // HBM traffic (outputs wrong)
+  auto fold = [&](int m, int which) {
+    const int r = SPARSE ? (m >> 1) : m;
+    return (size_t)((KH_TIMING_PAD_FOLD & which) ? (r & ((1 << KH_TIMING_PAD_ROWS_LOG2) - 1)) : r) * L + g;
+  };
+  auto slot_w = [&](int m) { return fold(m, 1); };
+  auto slot = [&](int m) { return fold(m, 2); };
+#else
   auto slot = [&](int m) { return (size_t)(SPARSE ? (m >> 1) : m) * L + g; };
+  auto slot_w = slot;
+#endif
   // Deferred-probe walks (one 16-B split-block load per point, issued a step ahead): the BSGS giant
   // walk against the blocked layer 1 (kind 4) and -m xpoint against the blocked target filter (kind 3)
   constexpr bool DEFER = MODE == KM_BSGSB || MODE == KM_XPOINTB;
@@ -583,9 +619,9 @@ __global__ void __launch_bounds__((walk_threads<MODE, H>()), (walk_blocks_per_cu
           acc = dx0;
         else
           fe_mul(acc, acc, dx0);
-        scr_store(scr, slot(i), acc, g, L);
+        scr_store(scr, slot_w(i), acc, g, L);
         fe_mul(acc, acc, dx1);
-        if (!SPARSE) scr_store(scr, slot(i + 1), acc, g, L);
+        if (!SPARSE) scr_store(scr, slot_w(i + 1), acc, g, L);
       }
     } else {
 #pragma unroll 1
@@ -597,7 +633,7 @@ __global__ void __launch_bounds__((walk_threads<MODE, H>()), (walk_blocks_per_cu
           acc = dx;
         else
           fe_mul(acc, acc, dx);
-        if (!SPARSE || (i & 1) == 0) scr_store(scr, slot(i), acc, g, L);
+        if (!SPARSE || (i & 1) == 0) scr_store(scr, slot_w(i), acc, g, L);
       }
     }
     fe t2x, t2y, dxn;
@@ -638,11 +674,26 @@ __global__ void __launch_bounds__((walk_threads<MODE, H>()), (walk_blocks_per_cu
 #if defined(__HIP_DEVICE_COMPILE__)
     if constexpr (MODE == KM_XPOINTB && KH_FULL_GROUPS) wfull = !kh_any(cidx + H > A.n_points);
 #endif
+    // KEEP (sparse pad): the even prefix row last loaded, as its two loaded halves; otherwise `pre`
+    constexpr bool KEEP = SPARSE && KH_SPARSE_KEEP;
+    static_assert(!KEEP || (H % 2) == 0, "the sparse pad pairs odd and even steps");
     fe pre;
-    scr_load(pre, scr, slot(H - 2), g, L);
-#pragma unroll 1
-    for (int i = H - 1; i >= 0; i--) {
+    pad4 ru, rv;
+    if constexpr (KEEP)
+      scr_load_raw(ru, rv, scr, slot(H - 2), g, L);
+    else
+      scr_load(pre, scr, slot(H - 2), g, L);
+    // one backward step; `par` is the parity of i when the caller knows it (1 odd, 2 even, 0 unknown)
+    auto step = [&](const int i, const int par) __attribute__((always_inline)) {
       fe tx, ty, di;
+#if KH_PROBE_EARLY
+      // the previous pair's block loads issued before this step's inverse too (they fly during it)
+      uint4 vm, vp;
+      if constexpr (DEFER) {
+        vm = dload(pm);
+        vp = dload(pp);
+      }
+#endif
       ld_tx(tx, i);
       ld_ty(ty, i);
       if constexpr (KH_TAB_VCOPY && MODE == KM_BSGSB && !LDS) {
@@ -651,15 +702,34 @@ __global__ void __launch_bounds__((walk_threads<MODE, H>()), (walk_blocks_per_cu
       }
       if (i > 0) {
         fe dx;
-        if (SPARSE && ((i - 1) & 1)) {  // prefix[i-1] = prefix[i-2] * dx[i-1] (pre holds prefix[i-2])
-          fe tpx, d1;
-          ld_tx(tpx, i - 1);
-          fe_sub(d1, tpx, cx);
-          fe_mul(pre, pre, d1);
+        if constexpr (KEEP) {
+          // An odd step i needs the even prefix[i-1], the row R itself, and then loads the next row,
+          // prefix[i-3], which serves the two steps after it; an even step rebuilds the odd
+          // prefix[i-1] = R * dx[i-1].  R is written by its loads only, so they land in place and
+          // fly for a whole step, and each row is read once.
+          fe r;
+          pad_unpack(r, ru, rv);
+          if (par == 1 || (par == 0 && (i & 1))) {
+            fe_mul(di, inv, r);
+            if (i > 1) scr_load_raw(ru, rv, scr, slot(i - 3), g, L);
+          } else {
+            fe tpx, d1, p;
+            ld_tx(tpx, i - 1);
+            fe_sub(d1, tpx, cx);
+            fe_mul(p, r, d1);
+            fe_mul(di, inv, p);
+          }
+        } else {
+          if (SPARSE && ((i - 1) & 1)) {  // prefix[i-1] = prefix[i-2] * dx[i-1] (pre holds prefix[i-2])
+            fe tpx, d1;
+            ld_tx(tpx, i - 1);
+            fe_sub(d1, tpx, cx);
+            fe_mul(pre, pre, d1);
+          }
+          fe_mul(di, inv, pre);
+          // refill `pre` for the next step right after its last use
+          if (i > 1) scr_load(pre, scr, slot(i - 2), g, L);
         }
-        fe_mul(di, inv, pre);
-        // refill `pre` for the next step right after its last use (no register copy)
-        if (i > 1) scr_load(pre, scr, slot(i - 2), g, L);
         fe_sub(dx, tx, cx);
         fe_mul(inv, inv, dx);
       } else {
@@ -669,7 +739,9 @@ __global__ void __launch_bounds__((walk_threads<MODE, H>()), (walk_blocks_per_cu
         // The previous pair's block loads are issued first and tested after this pair's field
         // math: the loads fly during it.  Only their addresses cross the loop edge (ALU values),
         // never an in-flight load destination.
+#if !KH_PROBE_EARLY
         const uint4 vm = dload(pm), vp = dload(pp);
+#endif
         fe xm, xp, s, dy, sx;
         // x3 = s^2 - (C.x + T.x) for both points; dy = -(dy of C - T[i]): only s^2 is needed, so
         // the sign drops out.  Adjacent independent add/sub pairs share one interleaved chain.
@@ -693,7 +765,7 @@ __global__ void __launch_bounds__((walk_threads<MODE, H>()), (walk_blocks_per_cu
           plm = off > lm;
           plp = off < hp;  // also false at i = H - 1 (off = H >= hp): C + H is the next group's
         }
-        continue;
+        return;
       }
       if constexpr (MODE == KM_BSGS) {
         // both points first, then one lockstep probe of the pair (two loads in flight per lane)
@@ -709,7 +781,7 @@ __global__ void __launch_bounds__((walk_threads<MODE, H>()), (walk_blocks_per_cu
         fe_sub(xp, xp, sx);
         const uint64_t off = (uint64_t)(i + 1);
         probe_pair_bsgs(A, xm, cidx - off, xp, cidx + off, i < H - 1);
-        continue;
+        return;
       }
       fe sx;
       fe_add(sx, cx, tx);  // x3 = s^2 - (C.x + T.x) on both sides
@@ -734,6 +806,17 @@ __global__ void __launch_bounds__((walk_threads<MODE, H>()), (walk_blocks_per_cu
         const uint64_t off = (uint64_t)(i + 1);
         probe_point<MODE>(A, x, y, side ? cidx + off : cidx - off);
       }
+    };
+    if constexpr (KEEP) {
+      // two steps per trip, odd then even: the kept row's loads land in place (no copy to wait on)
+#pragma unroll 1
+      for (int i = H - 1; i > 0; i -= 2) {
+        step(i, 1);
+        step(i - 1, 2);
+      }
+    } else {
+#pragma unroll 1
+      for (int i = H - 1; i >= 0; i--) step(i, 0);
     }
     if constexpr (DEFER) {  // the last pair of the group
       if (plm && blk_match_rec(dload(pm), pm)) record_hit(A, cidx - poff, DKIND);
