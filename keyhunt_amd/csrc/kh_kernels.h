@@ -108,6 +108,11 @@ KH_HD void kh_blk_masks(uint32_t s0, uint32_t s1, uint32_t s2, uint32_t m[4]) {
 #ifndef KH_SPARSE_BSGS
 #define KH_SPARSE_BSGS 1
 #endif
+//   KH_SPARSE_XPOINT the sparse pad (even prefix products only) for -m xpoint's blocked walk too
+//                  (round 4, with KH_SPARSE_KEEP: +1.5 %, profiles/r04o_sparse_xpoint_ab.json)
+#ifndef KH_SPARSE_XPOINT
+#define KH_SPARSE_XPOINT 1
+#endif
 #ifndef KH_SPARSE_ALL
 #define KH_SPARSE_ALL 0
 #endif

@@ -573,9 +573,10 @@ __global__ void __launch_bounds__((walk_threads<MODE, H>()), (walk_blocks_per_cu
   load_soa(cx, A.cx, A.L, g);
   load_soa(cy, A.cy, A.L, g);
 
-  // BSGS walks keep only the even prefix products in the pad and rebuild each odd one with one
-  // multiplication in the backward pass: half the pad traffic for +1/2 multiplication per pair
-  constexpr bool SPARSE = KH_SPARSE_ALL || (KH_SPARSE_BSGS && (MODE == KM_BSGSB || MODE == KM_BSGS));
+  // BSGS and xpoint walks keep only the even prefix products in the pad and rebuild each odd one
+  // with one multiplication in the backward pass: half the pad traffic for +1/2 multiplication per pair
+  constexpr bool SPARSE = KH_SPARSE_ALL || (KH_SPARSE_BSGS && (MODE == KM_BSGSB || MODE == KM_BSGS)) ||
+                          (KH_SPARSE_XPOINT && MODE == KM_XPOINTB);
 #ifdef KH_TIMING_PAD_ROWS_LOG2
   // timing-only build: the pad's stores (KH_TIMING_PAD_FOLD & 1) and/or loads (& 2) folded onto its
   // first 2^LOG2 rows (8 MB each at 2^18 lanes), which stay on die -- those accesses without their
