@@ -51,9 +51,11 @@ import sys
 
 # kernel -> (symbol, its largest loop runs once per point: the hash walks' side loop, prefix
 # products per forward-loop trip: the deferred-probe walks pair two per trip, kh_kernels.hip)
-KERNELS = {"k_walk<7, 2048>": ("_Z6k_walkILi7ELi2048EEv9walk_args", False, 2),
-           "k_walk<10, 2048>": ("_Z6k_walkILi10ELi2048EEv9walk_args", False, 2),
-           "k_walk<11, 2048>": ("_Z6k_walkILi11ELi2048EEv9walk_args", True, 1)}
+# (symbol, per-point side loop, prefix products per forward trip, backward steps per trip: the
+# sparse-pad walks run two steps, odd then even, per backward trip since round 4's kept row)
+KERNELS = {"k_walk<7, 2048>": ("_Z6k_walkILi7ELi2048EEv9walk_args", False, 2, 2),
+           "k_walk<10, 2048>": ("_Z6k_walkILi10ELi2048EEv9walk_args", False, 2, 2),
+           "k_walk<11, 2048>": ("_Z6k_walkILi11ELi2048EEv9walk_args", True, 1, 1)}
 
 # ubench_cost.txt pattern name -> class
 PATTERN = {"mad_u64_u32 acc, 4 chains": "mad64", "add_co/addc, 4 sgpr chains": "carry", "v_mov_b32": "mov",
@@ -215,7 +217,7 @@ def common_path(bl, a, b):
     return w
 
 
-def mix(listing: str, sym: str, per_point_loop: bool, fwd_per_trip: int = 1):
+def mix(listing: str, sym: str, per_point_loop: bool, fwd_per_trip: int = 1, bwd_per_trip: int = 1):
     """Lane-instructions per point by class.  The largest loop of the kernel is its per-pair
     backward loop (deferred-probe walks) or, with per_point_loop, the per-point side loop of the
     hash walks inside it; loops overlapping it are the rest of the backward loop (per pair), and the
@@ -231,7 +233,7 @@ def mix(listing: str, sym: str, per_point_loop: bool, fwd_per_trip: int = 1):
     for k in range(fwd[0], fwd[1] + 1):
         weight[k] = 0.5 / fwd_per_trip  # a trip makes fwd_per_trip prefix products (2 points each)
     for k in range(lo, hi + 1):
-        weight[k] = 1.0 if (per_point_loop and top[0] <= k <= top[1]) else 0.5
+        weight[k] = 1.0 if (per_point_loop and top[0] <= k <= top[1]) else 0.5 / bwd_per_trip
     # one control-flow walk over the whole backward loop (its nested ranges share the header lo)
     cp = [common_path(bl, lo, hi), common_path(bl, fwd[0], fwd[1])]
     rare = {k for w in cp for k in range(len(w)) if w[k] == 0.0}
@@ -261,8 +263,8 @@ def main():
     nop = nop_in_situ(cost_path)
     pm = json.load(open(pmc))
     res = {}
-    for name, (sym, ppl, fpt) in KERNELS.items():
-        pp = mix(listing, sym, ppl, fpt)
+    for name, (sym, ppl, fpt, bpt) in KERNELS.items():
+        pp = mix(listing, sym, ppl, fpt, bpt)
         # pp: lane-instructions per point (every lane walks its own points); a wave-instruction
         # serves 64 points, so SIMD cycles per point = sum(count x class cost) / 64
         valu = sum(v for k, v in pp.items() if k != "s_nop")
