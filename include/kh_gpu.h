@@ -136,6 +136,12 @@ int kh_set_vanity(kh_ctx *ctx, const uint8_t *ranges, uint64_t n, uint32_t probe
  * lanes instead of starting them again: sequential chunks are cheaper, results are the same. */
 int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride[32], uint64_t n_keys, uint32_t mode,
             uint32_t search, kh_hit *hits, uint32_t cap, uint32_t *n_hits);
+/* The device bytes one context's kh_scan of n_keys-key chunks holds at the default geometry, exact
+ * targets (the inversion pad -- 2^20 lanes x 4096-point groups for the 2^32-key chunks of -m xpoint and
+ * -l compress, half of it for xpoint's sparse pad -- lane centres, comb, hit buffer; target tables come
+ * on top).  Hosts that stack contexts on one device check it against kh_device_memory first.  With
+ * --rmd-batch-size (kh_set_rmd_batch) a chunk needs less. */
+int kh_scan_memory(uint64_t n_keys, uint32_t mode, uint32_t search, uint64_t *needed_bytes);
 /* -m rmd160 --rmd-batch-size (keyhunt.cpp:815-829, 3301-3307): group = the reference's clamped
  * rmd_batch_size (a multiple of 4 in [4, 1024]; 1024 or 0 = the ordinary walk).  Below 1024 the
  * following hash160 kh_scan calls reproduce the reference's groups of `group` keys exactly as it
@@ -150,6 +156,10 @@ int kh_set_rmd_batch(kh_ctx *ctx, uint32_t group);
 /* ---- BSGS --------------------------------------------------------------------------------- */
 /* layer-1 layout for the next kh_bsgs_setup (KH_LAYER1_BLOCKED unless changed) */
 int kh_bsgs_set_layer1(kh_ctx *ctx, uint32_t layout);
+/* -z (FLAGBLOOMMULTIPLIER, keyhunt.cpp:1111-1117) for the next kh_bsgs_setup: initBloomFilter sizes a
+ * shard of more than 10000 items for mult x items entries (keyhunt.cpp:7608), so the three layers'
+ * geometry -- and their -S files -- follow it as the reference's do.  Default 1. */
+int kh_bsgs_set_bloom_multiplier(kh_ctx *ctx, uint32_t mult);
 int kh_bsgs_setup(kh_ctx *ctx, uint64_t n, uint64_t k, kh_bsgs_info *info);
 /* after kh_bsgs_setup: the device bytes this context holds once its tables are built and it scans
  * (the three layers, the bP rows, the inversion pad of the giant walk, lane state, candidate buffers

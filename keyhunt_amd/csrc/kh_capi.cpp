@@ -124,6 +124,18 @@ u256 sc_mul(const u256 &a, const u256 &b) {
     }
   return r;
 }
+// a^-1 mod n (Fermat, a^(n-2); a != 0).  Host only, per chunk at most
+u256 sc_inv(const u256 &a) {
+  u256 e;
+  u256_sub_raw(e, ORDER_N, u256_u64(2));
+  u256 r = u256_u64(1), x = a;
+  for (int i = 0; i < 4; i++)
+    for (int j = 0; j < 64; j++) {
+      if ((e.v[i] >> j) & 1) r = sc_mul(r, x);
+      x = sc_mul(x, x);
+    }
+  return r;
+}
 void u256_to_limbs(uint32_t out[8], const u256 &a) {
   for (int i = 0; i < 4; i++) {
     out[2 * i] = (uint32_t)a.v[i];
@@ -361,6 +373,7 @@ struct kh_ctx {
 
   // bsgs
   uint32_t l1_layout = KH_LAYER1_BLOCKED;
+  uint32_t bloom_mult = 1;   // -z (FLAGBLOOMMULTIPLIER) for the BSGS shards, kh_bsgs_set_bloom_multiplier
   bool bsgs_ready = false, bsgs_built = false;
   kh_bsgs_info info{};
   bloom_desc bd[3]{};
@@ -451,7 +464,8 @@ kh_ctx::~kh_ctx() {
 
 namespace {
 
-// lane centres for L lanes and an inversion pad of H entries per lane
+// lane centres for L lanes and an inversion pad of H rows per lane (walk_pad_rows: half the group for
+// the sparse-pad walks)
 int ensure_lanes(kh_ctx *c, uint32_t L, int H = KH_WALK_H) {
   if (L <= c->lanes_alloc && H <= c->scratch_h) return KH_OK;
   L = std::max(L, c->lanes_alloc);
@@ -812,6 +826,28 @@ int kh_set_vanity(kh_ctx *ctx, const uint8_t *ranges, uint64_t n, uint32_t probe
   return upload_tblk(ctx);
 }
 
+int kh_scan_memory(uint64_t n_keys, uint32_t mode, uint32_t search, uint64_t *needed_bytes) {
+  if (!needed_bytes || n_keys == 0) return KH_E_ARG;
+  const bool endo = (mode & KH_MODE_ENDO) != 0;
+  mode &= ~(uint32_t)KH_MODE_ENDO;
+  if (mode > KH_MODE_ETH || search > KH_SEARCH_BOTH) return KH_E_ARG;
+  int km = mode == KH_MODE_XPOINT ? KM_XPOINT
+         : mode == KH_MODE_ETH ? KM_ETH
+         : search == KH_SEARCH_COMPRESS ? KM_H160C
+         : search == KH_SEARCH_UNCOMPRESS ? KM_H160U
+                                          : KM_H160B;
+  if (endo) km |= KM_ENDO;
+  // kh_scan's choice at the default geometry (a chunk that reaches the order keeps the small groups,
+  // which need less): exact targets, so -m xpoint probes the blocked filter with the sparse pad
+  const int H = (km == KM_XPOINT || km == KM_H160C) && n_keys % (2 * KH_WALK_HB) == 0 ? KH_WALK_HB : KH_WALK_H;
+  const uint64_t lanes = H == KH_WALK_HB ? KH_LANES_HB : (1u << 18);
+  const uint64_t groups = (n_keys + 2 * H - 1) / (2 * H);
+  const uint64_t gpl = (groups + lanes - 1) / lanes, L = (groups + gpl - 1) / gpl;
+  *needed_bytes = L * (uint64_t)walk_pad_rows(km, true, H) * 32 + L * 32 * 3 + (512u << 10) +
+                  (uint64_t)65536 * sizeof(kh_dev_hit);
+  return KH_OK;
+}
+
 int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride_be[32], uint64_t n_keys, uint32_t mode,
             uint32_t search, kh_hit *hits, uint32_t cap, uint32_t *n_hits) {
   if (!ctx || !start || !n_hits || n_keys == 0) return KH_E_ARG;
@@ -827,13 +863,31 @@ int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride_be[32], u
   }
   if (!ctx->d_tbloom) return KH_E_STATE;
   (void)hipSetDevice(ctx->device);
-  if (zg && reaches_order(sc_reduce(u256_from_be(start)),
-                          stride_be ? sc_reduce(u256_from_be(stride_be)) : u256_u64(1), n_keys + 2 * (uint64_t)zg)) {
-    // k_walk_zinv advances each lane's centre by C += G*stride*D; where a centre meets -that (the
-    // next centre is the point at infinity, keys at the group order) the reference's own group is
-    // built from its infinity representation, which this engine does not restate
-    ctx->err = "--rmd-batch-size below 1024 on a chunk that reaches the group order";
-    return KH_E_RANGE;
+  if (zg) {
+    // k_walk_zinv centres group m on offset zg/2 + m*zg and reaches it by C += T[H] from the previous
+    // centre (or, a lane's first, by a scalar multiplication).  A centre whose key is 0 mod n -- offset
+    // k0 = -start * stride^-1 mod n -- is the point at infinity, from which the reference builds its
+    // group out of its own infinity representation; this engine does not restate that group.  The
+    // groups before it are scanned (and their hits returned), then the call reports KH_E_RANGE.
+    const u256 st0 = sc_reduce(u256_from_be(start));
+    const u256 sd0 = stride_be ? sc_reduce(u256_from_be(stride_be)) : u256_u64(1);
+    if (u256_is_zero(sd0)) return KH_E_ARG;
+    const u256 k0 = u256_cmp(sd0, u256_u64(1)) == 0 ? sc_neg(st0) : sc_mul(sc_neg(st0), sc_inv(sd0));
+    const uint64_t half = zg / 2, groups = (n_keys + zg - 1) / zg;
+    if (k0.v[1] == 0 && k0.v[2] == 0 && k0.v[3] == 0 && k0.v[0] >= half && (k0.v[0] - half) % zg == 0 &&
+        (k0.v[0] - half) / zg < groups) {
+      const uint64_t m_bad = (k0.v[0] - half) / zg;
+      uint32_t nh = 0;
+      int r0 = KH_OK;
+      if (m_bad) {
+        r0 = kh_scan(ctx, start, stride_be, m_bad * zg, mode | (endo ? KH_MODE_ENDO : 0), search, hits, cap, &nh);
+        if (r0 && r0 != KH_E_OVERFLOW) return r0;
+      }
+      *n_hits = nh;
+      ctx->err = "--rmd-batch-size below 1024: a group centred on the key 0 mod n (the reference builds it "
+                 "from its point at infinity); the groups before it were scanned";
+      return r0 == KH_E_OVERFLOW ? r0 : KH_E_RANGE;
+    }
   }
   int km = mode == KH_MODE_XPOINT ? KM_XPOINT
          : mode == KH_MODE_ETH ? KM_ETH
@@ -882,17 +936,26 @@ int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride_be[32], u
                       ctx->cont_L == jg.L && ctx->cont_H == H && u256_cmp(ctx->cont_next, st) == 0 &&
                       u256_cmp(ctx->cont_stride, stride) == 0;
   ctx->cont_valid = false;
+  // lane g's first centre: offset H + g * lane_step, lane_step = 2H (interleaved) or gpl * 2H; the
+  // scalars follow one another by one addition (a -R chunk restarts 2^20 lanes, and with a stride each
+  // mul_stride is a 128-step double-and-add)
+  const u256 lane_step = mul_stride(inter ? (u128)(2 * H) : (u128)jg.gpl * (2 * H));
+  auto lane_scalars = [&](std::vector<u256> &v) {
+    u256 c = sc_add(st, mul_stride((u128)H));
+    for (uint32_t g = 0; g < v.size(); g++, c = sc_add(c, lane_step)) v[g] = c;
+  };
   std::vector<u256> s(resume ? 0 : jg.L);
-  for (uint32_t g = 0; g < s.size(); g++) {
-    u128 off = inter ? (u128)g * (2 * H) + H : (u128)g * jg.gpl * (2 * H) + H;
-    s[g] = sc_add(st, mul_stride(off));
+  lane_scalars(s);
+  for (uint32_t g = 0; g < s.size(); g++)
     if (u256_is_zero(s[g])) {
       ctx->err = "lane centre scalar is 0 mod n";
       return KH_E_ARG;
     }
-  }
   if (!resume) {
-    r = ensure_lanes(ctx, jg.L, H);  // the pad for H entries per lane, before the centres are set
+    // the pad's rows per lane, before the centres are set (the walk below probes the blocked target
+    // filter exactly when A.tblk is set)
+    const bool tblk = !(ctx->vanity || getenv("KH_REF_TARGET_BLOOM")) && ctx->d_tblk;
+    r = ensure_lanes(ctx, jg.L, zg ? H : walk_pad_rows(km, tblk, H));  // km keeps KM_ENDO: as launch_walk sees it
     if (r) return r;
     r = run_setup(ctx, s, nullptr);
     if (r) return r;
@@ -938,7 +1001,7 @@ int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride_be[32], u
     A.hit_cap = ctx->hit_cap;
     if (s.empty()) {  // resumed lanes: compute their start scalars for the redo
       s.resize(jg.L);
-      for (uint32_t g = 0; g < jg.L; g++) s[g] = sc_add(st, mul_stride((u128)g * (2 * H) + H));
+      lane_scalars(s);
     }
     r = run_setup(ctx, s, nullptr);  // the walk moved the lane centres on: start them again
     if (r) return r;
@@ -1105,7 +1168,8 @@ int kh_bsgs_setup(kh_ctx *ctx, uint64_t n, uint64_t k, kh_bsgs_info *info) {
   it[1] = (m2 / 256 > 1000) ? (m2 / 256 + (m2 % 256 ? 1 : 0)) : 1000;
   it[2] = (m3 / 256 > 1000) ? (m3 / 256 + (m3 % 256 ? 1 : 0)) : 1000;
   for (int l = 0; l < 3; l++) {
-    ctx->entries[l] = bloom_entries(it[l]);
+    // initBloomFilter's entry count (keyhunt.cpp:7608): the 10000 floor, else -z x items
+    ctx->entries[l] = it[l] <= 10000 ? 10000 : (uint64_t)ctx->bloom_mult * it[l];
     ctx->bd[l] = bloom_size(ctx->entries[l]);
     ctx->bd_ref1 = l == 0 ? ctx->bd[0] : ctx->bd_ref1;
     ctx->bd_ref1.stride = (ctx->bd_ref1.bytes + 255) & ~255ULL;
@@ -1179,6 +1243,12 @@ int kh_bsgs_set_layer1(kh_ctx *ctx, uint32_t layout) {
   return KH_OK;
 }
 
+int kh_bsgs_set_bloom_multiplier(kh_ctx *ctx, uint32_t mult) {
+  if (!ctx || !mult) return KH_E_ARG;
+  ctx->bloom_mult = mult;
+  return KH_OK;
+}
+
 namespace {
 // the baby-step walk (thread_bPload, keyhunt.cpp:5284-5472): babies (i+1)G, i < M, into layer 1
 // (bl1/bd1, reference or blocked layout by `mode`), layers 2/3 (the context's) and the bP rows
@@ -1234,7 +1304,7 @@ int kh_bsgs_memory(kh_ctx *ctx, uint64_t *needed_bytes, uint64_t *held_bytes) {
   // list adds 32 B per base), and the build's transient row keys (m3 x 12 B).  A round whose
   // candidates overflow doubles its buffers on demand (up to 2^28 entries), which this figure cannot
   // foresee.
-  const uint64_t walk = L * (uint64_t)KH_WALK_HB * 32 + L * 32 * 3 + (512u << 10) + 4ull * ctx->cand_cap * 16 +
+  const uint64_t walk = L * (uint64_t)walk_pad_rows(KM_BSGSB, false, KH_WALK_HB) * 32 + L * 32 * 3 + (512u << 10) + 4ull * ctx->cand_cap * 16 +
                         (1ull << 16) * 32 + ctx->info.m3 * 12;
   if (needed_bytes) *needed_bytes = layers + walk;
   if (held_bytes)
@@ -1798,7 +1868,7 @@ int ensure_pipeline(kh_ctx *c, uint32_t L, int H) {
     }
     c->h_scal_cap = L;
   }
-  return ensure_lanes(c, L, H);
+  return ensure_lanes(c, L, walk_pad_rows(KM_BSGSB, false, H));  // the giant walks' sparse pad
 }
 
 // grow the per-round candidate buffers to hold `need` entries (stream must be idle)

@@ -248,6 +248,15 @@ struct refine_args {
 
 namespace kh {
 hipError_t launch_walk(int mode, const walk_args &A, hipStream_t st, int H = KH_WALK_H);
+// Inversion-pad rows per lane the walk launch_walk runs for (mode, blocked target filter) touches: the
+// sparse-pad walks (k_walk's SPARSE: the BSGS giant walks, -m xpoint against the blocked filter) keep
+// only the even prefix products, rows [0, H/2); the others all H
+inline int walk_pad_rows(int mode, bool tblk, int H) {
+  if (KH_XPOINT_DEFER && mode == KM_XPOINT && tblk) mode = KM_XPOINTB;
+  const bool sparse = KH_SPARSE_ALL || (KH_SPARSE_BSGS && (mode == KM_BSGSB || mode == KM_BSGS)) ||
+                      (KH_SPARSE_XPOINT && mode == KM_XPOINTB);
+  return sparse ? H / 2 : H;
+}
 hipError_t launch_walk_zinv(int mode, const walk_args &A, hipStream_t st);
 hipError_t launch_refine(const refine_args &A, hipStream_t st);
 hipError_t launch_setup(const setup_args &A, hipStream_t st);

@@ -201,6 +201,16 @@ class Engine:
         return [ScanHit(int.from_bytes(bytes(h.key), "big"), h.offset, h.kind, bool(h.compressed))
                 for h in hits[: n.value]]
 
+    def scan_status(self, start: int, n_keys: int, mode: int = KH_MODE_ADDRESS, search: int = KH_SEARCH_BOTH,
+                    stride: int = 1, cap: int = 4096) -> tuple[int, list[ScanHit]]:
+        """kh_scan returning (status, hits) instead of raising: a KH_E_RANGE call (--rmd-batch-size, a
+        group centred on the key 0 mod n) still returns the hits of the groups before it."""
+        hits = (KhHit * cap)()
+        n = ctypes.c_uint32(0)
+        r = lib().kh_scan(self._ctx, be32(start), be32(stride), n_keys, mode, search, hits, cap, ctypes.byref(n))
+        return r, [ScanHit(int.from_bytes(bytes(h.key), "big"), h.offset, h.kind, bool(h.compressed))
+                   for h in hits[: min(n.value, cap)]]
+
     # -- BSGS ----------------------------------------------------------------------------------
     def bsgs_setup(self, n: int, k: int, layer1: int = None) -> KhBsgsInfo:
         """layer1: KH_LAYER1_BLOCKED (default) or KH_LAYER1_REFERENCE (bit-identical to the reference)."""

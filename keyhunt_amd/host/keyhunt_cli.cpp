@@ -27,6 +27,7 @@
 #include <algorithm>
 #include <random>
 #include <atomic>
+#include <condition_variable>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -590,17 +591,23 @@ void addr_worker(addr_job *j) {
       r = kh_scan(ctx, st_be, stride_be, j->nseq, KH_MODE_ADDRESS | (opt.endo ? KH_MODE_ENDO : 0),
                   (uint32_t)opt.search, hits.data(), (uint32_t)hits.size(), &nh);
     }
-    if (r) {
+    // KH_E_RANGE (--rmd-batch-size, a group centred on the key 0 mod n): the hits of the groups
+    // before it are reported, then the worker stops
+    if (r && r != KH_E_RANGE) {
       fprintf(stderr, "[E] kh_scan: %s (%s)\n", kh_strerror(r), kh_last_error(ctx));
       break;
     }
-    for (uint32_t i = 0; i < nh; i++) {
+    for (uint32_t i = 0; i < nh && i < hits.size(); i++) {
       if ((hits[i].kind & 15u) == KH_KIND_ETH)
         writekeyeth(ctx, hits[i].key);
       else if (opt.mode == MODE_VANITY)
         writevanitykey(ctx, hits[i].compressed != 0, hits[i].key);
       else
         writekey(ctx, hits[i].compressed != 0, hits[i].key);
+    }
+    if (r) {
+      fprintf(stderr, "[E] kh_scan: %s (%s)\n", kh_strerror(r), kh_last_error(ctx));
+      break;
     }
     g_groups_done += (j->nseq + group - 1) / group;
   }
@@ -699,29 +706,47 @@ bool take_progression(const U &step, uint64_t want, U &start, uint64_t &count) {
 
 // --ptable-cache: FILE.md5 holds the file's MD5 as hex text; FILE.cache the 257 bucket starts of
 // the rows by value[0] under that MD5 (struct bptable_cache_file, keyhunt.cpp:137-143, 186-241).
-// With --load-ptable an existing FILE.md5 is trusted (1958-1981); otherwise the MD5 is computed
-// from the file and written.  A cache file of another MD5 or size is rebuilt (2655-2700).  Only
-// the files are produced: the engine's third check does not need the buckets.
-void ptable_cache(const uint8_t *rows, uint64_t m3, bool loaded) {
+// Two phases, where the reference has them: with --load-ptable, before the tables are built, an
+// existing FILE.md5 is trusted, else the MD5 is computed from the file and written (1956-1981);
+// after the tables (and the -S files), the MD5 is computed if it is not known yet, and the cache
+// file is checked and rebuilt when it is of another MD5 or size (2655-2700).  Only the files are
+// produced: the engine's third check does not need the buckets.
+uint8_t g_md5[16];
+bool g_md5_ready = false;
+
+void ptable_md5_loaded() {
+  if (!opt.ptable_cache || !opt.load_ptable || !opt.ptable) return;
+  const std::string md5_path = std::string(opt.ptable) + ".md5";
+  if (read_md5_file(md5_path.c_str(), g_md5)) {
+    g_md5_ready = true;
+    printf("[+] bP table MD5 loaded (%s)\n", md5_path.c_str());
+  } else if (md5_of_file(opt.ptable, g_md5)) {
+    g_md5_ready = true;
+    uint8_t disk[16];
+    if (read_md5_file(md5_path.c_str(), disk))
+      printf(memcmp(disk, g_md5, 16) == 0 ? "[+] bP table MD5 verified (%s)\n" : "[W] bP table MD5 mismatch (%s); refreshing\n",
+             md5_path.c_str());
+    if (!write_md5_file(md5_path.c_str(), g_md5))
+      fprintf(stderr, "[W] Unable to write bP table MD5 file %s\n", md5_path.c_str());
+  } else {
+    fprintf(stderr, "[W] Unable to compute MD5 for bP table %s\n", opt.ptable);
+  }
+}
+
+void ptable_cache(const uint8_t *rows, uint64_t m3) {
   if (!opt.ptable_cache) return;
   const std::string md5_path = std::string(opt.ptable) + ".md5", cache_path = std::string(opt.ptable) + ".cache";
-  uint8_t md5[16];
-  bool ready = false;
-  if (loaded) {
-    ready = read_md5_file(md5_path.c_str(), md5);
-    if (ready) printf("[+] bP table MD5 loaded (%s)\n", md5_path.c_str());
-  }
-  if (!ready) {
-    ready = md5_of_file(opt.ptable, md5);
-    if (ready) {
-      if (!write_md5_file(md5_path.c_str(), md5))
+  if (!g_md5_ready) {
+    g_md5_ready = md5_of_file(opt.ptable, g_md5);
+    if (g_md5_ready) {
+      if (!write_md5_file(md5_path.c_str(), g_md5))
         fprintf(stderr, "[W] Unable to write bP table MD5 file %s\n", md5_path.c_str());
     } else {
       fprintf(stderr, "[W] Unable to compute MD5 for bP table %s\n", opt.ptable);
     }
   }
-  if (!ready) return;
-  const int status = bptable_cache_status(cache_path.c_str(), md5, m3);
+  if (!g_md5_ready) return;
+  const int status = bptable_cache_status(cache_path.c_str(), g_md5, m3);
   if (status == 1) {
     printf("[+] bP table cache hit (%s)\n", cache_path.c_str());
     return;
@@ -730,7 +755,7 @@ void ptable_cache(const uint8_t *rows, uint64_t m3, bool loaded) {
     printf("[W] bP table cache mismatch (%s); rebuilding\n", cache_path.c_str());
   else
     printf("[I] bP table cache not found (%s); creating\n", cache_path.c_str());
-  if (bptable_cache_write(cache_path.c_str(), md5, rows, m3))
+  if (bptable_cache_write(cache_path.c_str(), g_md5, rows, m3))
     printf("[+] bP table cache refreshed (%s)\n", cache_path.c_str());
   else
     printf("[W] Unable to write bP table cache to %s\n", cache_path.c_str());
@@ -774,7 +799,7 @@ int bsgs_ptable(kh_ctx *ctx, const kh_bsgs_info &info, bool first) {
     }
     close(fd);
     int r = kh_bsgs_set_table(ctx, map, info.m3);
-    if (!r && first) ptable_cache(map, info.m3, true);
+    if (!r && first) ptable_cache(map, info.m3);
     if (map) munmap((void *)map, bytes);
     if (r) fprintf(stderr, "[E] %s\n", kh_last_error(ctx));
     return r;
@@ -814,8 +839,68 @@ int bsgs_ptable(kh_ctx *ctx, const kh_bsgs_info &info, bool first) {
     fprintf(stderr, "[E] Cannot write bP table file\n");
     return KH_E_IO;
   }
-  ptable_cache(rows, info.m3, false);
+  ptable_cache(rows, info.m3);
   return KH_OK;
+}
+
+// The reference's table-setup lines, which the first context's worker prints in the reference's order
+// (keyhunt.cpp:1631-1845, 2225-2503); every number follows from M, M2, M3 and the shard geometry.
+// The other workers wait for them (setup_done / setup_wait) before they print a base line.
+//
+// The three layers as initBloomFilter reports them (1687-1781 with 7605-7626): per layer the element
+// count, then per shard its item count and bloom_init2 size, then the layer's total.  The --mapped
+// path prints the same lines as it opens the shard files (kh_mapped.h bsgs_layers).
+void print_layer_lines(const kh_bsgs_info &I) {
+  const uint64_t ms[3] = {I.m, I.m2, I.m3}, floor_[3] = {10000, 1000, 1000};
+  for (int l = 0; l < 3; l++) {
+    const uint64_t items = ms[l] / 256 > floor_[l] ? ms[l] / 256 + (ms[l] % 256 ? 1 : 0) : 1000;
+    const uint64_t bytes = mapped::init2_bytes(items <= 10000 ? 10000 : (uint64_t)opt.bloom_mult * items);
+    printf("[+] Bloom filter for %llu elements ", (unsigned long long)ms[l]);
+    for (int i = 0; i < 256; i++) {
+      printf("[+] Bloom filter for %llu elements.\n", (unsigned long long)items);
+      printf("[+] Loading data to the bloomfilter total: %.2f MB\n", (double)bytes / 1048576.0);
+    }
+    printf(": %.2f MB\n", mapped::layer_mb(256 * bytes));
+  }
+}
+
+// 1845: the bP table's size, in whole MB (the integer division is the reference's)
+void print_allocating(const kh_bsgs_info &I) {
+  printf("[+] Allocating %.2f MB for %llu bP Points\n", (double)(I.m3 * 16 / 1048576), (unsigned long long)I.m3);
+}
+
+// The baby-step build (2362-2503): its progress lines as one reference thread (-t 1) prints them -- the
+// count before the work units start, again at the loop's first pass, after each finished unit of
+// THREADBPWORKLOAD = 1048576 babies (93, clamped to M) but the last, then the 100 % line (2457) -- the
+// checksums of the three layers, and the sort of the bP rows (not with --load-ptable, 2495).  With more
+// threads the reference's count lines depend on its threads' timing; these are the single-thread ones.
+void print_build_lines(const kh_bsgs_info &I) {
+  const uint64_t m = I.m, w = std::min<uint64_t>(1048576, m), units = m / w + (m % w ? 1 : 0);
+  auto count = [&](uint64_t f) {
+    printf("\r[+] processing %llu/%llu bP points : %i%%\r", (unsigned long long)f, (unsigned long long)m,
+           (int)(((double)f / (double)m) * 100));
+  };
+  count(0);
+  for (uint64_t u = 0; u < units; u++) count(u * w);
+  printf("\r[+] processing %llu/%llu bP points : 100%%     \n", (unsigned long long)m, (unsigned long long)m);
+  printf("[+] Making checkums .. ... done\n");
+  if (!opt.load_ptable) printf("[+] Sorting %llu elements... Done!\n", (unsigned long long)I.m3);
+}
+
+std::mutex g_setup_mtx;
+std::condition_variable g_setup_cv;
+bool g_setup_done = false;
+void setup_done() {
+  fflush(stdout);
+  {
+    std::lock_guard<std::mutex> lk(g_setup_mtx);
+    g_setup_done = true;
+  }
+  g_setup_cv.notify_all();
+}
+void setup_wait() {
+  std::unique_lock<std::mutex> lk(g_setup_mtx);
+  g_setup_cv.wait(lk, [] { return g_setup_done; });
 }
 
 // -S (keyhunt.cpp:1983-2230, 2504-2652): the files of this N/k in the working directory are read
@@ -824,9 +909,23 @@ int bsgs_tables(kh_ctx *ctx, const kh_bsgs_info &info, bool first) {
   if (opt.mapped) {  // -S is skipped with --mapped (keyhunt.cpp:1983); the shards live in files
     int r = kh_bsgs_build(ctx);
     if (!r && first && !mapped::bsgs_layers(ctx, info)) r = KH_E_IO;
+    if (!r && first) {
+      print_allocating(info);
+      ptable_md5_loaded();
+      print_build_lines(info);
+    }
     return r;
   }
-  if (!opt.save_read) return kh_bsgs_build(ctx);
+  if (first) {
+    print_layer_lines(info);
+    print_allocating(info);
+    ptable_md5_loaded();
+  }
+  if (!opt.save_read) {
+    int r = kh_bsgs_build(ctx);
+    if (!r && first) print_build_lines(info);
+    return r;
+  }
   char f4[96], f6[96], f7[96], f2[96];
   if (opt.load_ptable) {
     // -S with --load-ptable (keyhunt.cpp:2153-2186): the reference reads the .tbl into its
@@ -861,7 +960,7 @@ int bsgs_tables(kh_ctx *ctx, const kh_bsgs_info &info, bool first) {
       fprintf(stderr, "[E] %s\n", kh_last_error(ctx));
       return r;
     }
-    if (first) {
+    if (first) {  // 1994-2225: a dot per 64 shards; nothing is built, checked or sorted after it
       printf("[+] Reading bloom filter from file %s .... Done!\n", f4);
       printf("[+] Reading bloom filter from file %s .... Done!\n", f6);
       printf("[+] Reading bP Table from file %s .... Done!\n", f2);
@@ -871,6 +970,7 @@ int bsgs_tables(kh_ctx *ctx, const kh_bsgs_info &info, bool first) {
   }
   int r = kh_bsgs_build(ctx);
   if (r || !first) return r;
+  print_build_lines(info);
   r = kh_bsgs_save(ctx, ".");
   if (r) {
     fprintf(stderr, "[E] %s\n", kh_last_error(ctx));
@@ -1013,14 +1113,21 @@ void bsgs_worker(bsgs_job *j) {
   int r = kh_open(j->device, &ctx);
   if (r) {
     j->rc = r;
+    if (j->first) setup_done();
     g_running--;
     return;
   }
   kh_bsgs_info info;
   r = kh_bsgs_set_layer1(ctx, opt.layer1);
+  if (!r) r = kh_bsgs_set_bloom_multiplier(ctx, (uint32_t)opt.bloom_mult);
   if (!r) r = kh_bsgs_setup(ctx, j->n, j->k, &info);
   if (!r) r = bsgs_tables(ctx, info, j->first);
   if (!r) r = bsgs_ptable(ctx, info, j->first);
+  // the first worker has printed the setup lines (or failed): the others' base lines follow them
+  if (j->first)
+    setup_done();
+  else
+    setup_wait();
   size_t nt = j->tx->size();
   std::vector<uint8_t> xy(64 * nt);
   for (size_t i = 0; i < nt; i++) {
@@ -1491,6 +1598,26 @@ int main(int argc, char **argv) {
     if (!have_data)
       printf("[+] Sorting data ... done! %llu values were loaded and sorted\n", (unsigned long long)(rows.size() / 20));
     if (!open_devices()) return EXIT_FAILURE;
+    {
+      // contexts stacked on one device must fit its free memory (each holds its own inversion pad,
+      // kh_scan_memory): checked before any is opened, as bsgsd-amd checks its BSGS tables
+      const uint32_t smode = opt.mode == MODE_XPOINT ? KH_MODE_XPOINT
+                             : (opt.eth && (opt.mode == MODE_ADDRESS || opt.mode == MODE_RMD160)) ? KH_MODE_ETH
+                                                                                                   : KH_MODE_ADDRESS;
+      uint64_t need = 0;
+      if (kh_scan_memory(nseq, smode | (opt.endo ? KH_MODE_ENDO : 0), (uint32_t)opt.search, &need) == KH_OK) {
+        for (int dev = 0; dev < ndev && dev < gpus; dev++) {
+          const uint64_t per = (uint64_t)(gpus / ndev + (dev < gpus % ndev ? 1 : 0));
+          uint64_t fr = 0, tot = 0;
+          if (kh_device_memory(dev, &fr, &tot) == KH_OK && fr && per * need > fr) {
+            fprintf(stderr, "[E] -g %d: %llu context(s) on GPU %d need %.1f GB of device memory (%.1f GB each), "
+                            "%.1f GB are free; use fewer contexts (-g) or a smaller -n\n",
+                    gpus, (unsigned long long)per, dev, per * need / 1e9, need / 1e9, fr / 1e9);
+            return EXIT_FAILURE;
+          }
+        }
+      }
+    }
     g_running = gpus;
     for (int d = 0; d < gpus; d++) {
       aj[d].device = d % ndev;
@@ -1565,6 +1692,7 @@ int main(int argc, char **argv) {
     printf("[+] N = 0x%llx\n", (unsigned long long)Nr);
     // GGSB block geometry from sqrt(N) (keyhunt.cpp:1477-1499) and the base step (1617-1627)
     g_step = twoN;
+    uint64_t ggsb_blocks = 1, ggsb_babies = M;
     if (opt.ggsb) {
       uint64_t bc = opt.ggsb_count, bs = opt.ggsb_size;
       if (bc == 0 && bs == 0) bc = 1;
@@ -1575,8 +1703,18 @@ int main(int argc, char **argv) {
       if (bc == 0) bc = 1;
       if (bs == 0) bs = m;
       if (bc > 1 && bs) g_step = u_mul_u64(u_from_u64(bs), 2);
+      ggsb_blocks = bc > 1 ? bc : 1;
+      if (bs) ggsb_babies = bs;
+    }
+    {
+      // keyhunt.cpp:1663-1685 (stderr): the build's layout and the expected layer / table sizes
+      const uint64_t items = M / 256 > 10000 ? M / 256 + (M % 256 ? 1 : 0) : 1000;
+      const long double err = opt.mapped && opt.mapped_error ? opt.mapped_error : 0.000001L;
+      const double shard_mb = (double)mapped::bytes_for(items, err) / 1048576.0;
       fprintf(stderr, "[i] BSGS table build: %s layout, creating %llu block(s) of %llu babies each.\n",
-              bc > 1 ? "GGSB" : "classic", (unsigned long long)bc, (unsigned long long)bs);
+              ggsb_blocks > 1 ? "GGSB" : "classic", (unsigned long long)ggsb_blocks, (unsigned long long)ggsb_babies);
+      fprintf(stderr, "[i] Expected sizes: each bloom layer ~%.2f MB (256 shards), bPtable ~%.2f MB per block (%.2f MB total).\n",
+              shard_mb * 256.0, (double)(ggsb_babies * 16) / 1048576.0, (double)(M * 16) / 1048576.0);
     }
     if (!open_devices()) return EXIT_FAILURE;
     g_running = gpus;

@@ -55,6 +55,18 @@ inline uint64_t bytes_for(uint64_t entries, long double error) {
   uint64_t bits = u64_of(allbits);
   return bits / 8 + ((bits % 8) ? 1 : 0);
 }
+// bloom_init2's byte count (bloom/bloom.cpp:154-187): bpe kept as a double (struct bloom's field),
+// bits = entries x bpe in long double; the size initBloomFilter's "Loading data" line reports
+inline uint64_t init2_bytes(uint64_t entries) {
+  long double num = -logl(0.000001L);
+  long double denom = 0.480453013918201;
+  const double bpe = (double)(num / denom);
+  const uint64_t bits = u64_of((long double)entries * bpe);
+  return bits / 8 + ((bits % 8) ? 1 : 0);
+}
+// the layer totals keyhunt prints after the 256 shards of a layer, computed in float
+// (keyhunt.cpp:1719, 1750, 1781; bsgsd.cpp:1200, 1222, 1244)
+inline double layer_mb(uint64_t total) { return (double)(float)((float)total / (float)1048576); }
 // bloom_entries_for_bytes (keyhunt.cpp:7510-7530) == entries_hashes_for_bytes (bloom.cpp:465-489)
 inline void entries_for(uint64_t bytes, uint64_t *entries, uint32_t *hashes) {
   uint64_t best_n = 0;
@@ -208,10 +220,10 @@ inline bool save(const filter &F) {
 // initBloomFilterMapped (keyhunt.cpp:7630-7706; bsgsd.cpp:584-656), FLAGMAPPED set: load or create
 // the filter of `items` elements; fname names a BSGS shard file, else --mapped/--bloom-file or
 // bloom.dat
-inline bool open_filter(filter &F, uint64_t items, const char *fname, bool quiet = false) {
+inline bool open_filter(filter &F, uint64_t items, const char *fname) {
   F.name = fname ? fname : (cfg.name ? cfg.name : "bloom.dat");
   F.chunks = cfg.chunks ? cfg.chunks : 1;
-  if (!quiet) printf("[+] Bloom filter for %llu elements.\n", (unsigned long long)items);
+  printf("[+] Bloom filter for %llu elements.\n", (unsigned long long)items);
   if (cfg.load_bloom) {
     struct stat st;
     if (cfg.bsgsd ? (stat(F.file(0).c_str(), &st) != 0 || st.st_size == 0) : !exists(F.file(0))) {
@@ -298,11 +310,11 @@ inline bool bsgs_layers(kh_ctx *ctx, const kh_bsgs_info &I) {
   std::vector<std::vector<filter>> F(3, std::vector<filter>(256));
   for (int l = 0; l < 3; l++) {
     const uint64_t items = ms[l] / 256 > floor_[l] ? ms[l] / 256 + (ms[l] % 256 ? 1 : 0) : 1000;
-    if (cfg.bsgsd) printf("[+] Bloom filter for %llu elements ", (unsigned long long)ms[l]);
+    printf("[+] Bloom filter for %llu elements ", (unsigned long long)ms[l]);
     uint64_t total = 0;
     for (int i = 0; i < 256; i++) {
       const std::string fn = pfx[l] + std::to_string(i) + ".dat";
-      if (!open_filter(F[l][i], items, fn.c_str(), !cfg.bsgsd)) {
+      if (!open_filter(F[l][i], items, fn.c_str())) {
         if (cfg.bsgsd)
           fprintf(stderr, l < 2 ? "[E] error bloom_init _ %i\n" : "[E] error bloom_init %i\n", i);
         else
@@ -312,10 +324,10 @@ inline bool bsgs_layers(kh_ctx *ctx, const kh_bsgs_info &I) {
         open_failed = true;
         return false;
       }
-      if (cfg.bsgsd) printf("[+] Loading data to the bloomfilter total: %.2f MB\n", (double)F[l][i].bytes / 1048576.0);
+      printf("[+] Loading data to the bloomfilter total: %.2f MB\n", (double)F[l][i].bytes / 1048576.0);
       total += F[l][i].bytes;
     }
-    if (cfg.bsgsd) printf(": %.2f MB\n", (double)total / 1048576.0);
+    printf(": %.2f MB\n", layer_mb(total));
   }
   for (int l = 0; l < 3; l++) {
     // one GPU pass per distinct shard geometry
@@ -341,13 +353,8 @@ inline bool bsgs_layers(kh_ctx *ctx, const kh_bsgs_info &I) {
         done[j] = true;
       }
     }
-    uint64_t total = 0;
-    for (int i = 0; i < 256; i++) {
+    for (int i = 0; i < 256; i++)
       if (!save(F[l][i])) return false;
-      total += F[l][i].bytes;
-    }
-    if (!cfg.bsgsd)
-      printf("[+] Bloom filter for %llu elements : %.2f MB\n", (unsigned long long)ms[l], (double)total / 1048576.0);
   }
   return true;
 }

@@ -608,6 +608,23 @@ STDOUT_RUNS = [
     ("bsgs_two_M", ["-m", "bsgs", "-f", "bsgs_two_targets.txt", "-n", "0x100000", "-r", "7cce5efdac000000:7cce5efdad000000", "-M"]),
     ("bsgs_two_verbose", ["-m", "bsgs", "-f", "bsgs_two_targets.txt", "-n", "0x100000", "-r", "7cce5efdac000000:7cce5efdad000000"]),
 ]
+# BSGS runs whose table-setup lines take other paths (keyhunt.cpp:1631-2700): -z above the 10000-item
+# floor, and sequences run in ONE directory -- -S building then reading its files, --mapped creating
+# then reloading its shard files, --ptable with --ptable-cache writing then --load-ptable reading
+STDOUT_RUNS += [
+    # the key is the last giant-step key of base 2 (base 2 + 2N), i.e. exactly base 3's start, which base 3
+    # cannot reach (offset 0): the found line follows base 2's progress line
+    ("bsgs_63_key_on_boundary_M", ["-m", "bsgs", "-f", "63.pub", "-n", "0x100000", "-r", "7cce5efdac6f6808:7cce5efdad6f6808", "-M"]),
+    ("bsgs_63_key_on_boundary_verbose", ["-m", "bsgs", "-f", "63.pub", "-n", "0x100000", "-r", "7cce5efdac6f6808:7cce5efdad6f6808"]),
+    ("bsgs_63_z2_M", ["-m", "bsgs", "-f", "63.pub", "-k", "2", "-z", "2", "-r", "7cce5a0000000000:7cce9a0000000000", "-M"]),
+]
+_SMALL = ["-m", "bsgs", "-f", "63.pub", "-n", "0x1000000", "-k", "2", "-r", "7cce5efdac000000:7cce5efdad000000", "-M"]
+STDOUT_SEQS = [
+    ("bsgs_S_build_then_read", [_SMALL + ["-S"], _SMALL + ["-S"]]),
+    ("bsgs_mapped_fresh_then_reload", [_SMALL + ["--mapped"], _SMALL + ["--mapped"]]),
+    ("bsgs_ptable_cache_then_load", [_SMALL + ["--ptable", "c.tbl", "--ptable-cache"],
+                                     _SMALL + ["--ptable", "c.tbl", "--ptable-cache", "--load-ptable"]]),
+]
 # the stats line (keyhunt.cpp:2904-2950) with and without -M: runs stopped after a few seconds; the
 # fixture keeps the lines, the test compares their shape (numbers are the run's)
 STATS_RUNS = [
@@ -617,17 +634,36 @@ STATS_RUNS = [
 STATS_LINE = re.compile(rb"\r?\[\+\] Total \d+ keys in \d+ seconds: [^\r\n]*[\r\n]")
 
 
-def gen_stdout():
+def gen_stdout(only: list[str] | None = None):
+    """--stdout [--only NAME ...]: with --only, just those fixtures are rerun and merged into the file."""
     subprocess.run(["make", "-s", "-C", HERE, "-f", "Makefile.ref", "-j8"], check=True)
-    res = {"_generator": "oracle/make_golden.py --stdout running oracle/_ref/keyhunt -t 1 -s 0"}
+    out = os.path.join(REPO, "tests", "golden", "ref_stdout.json")
+    res = json.load(open(out)) if only else {}
+    res["_generator"] = "oracle/make_golden.py --stdout running oracle/_ref/keyhunt -t 1 -s 0"
     for name, argv in STDOUT_RUNS:
+        if only and name not in only:
+            continue
         with tempfile.TemporaryDirectory() as td:
             for fn in os.listdir(DATA):
                 shutil.copy(os.path.join(DATA, fn), td)
             p = subprocess.run(["timeout", "300", REF_BIN] + argv + ["-t", "1", "-s", "0"], cwd=td, capture_output=True)
         res[name] = {"argv": argv, "exit": p.returncode, "stdout": p.stdout.decode("latin-1")}
         print(name, p.returncode, len(p.stdout), flush=True)
+    for name, argvs in STDOUT_SEQS:
+        if only and name not in only:
+            continue
+        runs = []
+        with tempfile.TemporaryDirectory() as td:
+            for fn in os.listdir(DATA):
+                shutil.copy(os.path.join(DATA, fn), td)
+            for argv in argvs:
+                p = subprocess.run(["timeout", "300", REF_BIN] + argv + ["-t", "1", "-s", "0"], cwd=td, capture_output=True)
+                runs.append({"argv": argv, "exit": p.returncode, "stdout": p.stdout.decode("latin-1")})
+        res[name] = {"seq": runs}
+        print(name, [(r["exit"], len(r["stdout"])) for r in runs], flush=True)
     for name, argv, secs in STATS_RUNS:
+        if only and name not in only:
+            continue
         with tempfile.TemporaryDirectory() as td:
             for fn in os.listdir(DATA):
                 shutil.copy(os.path.join(DATA, fn), td)
@@ -635,7 +671,7 @@ def gen_stdout():
         lines = [m.decode("latin-1") for m in STATS_LINE.findall(p.stdout)]
         res[name] = {"argv": argv, "stats_lines": lines}
         print(name, lines, flush=True)
-    with open(os.path.join(REPO, "tests", "golden", "ref_stdout.json"), "w") as f:
+    with open(out, "w") as f:
         json.dump(res, f, indent=1)
 
 
@@ -668,4 +704,4 @@ if __name__ == "__main__":
     if a.bsgsd_mapped:
         gen_bsgsd_mapped()
     if a.stdout:
-        gen_stdout()
+        gen_stdout(a.only)

@@ -115,12 +115,64 @@ def test_engine_rmd_batch_centre_on_the_jump(engine, oracle, G):
     assert sorted((h.key, h.compressed, h.kind) for h in got) == sorted(ref)
 
 
-def test_engine_rmd_batch_refuses_chunks_reaching_the_order(engine, oracle):
-    from keyhunt_amd.engine import KhError
-    engine.set_targets([bytes(20)])
-    engine.set_rmd_batch(512)
+def test_engine_rmd_batch_scans_up_to_the_zero_centre(engine, oracle):
+    """A chunk whose group m is centred on the key 0 mod n (the reference builds that group from its
+    point at infinity, which the engine does not restate): the groups before it are scanned and their
+    hits returned, with KH_E_RANGE for the rest."""
+    G, m_bad = 512, 3
+    start = ORDER_N - (G // 2 + m_bad * G)
+    rng = random.Random(77)
+    rows = _targets(oracle, start, m_bad * G, G, rng, n=16)
+    engine.set_targets(rows)
+    engine.set_rmd_batch(G)
     try:
-        with pytest.raises(KhError):
-            engine.scan(ORDER_N - 1000, 4096, mode=0, search=0)
+        r, got = engine.scan_status(start, 8 * G, mode=0, search=2)
     finally:
         engine.set_rmd_batch(1024)
+    assert r == -7  # KH_E_RANGE
+    ref = oracle.scan_chunk(0, 2, start, m_bad * G, rows, group=G)
+    assert ref
+    assert sorted((h.key, h.compressed, h.kind) for h in got) == sorted(ref)
+
+
+def test_engine_rmd_batch_near_the_order_without_a_zero_centre(engine, oracle):
+    """A chunk that ends past the order but centres no group on the key 0 mod n is scanned (the old
+    guard refused every chunk reaching the order): its groups below the order give the oracle's hits."""
+    G = 512
+    start = ORDER_N - 1000  # offset 1000 holds key 0: (1000 - 256) % 512 != 0, no group centred there
+    rng = random.Random(78)
+    rows = _targets(oracle, start, G, G, rng, n=8)  # the first group, wholly below the order
+    engine.set_targets(rows)
+    engine.set_rmd_batch(G)
+    try:
+        r, got = engine.scan_status(start, G, mode=0, search=2)
+        r2, _ = engine.scan_status(start, 4 * G, mode=0, search=2)
+    finally:
+        engine.set_rmd_batch(1024)
+    assert r == 0 and r2 == 0
+    ref = oracle.scan_chunk(0, 2, start, G, rows, group=G)
+    assert ref
+    assert sorted((h.key, h.compressed, h.kind) for h in got) == sorted(ref)
+
+
+def test_engine_rmd_batch_wrapping_stride(engine, oracle):
+    """-I strides that wrap the order many times per chunk (every such chunk was
+    refused).  Centres are real points: a centre planted as a target is found with its key
+    start + (G/2 + m G) * stride mod n.  (Parity with the reference for keys past the order, which it
+    keeps unreduced, is unpinned: no fixture holds such a run.)"""
+    G = 512
+    stride = (1 << 230) + 12345
+    start = 0x1234567890ABCDEF
+    centres = [(start + (G // 2 + m * G) * stride) % ORDER_N for m in (0, 5, 17)]
+    rows = []
+    for c in centres:
+        x, y = oracle.pubkey(c)
+        rows.append(oracle.hash160_comp(x, 2 + (y & 1)))
+    engine.set_targets(rows)
+    engine.set_rmd_batch(G)
+    try:
+        r, got = engine.scan_status(start, 32 * G, mode=0, search=0, stride=stride)
+    finally:
+        engine.set_rmd_batch(1024)
+    assert r == 0
+    assert sorted(h.key for h in got) == sorted(centres)

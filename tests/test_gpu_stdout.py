@@ -7,7 +7,9 @@ reference's byte for byte with -M (keyhunt.cpp:3333-3336, 4619-4624: one line pe
 as a terminal shows it without -M (3340-3345, 4626-4631: lines rewritten in place with \\r; the engine
 prints the overlay of a call's lines once, tests/_cli.render).  The stats line keeps the reference's
 shape and terminators (2904-2950): its own line with -M, rewritten in place without.  The header before
-the run section (option echoes, table-build progress) is the engine's own."""
+the run section -- option echoes, target loading, BSGS table-setup lines (keyhunt.cpp:1687-1845,
+2225-2503) -- equals the reference's line for line; only the version line and the engine's device
+count ("[+] GPUs : ...") are its own."""
 import json
 import os
 import re
@@ -49,11 +51,31 @@ def test_run_section_matches_reference(name):
     assert render(got) == render(want)
     if "-M" in ref["argv"]:  # one line per chunk / base: the bytes themselves
         assert got == want
-    # the header too (tests/test_cli_output.py checks it without a GPU): the engine's own lines are
-    # its version and the device count; BSGS compares up to "[+] N = " (then the tables are built)
-    bsgs = "bsgs" in ref["argv"]
-    head = [l for l in _header_lines(out, bsgs) if not l.startswith("[+] GPUs : ")]
-    assert head == _header_lines(ref["stdout"], bsgs)
+    # the whole header too, BSGS table-setup lines included (tests/test_cli_output.py checks the part
+    # before "[+] N = " without a GPU): the engine's own lines are its version and the device count
+    head = [l for l in _header_lines(out) if not l.startswith("[+] GPUs : ")]
+    assert head == _header_lines(ref["stdout"])
+
+
+SEQS = [k for k in REF if not k.startswith("_") and "seq" in REF[k]]
+
+
+@pytest.mark.parametrize("name", SEQS)
+def test_sequence_matches_reference(name):
+    """Runs that share one directory (-S building then reading its table files, --mapped creating then
+    reloading its shard files, --ptable with --ptable-cache then --load-ptable): each run's whole stdout
+    equals the reference CLI's, the setup lines of the path it takes included."""
+    with tempfile.TemporaryDirectory() as td:
+        for fn in os.listdir(DATA):
+            shutil.copy(os.path.join(DATA, fn), td)
+        for i, ref in enumerate(REF[name]["seq"]):
+            p = subprocess.run([CLI] + ref["argv"] + ["-t", "1", "-s", "0", "-g", "1"], cwd=td, capture_output=True,
+                               timeout=300)
+            assert p.returncode == ref["exit"], (i, p.stdout[-2000:] + p.stderr[-2000:])
+            out = p.stdout.decode("latin-1")
+            assert run_section(out) == run_section(ref["stdout"]), i
+            head = [l for l in _header_lines(out) if not l.startswith("[+] GPUs : ")]
+            assert head == _header_lines(ref["stdout"]), i
 
 
 def _shape(line: str) -> str:
