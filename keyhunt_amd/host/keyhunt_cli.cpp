@@ -528,6 +528,31 @@ bool data_file_name(const char *fn, std::string &name) {
   return true;
 }
 
+// writeFileIfNeeded (keyhunt.cpp:7756-7855) when the target filter lives in a mapped file (-S with
+// --mapped): sha256(bits) | that filter's struct bloom (kh_mapped.h struct_bloom) | its bits |
+// sha256(rows) | u64 row bytes | the 20-byte rows sorted.  (Without --mapped the engine writes the
+// file from its own filter, kh_targets_save.)
+bool write_mapped_data_file(const std::string &path, const mapped::filter &F, const std::vector<uint8_t> &rows) {
+  const size_t n = rows.size() / 20;
+  std::vector<uint32_t> ix(n);
+  for (size_t i = 0; i < n; i++) ix[i] = (uint32_t)i;
+  std::sort(ix.begin(), ix.end(), [&](uint32_t a, uint32_t b) { return memcmp(&rows[20 * (size_t)a], &rows[20 * (size_t)b], 20) < 0; });
+  std::vector<uint8_t> srt(rows.size());
+  for (size_t i = 0; i < n; i++) memcpy(&srt[20 * i], &rows[20 * (size_t)ix[i]], 20);
+  const uint64_t data_size = srt.size();
+  uint8_t ckb[32], ckd[32], h[112];
+  sha256(F.bf.data(), F.bytes, ckb);
+  sha256(srt.data(), srt.size(), ckd);
+  mapped::struct_bloom(F, h);
+  FILE *f = fopen(path.c_str(), "wb");
+  if (!f) return false;
+  bool ok = fwrite(ckb, 1, 32, f) == 32 && fwrite(h, 1, 112, f) == 112 &&
+            (F.bytes == 0 || fwrite(F.bf.data(), 1, F.bytes, f) == F.bytes) && fwrite(ckd, 1, 32, f) == 32 &&
+            fwrite(&data_size, 1, 8, f) == 8 && (data_size == 0 || fwrite(srt.data(), 1, data_size, f) == data_size);
+  ok = fclose(f) == 0 && ok;
+  return ok;
+}
+
 void addr_worker(addr_job *j) {
   kh_ctx *ctx = nullptr;
   int r = kh_open(j->device, &ctx);
@@ -545,6 +570,7 @@ void addr_worker(addr_job *j) {
   else
     r = kh_set_targets(ctx, j->rows->data(), j->rows->size() / 20, j->bloom_items);
   if (!r && j->save_data) {
+    printf("[D] size data %llu\n", (unsigned long long)(j->rows->size()));  // keyhunt.cpp:7773
     printf("[+] Writing file %s ........\n", j->data_file);
     r = kh_targets_save(ctx, j->data_file);
   }
@@ -1568,10 +1594,17 @@ int main(int argc, char **argv) {
         printf("[+] Reading file %s\n", data_file.c_str());
       }
     }
-    if (opt.mapped && opt.save_read && opt.mode != MODE_VANITY) {
-      fprintf(stderr, "[E] -S together with --mapped is not provided by this engine\n");
+    // -S with --mapped and no cache yet: the target filter is the mapped file's (bloom.dat, or the
+    // --mapped / --bloom-file name), and that filter -- its struct bloom and bits -- goes into the
+    // data file (keyhunt.cpp:7033-7049, 7630-7706, 7756-7855).  With --mapped-chunks above 1 the
+    // reference writes bloom.bytes from its FIRST chunk's mapping, past that mapping's end: refused
+    const bool mapped_data = opt.mapped && opt.save_read && opt.mode != MODE_VANITY && !have_data;
+    if (mapped_data && opt.mapped_chunks > 1) {
+      fprintf(stderr, "[E] -S with --mapped-chunks above 1: the reference writes the data file from its first chunk's "
+                      "mapping past that mapping's end; not provided\n");
       return EXIT_FAILURE;
     }
+    mapped::filter tf;
     std::vector<uint8_t> adds;  // the items the reference adds to its (mapped) target bloom
     std::vector<uint8_t> *addp = opt.mapped ? &adds : nullptr;
     if (have_data) {
@@ -1591,12 +1624,21 @@ int main(int argc, char **argv) {
           adds.insert(adds.end(), opt.vanity.ranges.begin() + j, opt.vanity.ranges.begin() + j + L);
         ok = mapped::targets(opt.vanity.total, adds, L);
       } else {
-        ok = mapped::targets(items, adds, 20);
+        ok = mapped::targets(items, adds, 20, mapped_data ? &tf : nullptr);
       }
       if (!ok) return EXIT_FAILURE;
     }
     if (!have_data)
       printf("[+] Sorting data ... done! %llu values were loaded and sorted\n", (unsigned long long)(rows.size() / 20));
+    if (mapped_data) {
+      printf("[D] size data %llu\n", (unsigned long long)rows.size());
+      if (!write_mapped_data_file(data_file, tf, rows)) {
+        fprintf(stderr, "[E] Error writing file %s\n", data_file.c_str());
+        return EXIT_FAILURE;
+      }
+      printf("[+] Writing file %s ........\n", data_file.c_str());
+      data_file.clear();  // the contexts take their targets from the rows
+    }
     if (!open_devices()) return EXIT_FAILURE;
     {
       // contexts stacked on one device must fit its free memory (each holds its own inversion pad,

@@ -115,6 +115,9 @@ struct filter {
   uint32_t chunks = 1;
   uint64_t bits = 0, bytes = 0;
   uint32_t hashes = 0;
+  uint64_t entries = 0;             // struct bloom's entries, error and bpe as the mapping left them
+  long double error = 0;
+  double bpe = 0;
   std::vector<uint64_t> chunk_bytes;  // size of each file
   std::vector<uint8_t> bf;          // flat bit array
   std::string file(uint32_t i) const { return chunks > 1 ? name + "." + std::to_string(i) : name; }
@@ -144,8 +147,9 @@ inline bool load(filter &F) {
   }
   F.bytes = F.bf.size();
   F.bits = F.bytes * 8;
-  uint64_t entries;
-  entries_for(F.bytes, &entries, &F.hashes);
+  entries_for(F.bytes, &F.entries, &F.hashes);
+  F.bpe = (double)F.bits / (double)F.entries;
+  F.error = powl(0.5L, (long double)F.hashes);
   return true;
 }
 
@@ -156,6 +160,9 @@ inline bool init(filter &F, uint64_t entries, long double error, bool resize) {
   long double num = -logl(error);
   long double denom = 0.480453013918201;
   const double bpe = (double)(num / denom);
+  F.entries = entries;
+  F.error = error;
+  F.bpe = bpe;
   F.bits = u64_of((long double)entries * bpe);
   F.bytes = F.bits / 8 + ((F.bits % 8) ? 1 : 0);
   F.hashes = (uint32_t)(uint8_t)ceil(0.693147180559945 * bpe);
@@ -289,13 +296,38 @@ inline int create() {
   return save(F) ? EXIT_SUCCESS : EXIT_FAILURE;
 }
 
-// a target filter (address / rmd160 / xpoint / eth / vanity): open it, add the items, write it back
-inline bool targets(uint64_t items, const std::vector<uint8_t> &adds, uint32_t len) {
+// struct bloom (bloom/bloom.h, 112 bytes on x86-64) of a mapped filter of ONE file as bloom_init_mmap /
+// bloom_load_mmap leave it (bloom.cpp:491-578, 589-724): what writeFileIfNeeded stores in data_<hex>.dat
+// when -S meets --mapped (keyhunt.cpp:7756-7855).  The mapping's address (bf) is written as 0; bf_chunks
+// is NULL for one file.
+inline void struct_bloom(const filter &F, uint8_t h[112]) {
+  memset(h, 0, 112);
+  memcpy(h + 0, &F.entries, 8);
+  memcpy(h + 8, &F.bits, 8);
+  memcpy(h + 16, &F.bytes, 8);
+  h[24] = (uint8_t)F.hashes;
+  const long double e = F.error;
+  memcpy(h + 32, &e, 10);  // the x87 value; its 6 padding bytes stay 0, as the memset left them
+  h[48] = 1;               // ready, BLOOM_VERSION_MAJOR 2, _MINOR 201
+  h[49] = 2;
+  h[50] = 201;
+  memcpy(h + 56, &F.bpe, 8);
+  const uint32_t mc = 1;
+  memcpy(h + 80, &mc, 4);
+  memcpy(h + 88, &F.bytes, 8);  // chunk_bytes, last_chunk_bytes
+  memcpy(h + 96, &F.bytes, 8);
+}
+
+// a target filter (address / rmd160 / xpoint / eth / vanity): open it, add the items, write it back;
+// out: the filter as the reference's run holds it afterwards (for -S's data file)
+inline bool targets(uint64_t items, const std::vector<uint8_t> &adds, uint32_t len, filter *out = nullptr) {
   filter F;
   if (!open_filter(F, items, nullptr)) return false;
   if (kh_bloom_add(F.bf.data(), F.bits, F.hashes, adds.data(), adds.size() / len, len) != KH_OK) return false;
   printf("[+] Loading data to the bloomfilter total: %.2f MB\n", (double)F.bytes / 1048576.0);
-  return save(F);
+  if (!save(F)) return false;
+  if (out) *out = std::move(F);
+  return true;
 }
 
 // the BSGS layers (keyhunt.cpp:1631-1785; bsgsd.cpp:1180-1255): 3 x 256 shard files bloom-%u.dat,

@@ -535,6 +535,13 @@ MAPPED_SEQS = [
                     "--mapped"]]),
     ("bsgs_fresh_then_reload", [BSGS_ARGS + ["--mapped"], BSGS_ARGS + ["--mapped"]]),
     ("bsgs_size_override", [BSGS_ARGS + ["--mapped-size", "64k"]]),
+    # -S with --mapped: a fresh run maps bloom.dat and writes data_<hex>.dat from that filter; a rerun reads
+    # the data file and leaves bloom.dat alone; after a plain --mapped run the -S run reloads bloom.dat with
+    # its size-derived geometry, which goes into the data file, and a plain -S run then reads that file
+    ("rmd160_S_mapped_fresh_then_reload", [RMD_ARGS + ["-S", "--mapped"], RMD_ARGS + ["-S", "--mapped"]]),
+    ("rmd160_mapped_then_S_mapped_then_S", [RMD_ARGS + ["--mapped"], RMD_ARGS + ["-S", "--mapped"], RMD_ARGS + ["-S"]]),
+    ("xpoint_S_mapped_override", [["-m", "xpoint", "-f", "1to63_65.txt", "-r", "1:100000", "-n", "0x100000", "-t", "4",
+                                   "-S", "--mapped", "--mapped-size", "1m"]]),
 ]
 
 
@@ -545,6 +552,8 @@ def mapped_files(d: str) -> dict:
         m = re.match(r"(bloom2?3?-)(\d+)\.dat$", f)
         if m:
             layers.setdefault(m.group(1), {})[int(m.group(2))] = f
+        elif f.startswith("data_") and f.endswith(".dat"):  # -S target cache: its mmap pointer masked
+            out[f] = [os.path.getsize(os.path.join(d, f)), masked_data_digest(os.path.join(d, f))]
         elif f.endswith(".dat") or re.search(r"\.dat\.\d+$", f):
             b = open(os.path.join(d, f), "rb").read()
             out[f] = [len(b), hashlib.sha256(b).hexdigest()]
@@ -559,10 +568,15 @@ def mapped_files(d: str) -> dict:
     return out
 
 
-def gen_mapped() -> None:
+def gen_mapped(only: list[str] | None = None) -> None:
+    """--mapped [--only NAME ...]: with --only, just those sequences are rerun and merged into the file."""
     subprocess.run(["make", "-s", "-C", HERE, "-f", "Makefile.ref", "-j8"], check=True)
-    res = {"_generator": "oracle/make_golden.py --mapped running oracle/_ref/keyhunt"}
+    out_path = os.path.join(REPO, "tests", "golden", "ref_mapped.json")
+    res = json.load(open(out_path)) if only else {}
+    res["_generator"] = "oracle/make_golden.py --mapped running oracle/_ref/keyhunt"
     for name, runs in MAPPED_SEQS:
+        if only and name not in only:
+            continue
         steps = []
         with tempfile.TemporaryDirectory() as td:
             for fn in os.listdir(DATA):
@@ -580,7 +594,7 @@ def gen_mapped() -> None:
                 steps.append({"argv": argv, "exit": p.returncode, "hits": hits, "files": mapped_files(td)})
                 print(name, argv[-3:], p.returncode, len(hits), {k: v[0] if k.endswith("*") is False else "..." for k, v in steps[-1]["files"].items()}, flush=True)
         res[name] = steps
-    with open(os.path.join(REPO, "tests", "golden", "ref_mapped.json"), "w") as f:
+    with open(out_path, "w") as f:
         json.dump(res, f, indent=1)
 
 
@@ -700,7 +714,7 @@ if __name__ == "__main__":
     if a.bsgsd:
         gen_bsgsd()
     if a.mapped:
-        gen_mapped()
+        gen_mapped(a.only)
     if a.bsgsd_mapped:
         gen_bsgsd_mapped()
     if a.stdout:

@@ -29,6 +29,10 @@ def mapped_files(d: str) -> dict:
         m = re.match(r"(bloom2?3?-)(\d+)\.dat$", f)
         if m:
             layers.setdefault(m.group(1), {})[int(m.group(2))] = f
+        elif f.startswith("data_") and f.endswith(".dat"):  # -S target cache: the mmap pointer masked
+            b = bytearray(open(os.path.join(d, f), "rb").read())
+            b[96:104] = bytes(8)
+            out[f] = [len(b), hashlib.sha256(bytes(b)).hexdigest()]
         elif f.endswith(".dat") or re.search(r"\.dat\.\d+$", f):
             b = open(os.path.join(d, f), "rb").read()
             out[f] = [len(b), hashlib.sha256(b).hexdigest()]
