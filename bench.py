@@ -57,7 +57,7 @@ and traffic = HBM bytes per launch from the PMC counters with the guide's gfx950
 (tools/pmc_summary.py), or null.
 cpu_baseline: rank 0 at N=1 only, on every leg the reference binary built from its own sources with
 its own optimisation flags (oracle/_ref/keyhunt_fast, oracle/Makefile.ref; kind "reference"), run for
---cpu-seconds of its own stats clock twice: on the job's CPU share (cpu_threads: "value", "threads")
+--cpu-seconds-primary (BSGS, 60 s) / --cpu-seconds (rmd160, xpoint, 20 s) of its own stats clock twice: on the job's CPU share (cpu_threads: "value", "threads")
 and with -t 1 ("per_core"), its own last stats line parsed each time; the host's sockets, physical
 cores and threads per core come from lscpu.  "long_sample" quotes the newest >= 60-s measurement
 (bench.py --cpu-only --cpu-seconds 60, profiles/r*_cpu_baseline_*.json).  BSGS skips the reference's
@@ -940,7 +940,10 @@ def main():
     ap.add_argument("--steps-rmd", type=int, default=None)
     ap.add_argument("--warmup-rmd", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=20.0,
-                    help="CPU baseline: seconds of the reference's own stats clock per run (threads run, then -t 1)")
+                    help="CPU baseline of the rmd160 / xpoint legs: seconds of the reference's own stats clock per "
+                         "run (threads run, then -t 1)")
+    ap.add_argument("--cpu-seconds-primary", type=float, default=60.0,
+                    help="the same for the BSGS leg (the line's cpu_baseline): >= 60 s of steady state, SURVEY.md 8d")
     ap.add_argument("--cpu-only", action="store_true",
                     help="only the CPU baselines of the three legs (the BSGS one still needs the GPU to write the "
                          "-S tables); prints one JSON object")
@@ -983,7 +986,7 @@ def main():
     clock.stop()
     cpu_b = cpu_r = cpu_x = None
     if D.rank == 0 and D.world == 1 and not args.no_cpu_baseline and not args.cpu_only:
-        cpu_b = cpu_baseline_bsgs(W.engs[0], BSGS_CONFIGS[args.config], args.cpu_seconds)
+        cpu_b = cpu_baseline_bsgs(W.engs[0], BSGS_CONFIGS[args.config], args.cpu_seconds_primary)
         if not args.no_secondary:
             cpu_r = cpu_baseline_rmd160(args.cpu_seconds)
             cpu_x = cpu_baseline_xpoint(args.cpu_seconds)
@@ -1040,6 +1043,11 @@ def main():
                 key = {"cpu_baseline": "bsgs", "secondary": "rmd160", "tertiary": "xpoint"}[k]
                 if cb is not None and long_cpu.get(key):
                     cb["long_sample"] = dict(long_cpu[key], source=long_cpu["source"])
+                    # this run's rates over the long record's (the spread between boxes and sample lengths)
+                    for kk in ("threads", "per_core"):
+                        mine, rec = cb.get(kk), (long_cpu[key].get(kk) or {})
+                        if mine and rec.get("value"):
+                            cb["long_sample"][kk + "_ratio"] = mine["value"] / rec["value"]
         json_out.write(json.dumps(line) + "\n")
         json_out.flush()
     D.close()

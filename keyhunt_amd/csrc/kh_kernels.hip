@@ -1196,11 +1196,15 @@ __global__ void k_test_bloom(const uint8_t *items, uint32_t n, uint32_t len, con
 // ------------------------------------------------------------------------------------------
 namespace kh {
 
+#if defined(KH_ISA_ONLY_BSGSB) && !defined(KH_ISA_ONLY_MODE)
+#define KH_ISA_ONLY_MODE KM_BSGSB
+#endif
 hipError_t launch_walk(int mode, const walk_args &A, hipStream_t st, int H) {
-#ifdef KH_ISA_ONLY_BSGSB
-  // analysis builds (tools/isa_hot.py): the BSGS giant walk alone, compiled in seconds
-  constexpr int TB1 = walk_threads<KM_BSGSB, KH_WALK_HB>();
-  hipLaunchKernelGGL((k_walk<KM_BSGSB, KH_WALK_HB>), dim3((A.L + TB1 - 1) / TB1), dim3(TB1), 0, st, A);
+#ifdef KH_ISA_ONLY_MODE
+  // analysis builds (tools/isa_hot.py, tools/valu_mix.py): one large-group walk alone (KH_ISA_ONLY_BSGSB:
+  // the BSGS giant walk; KH_ISA_ONLY_MODE=<kh_walk_mode>: any other), compiled in seconds
+  constexpr int TB1 = walk_threads<KH_ISA_ONLY_MODE, KH_WALK_HB>();
+  hipLaunchKernelGGL((k_walk<KH_ISA_ONLY_MODE, KH_WALK_HB>), dim3((A.L + TB1 - 1) / TB1), dim3(TB1), 0, st, A);
   (void)mode;
   (void)H;
   return hipGetLastError();
@@ -1255,7 +1259,7 @@ hipError_t launch_walk(int mode, const walk_args &A, hipStream_t st, int H) {
 }
 
 hipError_t launch_walk_zinv(int mode, const walk_args &A, hipStream_t st) {
-#ifdef KH_ISA_ONLY_BSGSB
+#ifdef KH_ISA_ONLY_MODE
   (void)mode;
   (void)A;
   (void)st;

@@ -819,7 +819,9 @@ KH_HD void ge_double(ge &r, const ge &p) {
 // ------------------------------------------------------------------------------------------
 KH_HD uint32_t rotr32(uint32_t x, int n) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  return __builtin_amdgcn_alignbit(x, x, n);
+  // llvm.fshr: one v_alignbit_b32, and constant-folded when x is a constant (the target-specific
+  // alignbit builtin was not, which kept the hash IVs' rotations and every bitop3 on them live)
+  return __builtin_rotateright32(x, (uint32_t)n);
 #else
   return (x >> n) | (x << (32 - n));
 #endif
@@ -830,20 +832,36 @@ KH_HD uint32_t bswap32(uint32_t x) {
 }
 // Any 3-input boolean function in one gfx950 v_bitop3_b32: IMM is the truth table evaluated on
 // a = 0xF0, b = 0xCC, c = 0xAA (so xor3 = 0x96, ch = 0xCA, maj = 0xE8).
+// The truth table as plain logic: what the host runs, and what the device runs when an operand is a
+// compile-time constant (below).
 template <uint32_t IMM>
-KH_HD uint32_t bitop3(uint32_t a, uint32_t b, uint32_t c) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  uint32_t r;
-  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:%4" : "=v"(r) : "v"(a), "v"(b), "v"(c), "i"(IMM));
-  return r;
-#else
+KH_HD uint32_t bitop3_logic(uint32_t a, uint32_t b, uint32_t c) {
   uint32_t r = 0;
+#pragma unroll
   for (int i = 0; i < 8; i++)
     if ((IMM >> i) & 1) {
       uint32_t m = ((i & 4) ? a : ~a) & ((i & 2) ? b : ~b) & ((i & 1) ? c : ~c);
       r |= m;
     }
   return r;
+}
+#ifndef KH_BITOP3_FOLD
+#define KH_BITOP3_FOLD 1
+#endif
+template <uint32_t IMM>
+KH_HD uint32_t bitop3(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  // An operand that is a constant after unrolling (the hash IVs and padding words: SHA-256's first
+  // rounds, sigma of the zero schedule words, RIPEMD-160's first steps) goes through plain logic,
+  // which LLVM folds; asm would pin each constant in a VGPR and keep the instruction.
+  // __builtin_constant_p is resolved after inlining and unrolling (llvm.is.constant).
+  if (KH_BITOP3_FOLD && __builtin_constant_p(a) && __builtin_constant_p(b) && __builtin_constant_p(c))
+    return bitop3_logic<IMM>(a, b, c);
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:%4" : "=v"(r) : "v"(a), "v"(b), "v"(c), "i"(IMM));
+  return r;
+#else
+  return bitop3_logic<IMM>(a, b, c);
 #endif
 }
 KH_HD uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) { return bitop3<0x96>(a, b, c); }
