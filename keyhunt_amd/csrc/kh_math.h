@@ -858,7 +858,16 @@ KH_HD uint32_t bitop3(uint32_t a, uint32_t b, uint32_t c) {
   if (KH_BITOP3_FOLD && __builtin_constant_p(a) && __builtin_constant_p(b) && __builtin_constant_p(c))
     return bitop3_logic<IMM>(a, b, c);
   uint32_t r;
-  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:%4" : "=v"(r) : "v"(a), "v"(b), "v"(c), "i"(IMM));
+  // one constant operand may come from an SGPR (the VOP3 constant-bus allows one scalar read): the
+  // hash IVs of the first rounds then cost no VGPR across the walk's loop
+  if (KH_BITOP3_FOLD && __builtin_constant_p(c))
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:%4" : "=v"(r) : "v"(a), "v"(b), "s"(c), "i"(IMM));
+  else if (KH_BITOP3_FOLD && __builtin_constant_p(b))
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:%4" : "=v"(r) : "v"(a), "s"(b), "v"(c), "i"(IMM));
+  else if (KH_BITOP3_FOLD && __builtin_constant_p(a))
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:%4" : "=v"(r) : "s"(a), "v"(b), "v"(c), "i"(IMM));
+  else
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:%4" : "=v"(r) : "v"(a), "v"(b), "v"(c), "i"(IMM));
   return r;
 #else
   return bitop3_logic<IMM>(a, b, c);

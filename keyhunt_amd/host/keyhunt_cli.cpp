@@ -1092,7 +1092,8 @@ void report_call(kh_ctx *ctx, const bsgs_job *j, const kh_bsgs_info &info, const
   std::vector<std::pair<uint64_t, uint32_t>> at;  // (base position, found index)
   for (uint32_t f = 0; f < nf && f < found.size(); f++) {
     const U key = u_from_be32(found[f].key);
-    uint64_t pos = count ? count - 1 : 0;
+    const uint64_t none = ~0ULL;
+    uint64_t pos = none;
     if (list) {
       for (uint64_t i = 0; i < count; i++) {
         const U b = (*list)[i];
@@ -1107,10 +1108,17 @@ void report_call(kh_ctx *ctx, const bsgs_job *j, const kh_bsgs_info &info, const
       if (u_cmp(rel, u_from_u64(W)) > 0) {
         uint64_t rem = 0;
         const U q = u_divmod_u64(u_sub(rel, u_from_u64(W)), step.v[0], &rem);
-        if (u_bitlen(q) < 63) pos = std::min<uint64_t>(pos, q.v[0] + (rem ? 1 : 0));
+        if (u_bitlen(q) < 63 && q.v[0] + (rem ? 1 : 0) < count) pos = q.v[0] + (rem ? 1 : 0);
       } else {
         pos = 0;
       }
+    }
+    if (pos == none) {
+      // no base of the call holds the key in its window (base, base + W]: the engine found a key the
+      // reference's per-base windows do not cover; it is printed after the call's last base line
+      fprintf(stderr, "[W] key %s lies outside every base window of its call; printed after the call's last base\n",
+              u_hex(key).c_str());
+      pos = count ? count - 1 : 0;
     }
     at.push_back({pos, f});
   }
