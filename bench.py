@@ -798,10 +798,29 @@ REF_BIN = next((p for p in (os.path.join(REPO, "oracle", "_ref", b) for b in ("k
 REF_FLAGS = os.path.join(REPO, "oracle", "_ref", "build_flags.txt")
 
 
-def run_reference_once(argv: list[str], td: str, threads: int, seconds: float) -> tuple[int, int] | None:
+def host_state(pid: int | None = None) -> dict:
+    """The host's 1-min load average, the mean clock of all its CPUs and of the CPU `pid` last ran on
+    (/proc): a single thread's rate follows the package's boost, which the other tenants' load sets."""
+    out = {}
+    try:
+        out["loadavg_1min"] = os.getloadavg()[0]
+        mhz = [float(l.split(":")[1]) for l in open("/proc/cpuinfo") if l.startswith("cpu MHz")]
+        if mhz:
+            out["cpu_mhz_mean"] = sum(mhz) / len(mhz)
+        if pid:
+            cpu = int(open(f"/proc/{pid}/stat").read().rsplit(")", 1)[1].split()[36])
+            if 0 <= cpu < len(mhz):
+                out["cpu_mhz_of_ref"] = mhz[cpu]
+    except Exception:
+        pass
+    return out
+
+
+def run_reference_once(argv: list[str], td: str, threads: int, seconds: float) -> tuple[int, int, dict] | None:
     """One run of the reference CLI in `td` with `threads` threads until its own stats line covers
     `seconds` (its clock starts once its tables are ready): (keys, seconds) of the last such line
-    ("Total N keys in S seconds", keyhunt.cpp:2906-2946), keys counted as the reference counts them."""
+    ("Total N keys in S seconds", keyhunt.cpp:2906-2946), keys counted as the reference counts them,
+    and the host's state sampled every 5 s over the run (host_state, means)."""
     cmd = [REF_BIN] + argv + ["-t", str(threads), "-s", "5", "-q"]
     p = subprocess.Popen(cmd, cwd=td, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL)
     out = b""
@@ -809,8 +828,12 @@ def run_reference_once(argv: list[str], td: str, threads: int, seconds: float) -
     os.set_blocking(p.stdout.fileno(), False)
     last = None
     tick = t0
+    samples, tsamp = [], t0
     while time.time() - t0 < seconds + 120:
         time.sleep(0.5)
+        if time.time() - tsamp >= 5:
+            tsamp = time.time()
+            samples.append(host_state(p.pid))
         if time.time() - tick >= 30:
             tick = time.time()
             progress(f"CPU baseline running ({tick - t0:.0f} s, -t {threads})")
@@ -834,7 +857,9 @@ def run_reference_once(argv: list[str], td: str, threads: int, seconds: float) -
         except subprocess.TimeoutExpired:
             p.kill()
             p.wait()
-    return last if last and last[1] else None
+    state = {k: sum(x[k] for x in samples if k in x) / max(1, sum(1 for x in samples if k in x))
+             for k in ("loadavg_1min", "cpu_mhz_mean", "cpu_mhz_of_ref") if any(k in x for x in samples)}
+    return (last[0], last[1], state) if last and last[1] else None
 
 
 def run_reference(argv: list[str], files: list[str], seconds: float, setup=None, per_core_seconds: float | None = None):
@@ -863,9 +888,9 @@ def run_reference(argv: list[str], files: list[str], seconds: float, setup=None,
     name = f"oracle/_ref/{os.path.basename(REF_BIN)} {' '.join(argv)}"
     out = {"value": many[0] / many[1] / 1e6, "unit": "Mkeys/s", "cores": thr, "kind": "reference",
            "threads": {"value": many[0] / many[1] / 1e6, "threads": thr, "seconds": many[1], "keys": many[0],
-                       "measured": True},
+                       "measured": True, "host_state": many[2]},
            "per_core": ({"value": one[0] / one[1] / 1e6, "threads": 1, "seconds": one[1], "keys": one[0],
-                         "measured": True} if one else None),
+                         "measured": True, "host_state": one[2]} if one else None),
            "host": host, "build_flags": flags,
            "sample": f"{name} -t {thr}: {many[0]} keys in {many[1]} s" +
                      (f"; -t 1: {one[0]} keys in {one[1]} s" if one else "") +
@@ -1048,6 +1073,11 @@ def main():
                         mine, rec = cb.get(kk), (long_cpu[key].get(kk) or {})
                         if mine and rec.get("value"):
                             cb["long_sample"][kk + "_ratio"] = mine["value"] / rec["value"]
+                    if abs(cb["long_sample"].get("per_core_ratio", 1.0) - 1.0) > 0.1:
+                        cb["long_sample"]["per_core_note"] = (
+                            "the -t 1 rate is the host's single-core boost, which the load of the machine's other "
+                            "tenants sets (the 256-CPU host is shared; this run's host_state gives its load average "
+                            "and the clock of the CPU the reference ran on); both samples are >= 60 s")
         json_out.write(json.dumps(line) + "\n")
         json_out.flush()
     D.close()

@@ -154,6 +154,7 @@ static void kh_gpu_bsgs_tables(void) {
 		bool fresh;
 		kh_ctx *gpu = kh_gpu_open_dev(d, &fresh);
 		kh_bsgs_info info;
+		kh_gpu_check(gpu, kh_bsgs_set_bloom_multiplier(gpu, (uint32_t)FLAGBLOOMMULTIPLIER), "kh_bsgs_set_bloom_multiplier");
 		kh_gpu_check(gpu, kh_bsgs_setup(gpu, BSGS_N.GetInt64(), (uint64_t)KFACTOR, &info), "kh_bsgs_setup");
 		int r = KH_E_IO;
 		if (FLAGSAVEREADFILE) r = kh_bsgs_load(gpu, ".", FLAGSKIPCHECKSUM ? KH_LOAD_SKIP_CHECKSUM : 0);

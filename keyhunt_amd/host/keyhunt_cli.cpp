@@ -931,14 +931,68 @@ void setup_wait() {
 
 // -S (keyhunt.cpp:1983-2230, 2504-2652): the files of this N/k in the working directory are read
 // when they are all there, else the tables are built and (by the first GPU's worker) written.
+// -S with --mapped (keyhunt.cpp:1983 skips the reads, 2504-2652 still writes): the table files hold the
+// mapped shard filters -- each shard's struct bloom as the mapping left it, its bits and their sha256
+// twice -- and the sorted bP rows with their sha256, in the reference's order 4, 6, 2, 7
+int write_mapped_tables(kh_ctx *ctx, const kh_bsgs_info &info, const std::vector<std::vector<mapped::filter>> &F) {
+  const uint64_t ms[3] = {info.m, info.m2, info.m3};
+  const int kinds[3] = {4, 6, 7};
+  auto layer = [&](int l) {
+    char fn[96];
+    snprintf(fn, sizeof fn, "keyhunt_bsgs_%d_%llu.blm", kinds[l], (unsigned long long)ms[l]);
+    FILE *f = fopen(fn, "wb");
+    if (!f) {
+      fprintf(stderr, "[E] Error can't create the file %s\n", fn);
+      return false;
+    }
+    bool ok = true;
+    for (int i = 0; i < 256 && ok; i++) {
+      uint8_t h[112], ck[32];
+      mapped::struct_bloom(F[l][i], h);
+      sha256(F[l][i].bf.data(), F[l][i].bytes, ck);
+      ok = fwrite(h, 1, 112, f) == 112 && (F[l][i].bytes == 0 || fwrite(F[l][i].bf.data(), 1, F[l][i].bytes, f) == F[l][i].bytes) &&
+           fwrite(ck, 1, 32, f) == 32 && fwrite(ck, 1, 32, f) == 32;
+    }
+    ok = fclose(f) == 0 && ok;
+    if (!ok) fprintf(stderr, "[E] Error writing the file %s\n", fn);
+    else printf("[+] Writing bloom filter to file %s .... Done!\n", fn);
+    return ok;
+  };
+  if (!layer(0) || !layer(1)) return KH_E_IO;
+  if (opt.load_ptable) return layer(2) ? KH_OK : KH_E_IO;  // no .tbl with --load-ptable (2588)
+  const uint8_t *rows = nullptr;
+  uint64_t n = 0;
+  int r = kh_bsgs_table_rows(ctx, &rows, &n);
+  if (r) return r;
+  char fn[96];
+  snprintf(fn, sizeof fn, "keyhunt_bsgs_2_%llu.tbl", (unsigned long long)info.m3);
+  FILE *f = fopen(fn, "wb");
+  if (!f) {
+    fprintf(stderr, "[E] Error can't create the file %s\n", fn);
+    return KH_E_IO;
+  }
+  uint8_t ck[32];
+  sha256(rows, n * 16, ck);
+  bool ok = (n == 0 || fwrite(rows, 1, n * 16, f) == n * 16) && fwrite(ck, 1, 32, f) == 32;
+  ok = fclose(f) == 0 && ok;
+  if (!ok) {
+    fprintf(stderr, "[E] Error writing the file %s\n", fn);
+    return KH_E_IO;
+  }
+  printf("[+] Writing bP Table to file %s .. Done!\n", fn);
+  return layer(2) ? KH_OK : KH_E_IO;
+}
+
 int bsgs_tables(kh_ctx *ctx, const kh_bsgs_info &info, bool first) {
   if (opt.mapped) {  // -S is skipped with --mapped (keyhunt.cpp:1983); the shards live in files
     int r = kh_bsgs_build(ctx);
-    if (!r && first && !mapped::bsgs_layers(ctx, info)) r = KH_E_IO;
+    std::vector<std::vector<mapped::filter>> F;
+    if (!r && first && !mapped::bsgs_layers(ctx, info, opt.save_read ? &F : nullptr)) r = KH_E_IO;
     if (!r && first) {
       print_allocating(info);
       ptable_md5_loaded();
       print_build_lines(info);
+      if (opt.save_read) r = write_mapped_tables(ctx, info, F);
     }
     return r;
   }
@@ -1765,6 +1819,12 @@ int main(int argc, char **argv) {
               ggsb_blocks > 1 ? "GGSB" : "classic", (unsigned long long)ggsb_blocks, (unsigned long long)ggsb_babies);
       fprintf(stderr, "[i] Expected sizes: each bloom layer ~%.2f MB (256 shards), bPtable ~%.2f MB per block (%.2f MB total).\n",
               shard_mb * 256.0, (double)(ggsb_babies * 16) / 1048576.0, (double)(M * 16) / 1048576.0);
+    }
+    if (opt.mapped && opt.save_read && opt.mapped_chunks > 1) {
+      // the reference writes each shard's bits from its first chunk's mapping, past that mapping's end
+      fprintf(stderr, "[E] -S with --mapped-chunks above 1: the reference writes the table files from each shard's "
+                      "first chunk mapping past its end; not provided\n");
+      return EXIT_FAILURE;
     }
     if (!open_devices()) return EXIT_FAILURE;
     g_running = gpus;

@@ -335,7 +335,7 @@ inline bool targets(uint64_t items, const std::vector<uint8_t> &adds, uint32_t l
 // in that order first (the size override is applied to the first), then filled by the baby steps
 // of their layer on the GPU.  A shard that cannot be opened stops the start: the files opened
 // before it are left as the reference's mmap left them (created, or loaded and unchanged)
-inline bool bsgs_layers(kh_ctx *ctx, const kh_bsgs_info &I) {
+inline bool bsgs_layers(kh_ctx *ctx, const kh_bsgs_info &I, std::vector<std::vector<filter>> *keep = nullptr) {
   const uint64_t ms[3] = {I.m, I.m2, I.m3};
   const uint64_t floor_[3] = {10000, 1000, 1000};
   const char *pfx[3] = {"bloom-", "bloom2-", "bloom3-"};
@@ -388,6 +388,7 @@ inline bool bsgs_layers(kh_ctx *ctx, const kh_bsgs_info &I) {
     for (int i = 0; i < 256; i++)
       if (!save(F[l][i])) return false;
   }
+  if (keep) *keep = std::move(F);  // -S writes the layers' filters as the run left them
   return true;
 }
 

@@ -540,6 +540,9 @@ MAPPED_SEQS = [
     # its size-derived geometry, which goes into the data file, and a plain -S run then reads that file
     ("rmd160_S_mapped_fresh_then_reload", [RMD_ARGS + ["-S", "--mapped"], RMD_ARGS + ["-S", "--mapped"]]),
     ("rmd160_mapped_then_S_mapped_then_S", [RMD_ARGS + ["--mapped"], RMD_ARGS + ["-S", "--mapped"], RMD_ARGS + ["-S"]]),
+    # BSGS -S with --mapped: the reads are skipped (keyhunt.cpp:1983) but the table files are written from the
+    # mapped shard filters (2504-2652), fresh and over reloaded shard files
+    ("bsgs_S_mapped_fresh_then_rerun", [BSGS_ARGS + ["-S", "--mapped"], BSGS_ARGS + ["-S", "--mapped"]]),
     ("xpoint_S_mapped_override", [["-m", "xpoint", "-f", "1to63_65.txt", "-r", "1:100000", "-n", "0x100000", "-t", "4",
                                    "-S", "--mapped", "--mapped-size", "1m"]]),
 ]
@@ -554,6 +557,8 @@ def mapped_files(d: str) -> dict:
             layers.setdefault(m.group(1), {})[int(m.group(2))] = f
         elif f.startswith("data_") and f.endswith(".dat"):  # -S target cache: its mmap pointer masked
             out[f] = [os.path.getsize(os.path.join(d, f)), masked_data_digest(os.path.join(d, f))]
+        elif f.startswith("keyhunt_bsgs_"):  # -S table files: each shard's bf pointer masked
+            out[f] = [os.path.getsize(os.path.join(d, f)), masked_table_digest(os.path.join(d, f))]
         elif f.endswith(".dat") or re.search(r"\.dat\.\d+$", f):
             b = open(os.path.join(d, f), "rb").read()
             out[f] = [len(b), hashlib.sha256(b).hexdigest()]

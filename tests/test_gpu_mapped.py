@@ -33,6 +33,13 @@ def mapped_files(d: str) -> dict:
             b = bytearray(open(os.path.join(d, f), "rb").read())
             b[96:104] = bytes(8)
             out[f] = [len(b), hashlib.sha256(bytes(b)).hexdigest()]
+        elif f.startswith("keyhunt_bsgs_"):  # -S table files: each shard's struct bloom bf pointer masked
+            b = bytearray(open(os.path.join(d, f), "rb").read())
+            if f.endswith(".blm"):
+                rec = len(b) // 256
+                for i in range(256):
+                    b[i * rec + 64: i * rec + 72] = bytes(8)
+            out[f] = [len(b), hashlib.sha256(bytes(b)).hexdigest()]
         elif f.endswith(".dat") or re.search(r"\.dat\.\d+$", f):
             b = open(os.path.join(d, f), "rb").read()
             out[f] = [len(b), hashlib.sha256(b).hexdigest()]
