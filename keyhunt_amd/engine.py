@@ -78,6 +78,8 @@ def lib() -> ctypes.CDLL:
     L.kh_close.argtypes = [P]
     L.kh_set_geometry.argtypes = [P, ctypes.c_uint32, ctypes.c_uint32]
     L.kh_synchronize.argtypes = [P]
+    L.kh_scan_memory.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64)]
+    L.kh_bsgs_set_bloom_multiplier.argtypes = [P, ctypes.c_uint32]
     L.kh_set_rmd_batch.argtypes = [P, ctypes.c_uint32]
     L.kh_set_targets.argtypes = [P, u8p, ctypes.c_uint64, ctypes.c_uint64]
     L.kh_scan.argtypes = [P, u8p, u8p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(KhHit),

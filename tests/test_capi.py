@@ -163,3 +163,20 @@ def test_host_md5_matches_hashlib(tmp_path):
         f.write_bytes(data)
         out = subprocess.run([str(exe), str(f)], capture_output=True, text=True, check=True).stdout
         assert out == hashlib.md5(data).hexdigest(), n
+
+
+def test_scan_memory_figures():
+    """kh_scan_memory (context-free, no device call): a 2^32-key chunk of -m address/rmd160 holds 2^20
+    lanes x 4096-point groups of 32-B pad rows (64 GiB), -m xpoint's sparse pad half of that, -e and
+    the small-group walks (a chunk that is no multiple of 4096 keys) the dense 1024-point pad."""
+    import ctypes
+    from keyhunt_amd.engine import lib
+    def need(n, mode, search):
+        v = ctypes.c_uint64(0)
+        assert lib().kh_scan_memory(n, mode, search, ctypes.byref(v)) == 0
+        return v.value
+    pad = (1 << 20) * 2048 * 32
+    assert pad <= need(1 << 32, 0, 0) < pad + (1 << 30)
+    assert pad // 2 <= need(1 << 32, 1, 0) < pad // 2 + (1 << 30)
+    assert need(1 << 32, 0, 2) < pad  # -l both: 1024-point groups, 2^18 lanes
+    assert lib().kh_scan_memory(0, 0, 0, ctypes.byref(ctypes.c_uint64())) != 0

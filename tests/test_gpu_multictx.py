@@ -9,11 +9,12 @@ bases, so the contexts really split them; the 2^20-key ones are one chunk, taken
 the others find the cursor at its end."""
 import json
 import os
+import re
 
 import pytest
 
 from conftest import GOLDEN
-from _cli import check_against_reference, without_threads
+from _cli import check_against_reference, run_cli, without_threads
 
 pytestmark = pytest.mark.gpu
 E2E = json.load(open(os.path.join(GOLDEN, "ref_e2e.json")))
@@ -30,3 +31,21 @@ def test_cli_contexts_match_reference(name, contexts):
     p = check_against_reference(E2E[name], _argv(name, contexts), name)
     if E2E[name]["exit"] != 255:  # the run got as far as opening its contexts (not a refused target file)
         assert f"({contexts} contexts)" in p.stdout
+
+
+def test_cli_refuses_contexts_beyond_device_memory():
+    """-g contexts stacked on one device must fit its free memory: at the default
+    2^32-key chunk each rmd160 context holds a 64 GB inversion pad (kh_scan_memory), so -g 8 on one
+    288 GB GPU is refused before any context opens, with the figures; xpoint's sparse pad is half."""
+    import ctypes
+    from keyhunt_amd.engine import lib
+    need = ctypes.c_uint64(0)
+    assert lib().kh_scan_memory(ctypes.c_uint64(1 << 32), 0, 0, ctypes.byref(need)) == 0
+    assert need.value >= 64 << 30
+    xp = ctypes.c_uint64(0)
+    assert lib().kh_scan_memory(ctypes.c_uint64(1 << 32), 1, 0, ctypes.byref(xp)) == 0
+    assert 32 << 30 <= xp.value < need.value
+    p, hits = run_cli(["-m", "rmd160", "-f", "66.rmd", "-l", "compress", "-b", "66", "-g", "8"], timeout=120)
+    assert p.returncode == 1, p.stderr[-2000:]
+    assert re.search(r"-g 8: 8 context\(s\) on GPU 0 need [\d.]+ GB of device memory \([\d.]+ GB each\)", p.stderr), p.stderr
+    assert not hits

@@ -25,7 +25,10 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CLI = os.path.join(REPO, "keyhunt_amd", "bin", "keyhunt-amd")
 ARGV = {"bsgs": ["-m", "bsgs", "-f", "125.txt", "-b", "125", "-k", "128"],
         "rmd160": ["-m", "rmd160", "-f", "66.rmd", "-b", "66", "-l", "compress"],
-        "xpoint": ["-m", "xpoint", "-f", "63.pub", "-b", "63"]}
+        "xpoint": ["-m", "xpoint", "-f", "63.pub", "-b", "63"],
+        # -R: every chunk starts at a random key, so every call sets its 2^20 lanes up again
+        "xpoint_random": ["-m", "xpoint", "-f", "63.pub", "-b", "63", "-R"],
+        "rmd160_random": ["-m", "rmd160", "-f", "66.rmd", "-b", "66", "-l", "compress", "-R"]}
 
 
 def main():
