@@ -353,6 +353,7 @@ struct kh_ctx {
   // hits
   uint32_t hit_cap = 1u << 16;
   uint32_t *d_hit_count = nullptr;
+  uint32_t *d_zero_flag = nullptr;  // k_setup's progression mode: a lane scalar was 0 mod n
   kh_dev_hit *d_hits = nullptr;
   std::vector<kh_dev_hit> h_hits;
 
@@ -437,6 +438,7 @@ kh_ctx::~kh_ctx() {
   (void)hipFree(d_q);
   for (auto &t : tables) (void)hipFree(t.second);
   (void)hipFree(d_hit_count);
+  (void)hipFree(d_zero_flag);
   (void)hipFree(d_hits);
   (void)hipFree(d_tbloom);
   (void)hipFree(d_tblk);
@@ -571,6 +573,43 @@ int run_setup(kh_ctx *c, const std::vector<u256> &s, const ge *q) {
   c->tm[4].ms += ms;
   c->tm[4].points += L;
   if (dq) (void)hipFree(dq);
+  return KH_OK;
+}
+
+// Lane centres C_g = s_g * G for the progression s_g = s0 + g * step (mod n), g < L: the scalars are
+// derived on the device (k_setup's prog mode), so a chunk whose lanes restart (-R, the first chunk)
+// costs no host loop over 2^20 lanes and no 32 MB upload.  A lane scalar of 0 (its centre would be the
+// point at infinity) fails the call, as the host check did.
+int run_setup_prog(kh_ctx *c, const u256 &s0, const u256 &step, uint32_t L) {
+  c->cont_valid = false;
+  int r = ensure_lanes(c, L);
+  if (r) return r;
+  setup_args A;
+  memset(&A, 0, sizeof A);
+  A.comb = c->d_comb;
+  A.L = L;
+  A.cx = c->d_cx;
+  A.cy = c->d_cy;
+  A.prog = 1;
+  u256_to_limbs(A.s0, s0);
+  u256_to_limbs(A.step, step);
+  A.zero_flag = c->d_zero_flag;
+  HIPCHK(c, hipMemsetAsync(c->d_zero_flag, 0, 4, c->stream));
+  HIPCHK(c, hipEventRecord(c->ev_a, c->stream));
+  HIPCHK(c, launch_setup(A, c->stream));
+  HIPCHK(c, hipEventRecord(c->ev_b, c->stream));
+  uint32_t zero = 0;
+  HIPCHK(c, hipMemcpyAsync(&zero, c->d_zero_flag, 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  float ms = 0;
+  (void)hipEventElapsedTime(&ms, c->ev_a, c->ev_b);
+  c->tm[4].launches++;
+  c->tm[4].ms += ms;
+  c->tm[4].points += L;
+  if (zero) {
+    c->err = "lane centre scalar is 0 mod n";
+    return KH_E_ARG;
+  }
   return KH_OK;
 }
 
@@ -710,6 +749,7 @@ int kh_open(int device, kh_ctx **out) {
   // A/B and parity hook: KH_REFINE=host runs the second check on host threads instead of k_refine
   if (const char *e = getenv("KH_REFINE")) c->refine_host = strcmp(e, "host") == 0;
   if (hipMalloc(&c->d_hit_count, 4) != hipSuccess) return fail(KH_E_NOMEM);
+  if (hipMalloc(&c->d_zero_flag, 4) != hipSuccess) return fail(KH_E_NOMEM);
   if (hipMalloc(&c->d_hits, (size_t)c->hit_cap * sizeof(kh_dev_hit)) != hipSuccess) return fail(KH_E_NOMEM);
   *out = c;
   return KH_OK;
@@ -937,27 +977,17 @@ int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride_be[32], u
                       u256_cmp(ctx->cont_stride, stride) == 0;
   ctx->cont_valid = false;
   // lane g's first centre: offset H + g * lane_step, lane_step = 2H (interleaved) or gpl * 2H; the
-  // scalars follow one another by one addition (a -R chunk restarts 2^20 lanes, and with a stride each
-  // mul_stride is a 128-step double-and-add)
+  // scalars s0 + g * (lane_step * stride) are derived on the device (run_setup_prog: a -R chunk
+  // restarts 2^20 lanes)
   const u256 lane_step = mul_stride(inter ? (u128)(2 * H) : (u128)jg.gpl * (2 * H));
-  auto lane_scalars = [&](std::vector<u256> &v) {
-    u256 c = sc_add(st, mul_stride((u128)H));
-    for (uint32_t g = 0; g < v.size(); g++, c = sc_add(c, lane_step)) v[g] = c;
-  };
-  std::vector<u256> s(resume ? 0 : jg.L);
-  lane_scalars(s);
-  for (uint32_t g = 0; g < s.size(); g++)
-    if (u256_is_zero(s[g])) {
-      ctx->err = "lane centre scalar is 0 mod n";
-      return KH_E_ARG;
-    }
+  const u256 s0 = sc_add(st, mul_stride((u128)H));
   if (!resume) {
     // the pad's rows per lane, before the centres are set (the walk below probes the blocked target
     // filter exactly when A.tblk is set)
     const bool tblk = !(ctx->vanity || getenv("KH_REF_TARGET_BLOOM")) && ctx->d_tblk;
     r = ensure_lanes(ctx, jg.L, zg ? H : walk_pad_rows(km, tblk, H));  // km keeps KM_ENDO: as launch_walk sees it
     if (r) return r;
-    r = run_setup(ctx, s, nullptr);
+    r = run_setup_prog(ctx, s0, lane_step, jg.L);
     if (r) return r;
   }
 
@@ -999,11 +1029,7 @@ int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride_be[32], u
     ctx->hit_cap = (uint32_t)cap2;
     A.hits = ctx->d_hits;
     A.hit_cap = ctx->hit_cap;
-    if (s.empty()) {  // resumed lanes: compute their start scalars for the redo
-      s.resize(jg.L);
-      lane_scalars(s);
-    }
-    r = run_setup(ctx, s, nullptr);  // the walk moved the lane centres on: start them again
+    r = run_setup_prog(ctx, s0, lane_step, jg.L);  // the walk moved the lane centres on: start them again
     if (r) return r;
   }
   if (r) return r;

@@ -38,6 +38,13 @@ static_assert(KH_WALK_H >= 64 && KH_WALK_H <= 512 && (512 % KH_WALK_H) == 0,
 #ifndef KH_HASH_PAIR
 #define KH_HASH_PAIR 1
 #endif
+// KH_WALK_LB_H160CB: the compressed exact-target hash walk (the bench's rmd160 leg) at 4 waves/SIMD.  Since
+// the hash IVs fold (round 5) it fits 128 VGPRs with no spill in its per-point loop: +0.3 % in an
+// interleaved A/B, spreads disjoint (profiles/r05g_ab_hash_4waves.json); round 4 measured -1.1 % with the
+// constants still in VGPRs.  The other hash modes (Y, uncompressed, eth) keep KH_WALK_LB_HASH.
+#ifndef KH_WALK_LB_H160CB
+#define KH_WALK_LB_H160CB 4
+#endif
 #ifndef KH_WALK_LB_HASH
 #define KH_WALK_LB_HASH 3
 #endif
@@ -216,12 +223,17 @@ struct walk_args {
 };
 
 struct setup_args {
-  const uint32_t *scalars;  // L x 8 LE u32 limbs
+  const uint32_t *scalars;  // L x 8 LE u32 limbs (unless prog)
   const uint32_t *comb;     // 32 x 256 x 16 words
   const uint32_t *q;        // optional point added to every lane: {x[8], y[8]}
   uint32_t has_q;
   uint32_t L;
   uint32_t *cx, *cy;
+  // prog: the lane scalars are the progression s_g = s0 + g * step (mod n), derived on the device (no
+  // host loop, no upload); a lane whose scalar is 0 sets *zero_flag
+  uint32_t prog;
+  uint32_t s0[8], step[8];  // LE u32 limbs, both < n
+  uint32_t *zero_flag;
 };
 
 // BSGS second check on the GPU (bsgs_secondcheck, keyhunt.cpp:5151-5184).  Per first-level

@@ -505,8 +505,8 @@ constexpr bool needs_y() {
 // 4 waves/SIMD even with a few spills; the hash160 modes prefer 3).
 template <int MODE>
 constexpr int walk_lb() {
-  return ((MODE & 15) == KM_H160C || (MODE & 15) == KM_H160U || (MODE & 15) == KM_H160B || (MODE & 15) == KM_ETH ||
-          MODE == KM_H160CB)
+  return MODE == KM_H160CB ? KH_WALK_LB_H160CB
+         : ((MODE & 15) == KM_H160C || (MODE & 15) == KM_H160U || (MODE & 15) == KM_H160B || (MODE & 15) == KM_ETH)
              ? KH_WALK_LB_HASH
          : MODE == KM_DUMP                                          ? 2
                                                                     : KH_WALK_LB;
@@ -935,12 +935,53 @@ __device__ __forceinline__ void comb_mult(ge &r, const uint32_t s[8], const uint
   gej_to_ge(r, acc);
 }
 
+namespace {
+// r = (a + b) mod n for a, b < n (LE u32 limbs)
+__device__ __forceinline__ void sc_addmod(uint32_t r[8], const uint32_t a[8], const uint32_t b[8]) {
+  const uint32_t N[8] = {0xD0364141u, 0xBFD25E8Cu, 0xAF48A03Bu, 0xBAAEDCE6u,
+                         0xFFFFFFFEu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+  uint32_t t[8], u[8], c = 0, bo = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) t[i] = addc(a[i], b[i], c, c);
+#pragma unroll
+  for (int i = 0; i < 8; i++) u[i] = subb(t[i], N[i], bo, bo);
+  // a + b >= n exactly when the sum carried out of 2^256 or the subtraction did not borrow
+  const bool ge = c != 0 || bo == 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r[i] = ge ? u[i] : t[i];
+}
+}  // namespace
+
 __global__ void __launch_bounds__(256) k_setup(setup_args A) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= A.L) return;
   uint32_t s[8];  // 8 LE u32 limbs
+  if (A.prog) {
+    // s = s0 + g * step (mod n) by double-and-add over the bits of g, without lane-dependent branches
+    uint32_t acc[8], d[8], t[8];
 #pragma unroll
-  for (int i = 0; i < 8; i++) s[i] = A.scalars[(size_t)g * 8 + i];
+    for (int i = 0; i < 8; i++) {
+      acc[i] = A.s0[i];
+      d[i] = A.step[i];
+    }
+#pragma unroll 1
+    for (uint32_t m = g, b = 0; b < 32 && (A.L >> b) != 0; b++, m >>= 1) {
+      sc_addmod(t, acc, d);
+#pragma unroll
+      for (int i = 0; i < 8; i++) acc[i] = (m & 1) ? t[i] : acc[i];
+      sc_addmod(d, d, d);
+    }
+    uint32_t z = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      s[i] = acc[i];
+      z |= acc[i];
+    }
+    if (z == 0) atomicOr(A.zero_flag, 1u);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; i++) s[i] = A.scalars[(size_t)g * 8 + i];
+  }
   gej acc;
   comb_mult_jac(acc, s, A.comb);
   ge r;
