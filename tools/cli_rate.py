@@ -28,7 +28,10 @@ ARGV = {"bsgs": ["-m", "bsgs", "-f", "125.txt", "-b", "125", "-k", "128"],
         "xpoint": ["-m", "xpoint", "-f", "63.pub", "-b", "63"],
         # -R: every chunk starts at a random key, so every call sets its 2^20 lanes up again
         "xpoint_random": ["-m", "xpoint", "-f", "63.pub", "-b", "63", "-R"],
-        "rmd160_random": ["-m", "rmd160", "-f", "66.rmd", "-b", "66", "-l", "compress", "-R"]}
+        "rmd160_random": ["-m", "rmd160", "-f", "66.rmd", "-b", "66", "-l", "compress", "-R"],
+        # BSGS base schedules other than sequential go through kh_bsgs_scan_list (lanes restart per call)
+        "bsgs_random": ["-m", "bsgs", "-f", "125.txt", "-b", "125", "-k", "128", "-B", "random"],
+        "bsgs_both": ["-m", "bsgs", "-f", "125.txt", "-b", "125", "-k", "128", "-B", "both"]}
 
 
 def main():
