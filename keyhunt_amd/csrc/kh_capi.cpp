@@ -398,6 +398,7 @@ struct kh_ctx {
   uint32_t *d_amp2 = nullptr;        // 32 x {x[8], y[8]}
   uint32_t *d_ref_start = nullptr;   // 8 limbs
   uint32_t *d_ref_list = nullptr;    // list mode bases
+  uint32_t *h_ref_list = nullptr;    // their pinned staging copy
   uint64_t ref_list_cap = 0;
 
   // timing
@@ -446,6 +447,7 @@ kh_ctx::~kh_ctx() {
   (void)hipFree(d_amp2);
   (void)hipFree(d_ref_start);
   (void)hipFree(d_ref_list);
+  if (h_ref_list) (void)hipHostFree(h_ref_list);
   for (int i = 0; i < 2; i++) {
     (void)hipFree(d_cnt2[i]);
     (void)hipFree(d_hits2[i]);
@@ -675,6 +677,23 @@ int fetch_hits(kh_ctx *c, uint32_t &n) {
 // ==============================================================================================
 // C ABI
 // ==============================================================================================
+// f(lo, hi) over [0, n) split across up to `threads` host threads (serial below 2^16 items)
+template <class F>
+void parallel_for(uint64_t n, unsigned threads, F f) {
+  if (n < (1u << 16) || threads <= 1) {
+    f(0, n);
+    return;
+  }
+  const uint64_t per = (n + threads - 1) / threads;
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < threads; t++) {
+    const uint64_t lo = t * per, hi = std::min<uint64_t>(n, lo + per);
+    if (lo >= hi) break;
+    th.emplace_back(f, lo, hi);
+  }
+  for (auto &x : th) x.join();
+}
+
 extern "C" {
 
 int kh_abi_version(void) { return KH_ABI_VERSION; }
@@ -1972,12 +1991,36 @@ static int bsgs_scan_impl(kh_ctx *ctx, const u256 &st, const std::vector<u256> *
   // of a group whose first point is t sits at key base_b + M + 2M*(a + H).
   const uint64_t gpb = A_pts / (2 * H);  // walk groups per base
   const uint64_t total_groups = n_bases * gpb;
+  // lanes per launch: lanes_hb (2^20, four waves per SIMD slot) for the large groups when the call
+  // holds that many groups and the device has room for their scratch, else lanes_max (2^18).  At
+  // the CLI's call size (2^35 giant points) 2^20 lanes walk 41.6 G pts/s against 40.1 at 2^18 (and
+  // 38.8 at 2^19), same box, interleaved (profiles/r05n_geom_bsgs_bigcalls.json)
+  uint32_t lanes = ctx->lanes_max;
+  if (H == KH_WALK_HB && ctx->lanes_hb > lanes && total_groups >= ctx->lanes_hb && !getenv("KH_BSGS_NARROW")) {
+    if (ensure_pipeline(ctx, ctx->lanes_hb, H) == KH_OK) {
+      lanes = ctx->lanes_hb;
+    } else {  // out of device memory (other contexts): the smaller geometry
+      (void)hipGetLastError();
+      ctx->err.clear();
+    }
+  }
   job_geom jc{};
   uint64_t gpr = 0;  // continuous mode: groups per lane per round
   if (cont) {
     // interleaved lanes: lane g walks groups g, g + L, g + 2L, ... of the call, so after the call
     // it sits on group g of the call that starts where this one ends (kept across calls)
-    jc = plan(ctx, total_groups, 0);
+    jc = plan(ctx, total_groups, 0, lanes);
+    // keep the power-of-two lane count when the ragged last round (lanes past the call's end walk
+    // unprobed) costs at most 1/32 of the call: the balanced count plan() picks otherwise (e.g.
+    // 1039214 lanes for a 7274496-base call) walked 6 % slower than 2^20 lanes, interleaved on one
+    // box (profiles/r05q_geom_lanes_count.json)
+    if (total_groups >= lanes) {
+      const uint64_t gpl = (total_groups + lanes - 1) / lanes;
+      if ((gpl * lanes - total_groups) * 32 <= total_groups) {
+        jc.L = lanes;
+        jc.gpl = gpl;
+      }
+    }
     gpr = std::max<uint64_t>(1, KH_BSGS_ROUND_POINTS / ((uint64_t)jc.L * 2 * H));
     gpr = std::min<uint64_t>(gpr, jc.gpl);
     r = get_table(ctx, sc_neg(u256_u64(2 * I.m)), &tab, H, jc.L);
@@ -1986,25 +2029,53 @@ static int bsgs_scan_impl(kh_ctx *ctx, const u256 &st, const std::vector<u256> *
     ctx->cont_valid = false;
   }
   if (list) ctx->cont_valid = false;
-  const bool keep_lanes = cont && ctx->targets.size() == 1;
+  // lane g ends the call on group g + gpl*L of it: the first group of the next call only when the
+  // lanes tile the call exactly (else a following call starts its lanes again)
+  const bool keep_lanes = cont && ctx->targets.size() == 1 && (uint64_t)jc.L * jc.gpl == total_groups;
   // second check on the GPU: the kernel derives base_key from the candidate's giant index
   const bool gpu_refine = !ctx->refine_host;
-  if (gpu_refine) {
+  // per-base rounds derive their lane scalars on the device (k_setup prog 2) unless a centre key can
+  // reach n (key = base + M + 2M*(a0 + H) <= base + vmax; 0 mod n only at base + v = n) or
+  // KH_HOST_CENTRES is set; the host loop cost ~50 ns per lane, 2^18 lanes a round
+  bool dev_centres = !cont && !getenv("KH_HOST_CENTRES");
+  const u256 vmax = u256_from_u128((u128)I.m * (2 * (A_pts + H) + 1));
+  if (dev_centres && !list) {
+    u256 top;
+    dev_centres = !u256_add_raw(top, st, vmax) && !reaches_order(top, u256_from_u128((u128)2 * I.n), n_bases - 1);
+  }
+  if (list) {
+    // the bases as device limbs, packed on the host threads into a pinned buffer (a serial pass over
+    // 2^20 bases and a pageable copy took ~15 ms of each CLI call), with the centre-key check
+    if (n_bases > ctx->ref_list_cap) {
+      (void)hipFree(ctx->d_ref_list);
+      if (ctx->h_ref_list) (void)hipHostFree(ctx->h_ref_list);
+      ctx->d_ref_list = ctx->h_ref_list = nullptr;
+      ctx->ref_list_cap = 0;
+      HIPCHK(ctx, hipMalloc(&ctx->d_ref_list, (size_t)n_bases * 32));
+      HIPCHK(ctx, hipHostMalloc(&ctx->h_ref_list, (size_t)n_bases * 32, hipHostMallocDefault));
+      ctx->ref_list_cap = n_bases;
+    }
+    u256 thr;
+    u256_sub_raw(thr, ORDER_N, vmax);
+    std::atomic<bool> risky{false};
+    uint32_t *hl = ctx->h_ref_list;
+    parallel_for(n_bases, ctx->refine_threads, [&](uint64_t lo, uint64_t hi) {
+      bool r = false;
+      for (uint64_t b = lo; b < hi; b++) {
+        u256_to_limbs(hl + b * 8, (*list)[b]);
+        r |= u256_cmp((*list)[b], thr) >= 0;
+      }
+      if (r) risky = true;
+    });
+    if (risky) dev_centres = false;
+  }
+  if (gpu_refine || dev_centres) {
     uint32_t sl[8];
     u256_to_limbs(sl, st);
     HIPCHK(ctx, hipMemcpyAsync(ctx->d_ref_start, sl, 32, hipMemcpyHostToDevice, ctx->stream));
-    if (list) {
-      if (n_bases > ctx->ref_list_cap) {
-        (void)hipFree(ctx->d_ref_list);
-        ctx->d_ref_list = nullptr;
-        ctx->ref_list_cap = 0;
-        HIPCHK(ctx, hipMalloc(&ctx->d_ref_list, (size_t)n_bases * 32));
-        ctx->ref_list_cap = n_bases;
-      }
-      std::vector<uint32_t> lw((size_t)n_bases * 8);
-      for (uint64_t b = 0; b < n_bases; b++) u256_to_limbs(&lw[b * 8], (*list)[b]);
-      HIPCHK(ctx, hipMemcpy(ctx->d_ref_list, lw.data(), lw.size() * 4, hipMemcpyHostToDevice));
-    }
+    if (list)
+      HIPCHK(ctx, hipMemcpyAsync(ctx->d_ref_list, ctx->h_ref_list, (size_t)n_bases * 32, hipMemcpyHostToDevice,
+                                 ctx->stream));
   }
   auto centre_scalar = [&](uint64_t t0) {  // -(key of the centre of the group starting at t0)
     uint64_t b = t0 / A_pts, a0 = t0 % A_pts;
@@ -2016,10 +2087,10 @@ static int bsgs_scan_impl(kh_ctx *ctx, const u256 &st, const std::vector<u256> *
     const ge Q = ctx->targets[tgt];
     // rounds are pipelined: the GPU walks round r+1 while the host refines round r's
     // first-level candidates
-    // per-base rounds (list mode, overlapping bases): up to lanes_max bases per round, each lane
+    // per-base rounds (list mode, overlapping bases): up to `lanes` bases per round, each lane
     // walking a divisor of gpb groups (plan), so large calls start one lane per base and small
     // ones still fill ~lanes_max lanes
-    const uint64_t round_max = (uint64_t)ctx->lanes_max * gpb;
+    const uint64_t round_max = (uint64_t)lanes * gpb;
     const uint64_t g_end = cont ? jc.gpl : total_groups;
     uint64_t g0 = 0;
     // continuous mode: (re)start the lanes at group g0, unless the previous call left them here
@@ -2045,7 +2116,7 @@ static int bsgs_scan_impl(kh_ctx *ctx, const u256 &st, const std::vector<u256> *
         R.t_round = 0;
       } else {
         rg = std::min<uint64_t>(g_end - g0, round_max);
-        jg = plan(ctx, rg, gpb);  // a lane's run never crosses a base
+        jg = plan(ctx, rg, gpb, lanes);  // a lane's run never crosses a base
         R.t_round = g0 * 2 * H;
       }
       R.g0 = g0;
@@ -2055,14 +2126,26 @@ static int bsgs_scan_impl(kh_ctx *ctx, const u256 &st, const std::vector<u256> *
       int rr = ensure_pipeline(ctx, jg.L, H);
       if (rr) return rr;
       if (!cont || need_setup) {
-        uint32_t *hs = ctx->h_scal2[slot];
-        for (uint32_t g = 0; g < jg.L; g++) {
-          uint64_t t0 = cont ? (g0 * jc.L + g) * 2 * H : R.t_round + (uint64_t)g * jg.gpl * 2 * H;
-          u256_to_limbs(hs + (size_t)g * 8, centre_scalar(t0));
-        }
-        HIPCHK(ctx, hipMemcpyAsync(ctx->d_scalars, hs, (size_t)jg.L * 32, hipMemcpyHostToDevice, ctx->stream));
         setup_args S;
         memset(&S, 0, sizeof S);
+        if (dev_centres) {
+          S.prog = 2;
+          S.list = list ? ctx->d_ref_list : nullptr;
+          S.start = ctx->d_ref_start;
+          S.t_round = R.t_round;
+          S.lane_pts = jg.gpl * 2 * H;
+          S.a_pts = A_pts;
+          S.two_n = 2 * I.n;
+          S.m = I.m;
+          S.h = (uint32_t)H;
+        } else {
+          uint32_t *hs = ctx->h_scal2[slot];
+          for (uint32_t g = 0; g < jg.L; g++) {
+            uint64_t t0 = cont ? (g0 * jc.L + g) * 2 * H : R.t_round + (uint64_t)g * jg.gpl * 2 * H;
+            u256_to_limbs(hs + (size_t)g * 8, centre_scalar(t0));
+          }
+          HIPCHK(ctx, hipMemcpyAsync(ctx->d_scalars, hs, (size_t)jg.L * 32, hipMemcpyHostToDevice, ctx->stream));
+        }
         S.scalars = ctx->d_scalars;
         S.comb = ctx->d_comb;
         S.q = dq;
@@ -2104,7 +2187,13 @@ static int bsgs_scan_impl(kh_ctx *ctx, const u256 &st, const std::vector<u256> *
         Aw.groups = (uint32_t)std::min<uint64_t>(per_launch, gb1 - gb);
         HIPCHK(ctx, launch_walk(ctx->info.layer1_layout == KH_LAYER1_BLOCKED ? KM_BSGSB : KM_BSGS, Aw, ctx->stream, H));
         R.launches++;
-        R.points += (uint64_t)jg.L * Aw.groups * 2 * H;
+        // probed points: continuous mode's ragged last round walks lanes past the call unprobed
+        uint64_t real = (uint64_t)jg.L * Aw.groups;
+        if (cont) {
+          const uint64_t lo = gb * jg.L, hi = std::min<uint64_t>((gb + Aw.groups) * jg.L, total_groups);
+          real = hi > lo ? hi - lo : 0;
+        }
+        R.points += real * 2 * H;
       }
       HIPCHK(ctx, hipEventRecord(ctx->ev_round[slot][2], ctx->stream));
       HIPCHK(ctx, hipStreamWaitEvent(ctx->side, ctx->ev_round[slot][2], 0));
@@ -2282,7 +2371,13 @@ int kh_bsgs_scan_list(kh_ctx *ctx, const uint8_t *bases, uint64_t n_bases, kh_bs
                       uint32_t *n_found) {
   if (!ctx || (!bases && n_bases) || !n_found) return KH_E_ARG;
   std::vector<u256> list(n_bases);
-  for (uint64_t b = 0; b < n_bases; b++) list[b] = sc_reduce(u256_from_be(bases + 32 * b));
+  if (!ctx->refine_threads) {
+    unsigned hw = std::thread::hardware_concurrency();
+    ctx->refine_threads = std::max(1u, std::min(16u, hw ? hw : 4u));
+  }
+  parallel_for(n_bases, ctx->refine_threads, [&](uint64_t lo, uint64_t hi) {
+    for (uint64_t b = lo; b < hi; b++) list[b] = sc_reduce(u256_from_be(bases + 32 * b));
+  });
   return bsgs_scan_impl(ctx, u256{}, &list, n_bases, found, cap, n_found);
 }
 

@@ -229,11 +229,17 @@ struct setup_args {
   uint32_t has_q;
   uint32_t L;
   uint32_t *cx, *cy;
-  // prog: the lane scalars are the progression s_g = s0 + g * step (mod n), derived on the device (no
+  // prog == 1: the lane scalars are the progression s_g = s0 + g * step (mod n), derived on the device (no
   // host loop, no upload); a lane whose scalar is 0 sets *zero_flag
   uint32_t prog;
   uint32_t s0[8], step[8];  // LE u32 limbs, both < n
   uint32_t *zero_flag;
+  // prog == 2, BSGS per-base rounds: lane g starts at giant index t0 = t_round + g*lane_pts of the call
+  // (base b = t0 / a_pts, a0 = t0 % a_pts) and its scalar is -(base(b) + m*(2*(a0 + h) + 1)) mod n,
+  // base(b) = list[b] (list != null) or start + b*two_n
+  const uint32_t *list, *start;  // 8 LE u32 limbs per base, < n
+  uint64_t t_round, lane_pts, a_pts, two_n, m;
+  uint32_t h;
 };
 
 // BSGS second check on the GPU (bsgs_secondcheck, keyhunt.cpp:5151-5184).  Per first-level

@@ -936,6 +936,35 @@ __device__ __forceinline__ void comb_mult(ge &r, const uint32_t s[8], const uint
 }
 
 namespace {
+// secp256k1 group order n, LE u32 limbs
+__device__ __forceinline__ uint32_t order_limb(int i) {
+  const uint32_t N[8] = {0xD0364141u, 0xBFD25E8Cu, 0xAF48A03Bu, 0xBAAEDCE6u,
+                         0xFFFFFFFEu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+  return N[i];
+}
+// r = (a + v) mod n for a < n and v = v0 + v1*2^64 + v2*2^128 < n (v2 <= 1)
+__device__ void sc_add_small(uint32_t r[8], const uint32_t a[8], uint64_t v0, uint64_t v1, uint32_t v2) {
+  const uint32_t v[8] = {(uint32_t)v0, (uint32_t)(v0 >> 32), (uint32_t)v1, (uint32_t)(v1 >> 32), v2, 0, 0, 0};
+  uint32_t c = 0;
+  for (int i = 0; i < 8; i++) r[i] = addc(a[i], v[i], c, c);
+  bool ge_n = c != 0;
+  if (!ge_n) {  // r >= n ?
+    ge_n = true;
+    for (int i = 7; i >= 0; i--) {
+      if (r[i] != order_limb(i)) {
+        ge_n = r[i] > order_limb(i);
+        break;
+      }
+    }
+  }
+  if (ge_n) {
+    uint32_t bo = 0;
+    for (int i = 0; i < 8; i++) r[i] = subb(r[i], order_limb(i), bo, bo);
+  }
+}
+}  // namespace
+
+namespace {
 // r = (a + b) mod n for a, b < n (LE u32 limbs)
 __device__ __forceinline__ void sc_addmod(uint32_t r[8], const uint32_t a[8], const uint32_t b[8]) {
   const uint32_t N[8] = {0xD0364141u, 0xBFD25E8Cu, 0xAF48A03Bu, 0xBAAEDCE6u,
@@ -956,7 +985,7 @@ __global__ void __launch_bounds__(256) k_setup(setup_args A) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= A.L) return;
   uint32_t s[8];  // 8 LE u32 limbs
-  if (A.prog) {
+  if (A.prog == 1) {
     // s = s0 + g * step (mod n) by double-and-add over the bits of g, without lane-dependent branches
     uint32_t acc[8], d[8], t[8];
 #pragma unroll
@@ -978,6 +1007,34 @@ __global__ void __launch_bounds__(256) k_setup(setup_args A) {
       z |= acc[i];
     }
     if (z == 0) atomicOr(A.zero_flag, 1u);
+  } else if (A.prog == 2) {
+    // BSGS per-base rounds: s = -(key of the centre of the group starting at giant index t0), key =
+    // base(b) + M + 2M*(a0 + H) with b = t0 / a_pts, a0 = t0 % a_pts (the host's centre_scalar); the
+    // host takes this path only when no centre key can be 0 mod n
+    const uint64_t t0 = A.t_round + (uint64_t)g * A.lane_pts;
+    const uint64_t b = t0 / A.a_pts, a0 = t0 % A.a_pts;
+    uint32_t base[8];
+    uint64_t v0 = 0, v1 = 0;
+    if (A.list) {
+#pragma unroll
+      for (int i = 0; i < 8; i++) base[i] = A.list[b * 8 + i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; i++) base[i] = A.start[i];
+      v0 = b * A.two_n;  // b*2N as 128 bits
+      v1 = __umul64hi(b, A.two_n);
+    }
+    const uint64_t f = 2 * (a0 + A.h) + 1;  // M + 2M*(a0 + H) = M*f
+    const uint64_t w0 = A.m * f, w1 = __umul64hi(A.m, f);
+    const uint64_t s0 = v0 + w0;
+    const uint64_t c0 = s0 < v0 ? 1 : 0;
+    const uint64_t s1 = v1 + w1 + c0;
+    const uint32_t s2 = (s1 < v1 || (s1 == v1 && (w1 | c0) != 0)) ? 1u : 0u;
+    uint32_t kb[8];
+    sc_add_small(kb, base, s0, s1, s2);
+    uint32_t bo = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) s[i] = subb(order_limb(i), kb[i], bo, bo);  // n - kb, kb != 0
   } else {
 #pragma unroll
     for (int i = 0; i < 8; i++) s[i] = A.scalars[(size_t)g * 8 + i];
@@ -1010,34 +1067,6 @@ __global__ void __launch_bounds__(256) k_setup(setup_args A) {
 // ------------------------------------------------------------------------------------------
 // BSGS second check (bsgs_secondcheck, keyhunt.cpp:5151-5184), one candidate per lane.
 // ------------------------------------------------------------------------------------------
-namespace {
-// secp256k1 group order n, LE u32 limbs
-__device__ __forceinline__ uint32_t order_limb(int i) {
-  const uint32_t N[8] = {0xD0364141u, 0xBFD25E8Cu, 0xAF48A03Bu, 0xBAAEDCE6u,
-                         0xFFFFFFFEu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
-  return N[i];
-}
-// r = (a + v) mod n for a < n and v = v0 + v1*2^64 + v2*2^128 < n (v2 <= 1)
-__device__ void sc_add_small(uint32_t r[8], const uint32_t a[8], uint64_t v0, uint64_t v1, uint32_t v2) {
-  const uint32_t v[8] = {(uint32_t)v0, (uint32_t)(v0 >> 32), (uint32_t)v1, (uint32_t)(v1 >> 32), v2, 0, 0, 0};
-  uint32_t c = 0;
-  for (int i = 0; i < 8; i++) r[i] = addc(a[i], v[i], c, c);
-  bool ge_n = c != 0;
-  if (!ge_n) {  // r >= n ?
-    ge_n = true;
-    for (int i = 7; i >= 0; i--) {
-      if (r[i] != order_limb(i)) {
-        ge_n = r[i] > order_limb(i);
-        break;
-      }
-    }
-  }
-  if (ge_n) {
-    uint32_t bo = 0;
-    for (int i = 0; i < 8; i++) r[i] = subb(r[i], order_limb(i), bo, bo);
-  }
-}
-}  // namespace
 
 __global__ void __launch_bounds__(64) k_refine(refine_args A) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;

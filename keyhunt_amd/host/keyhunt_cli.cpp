@@ -708,6 +708,36 @@ bool take_bases(const U &twoN, uint64_t want, std::vector<U> &out) {
   return !out.empty();
 }
 
+// One engine call's bases of a listed schedule: `drawn` in the reference's order (the progress
+// lines); a run 2N apart, ascending or descending (backward, both), goes through kh_bsgs_scan from its
+// lowest base, any other set through kh_bsgs_scan_list in drawn order (the engine needs no order)
+struct list_batch {
+  bool ok = false;
+  std::vector<U> drawn;
+  bool consecutive = false;
+  uint8_t st_be[32];
+  std::vector<uint8_t> be;
+};
+
+void prepare_batch(const U &twoN, uint64_t want, list_batch &B) {
+  B.ok = take_bases(twoN, want, B.drawn);
+  B.be.clear();
+  if (!B.ok) return;
+  const size_t n = B.drawn.size();
+  bool up = true, down = true;
+  for (size_t i = 1; i < n && (up || down); i++) {
+    if (up) up = u_cmp(B.drawn[i], B.drawn[i - 1]) > 0 && u_cmp(u_sub(B.drawn[i], B.drawn[i - 1]), twoN) == 0;
+    if (down) down = u_cmp(B.drawn[i - 1], B.drawn[i]) > 0 && u_cmp(u_sub(B.drawn[i - 1], B.drawn[i]), twoN) == 0;
+  }
+  B.consecutive = up || down;
+  if (B.consecutive) {
+    u_to_be32(up ? B.drawn[0] : B.drawn[n - 1], B.st_be);
+    return;
+  }
+  B.be.resize(32 * n);
+  for (size_t i = 0; i < n; i++) u_to_be32(B.drawn[i], &B.be[32 * i]);
+}
+
 // The sequential schedules (sequential, angrygiant, ggsb) as one progression: up to `want` bases
 // from the cursor, step apart, while below the end -- the bases take_bases would list, counted
 // instead of listed (a call of 2^20 bases spent ~9 % of the GPU's time listing, sorting and
@@ -1225,16 +1255,38 @@ void bsgs_worker(bsgs_job *j) {
   if (!r) r = kh_bsgs_set_targets(ctx, xy.data(), (uint32_t)nt);
   const U twoN = u_mul_u64(u_from_u64(info.n), 2);
   std::vector<kh_bsgs_found> found(nt + 1);
-  std::vector<U> bases, drawn;
   std::vector<uint8_t> list_be;
   const bool progression = opt.bsgs_mode == BM_SEQUENTIAL || opt.bsgs_mode == BM_ANGRYGIANT || opt.bsgs_mode == BM_GGSB;
+  // listed schedules (backward, both, random, dance): the next call's bases are drawn and packed on a
+  // helper thread while the GPU walks the current call's (drawing, checking and packing 2^20 bases
+  // took ~1/4 of a call's time on the host between calls)
+  list_batch cur, nxt;
+  if (!progression && !r) prepare_batch(twoN, j->list_bases_per_call, cur);
   while (!r) {
-    if (progression) {
+    if (!progression) {
+      if (!cur.ok) break;
+      std::thread pre([&]() { prepare_batch(twoN, j->list_bases_per_call, nxt); });
+      const uint64_t nb = cur.drawn.size();
+      uint32_t nf = 0;
+      if (cur.consecutive)
+        r = kh_bsgs_scan(ctx, cur.st_be, nb, found.data(), (uint32_t)found.size(), &nf);
+      else
+        r = kh_bsgs_scan_list(ctx, cur.be.data(), nb, found.data(), (uint32_t)found.size(), &nf);
+      pre.join();
+      if (r) {
+        fprintf(stderr, "[E] kh_bsgs_scan: %s (%s)\n", kh_strerror(r), kh_last_error(ctx));
+        break;
+      }
+      g_bases_done += nb;
+      report_call(ctx, j, info, U{}, g_step, nb, &cur.drawn, found, nf);
+      std::swap(cur, nxt);
+      continue;
+    }
+    {
       U st;
       uint64_t nb = 0;
       if (!take_progression(g_step, u_cmp(g_step, twoN) == 0 ? j->bases_per_call : j->list_bases_per_call, st, nb))
         break;
-      bases.assign(1, st);
       uint8_t st_be[32];
       u_to_be32(st, st_be);
       uint32_t nf = 0;
@@ -1252,31 +1304,7 @@ void bsgs_worker(bsgs_job *j) {
       }
       g_bases_done += nb;
       report_call(ctx, j, info, st, g_step, nb, nullptr, found, nf);
-      continue;
     }
-    if (!take_bases(g_step, j->list_bases_per_call, bases)) break;
-    const uint64_t nb = bases.size();
-    drawn = bases;  // the reference's order, for the progress lines
-    // consecutive ascending bases go through kh_bsgs_scan (one progression), others as a list
-    std::sort(bases.begin(), bases.end(), [](const U &a, const U &b) { return u_cmp(a, b) < 0; });
-    bool consecutive = true;
-    for (uint64_t i = 1; i < nb && consecutive; i++) consecutive = u_cmp(u_sub(bases[i], bases[i - 1]), twoN) == 0;
-    uint32_t nf = 0;
-    if (consecutive) {
-      uint8_t st_be[32];
-      u_to_be32(bases[0], st_be);
-      r = kh_bsgs_scan(ctx, st_be, nb, found.data(), (uint32_t)found.size(), &nf);
-    } else {
-      list_be.resize(32 * nb);
-      for (uint64_t i = 0; i < nb; i++) u_to_be32(bases[i], &list_be[32 * i]);
-      r = kh_bsgs_scan_list(ctx, list_be.data(), nb, found.data(), (uint32_t)found.size(), &nf);
-    }
-    if (r) {
-      fprintf(stderr, "[E] kh_bsgs_scan: %s (%s)\n", kh_strerror(r), kh_last_error(ctx));
-      break;
-    }
-    g_bases_done += nb;
-    report_call(ctx, j, info, U{}, g_step, nb, &drawn, found, nf);
   }
   j->rc = r;
   kh_close(ctx);
@@ -1839,12 +1867,14 @@ int main(int argc, char **argv) {
       // ~2^35 giant points per engine call (16 pipelined rounds, ~1 s): the end of a call drains
       // the pipeline (the last round's second check, the hit copies), which at 2^31 points per call
       // cost 7 % of the rate (profiles/r03f_cli_rate_bsgs.json); a call returns as soon as every
-      // target is found.  A range of fewer bases than that is dealt out evenly over the contexts (the
-      // reference's threads take one base each, keyhunt.cpp:4600-4617)
+      // target is found.  Listed schedules take calls of the same size (at 2^31 points per call,
+      // -B random ran 17 % and -B both 9 % below sequential: profiles/r05k_cli_rate_bsgs_*.json).
+      // A range of fewer bases than that is dealt out evenly over the contexts (the reference's
+      // threads take one base each, keyhunt.cpp:4600-4617)
       {
         uint64_t aux = Nr / M, pts = ((aux + 1023) / 1024) * 1024;
         bj[d].bases_per_call = std::max<uint64_t>(1, (1ULL << 35) / pts);
-        bj[d].list_bases_per_call = std::max<uint64_t>(1, (1ULL << 31) / pts);
+        bj[d].list_bases_per_call = bj[d].bases_per_call;
         const U span = u_sub(opt.end, opt.start);
         if (g_step.v[1] == 0 && g_step.v[2] == 0 && g_step.v[3] == 0 && g_step.v[4] == 0) {
           uint64_t rem = 0;

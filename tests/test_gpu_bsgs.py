@@ -339,6 +339,112 @@ def test_gpu_refine_equals_host_refine(mode, oracle, monkeypatch):
     assert res[0][1][1] >= 2
 
 
+@pytest.mark.parametrize("mode", ["per_base", "list"])
+def test_device_centres_equal_host_centres(mode, oracle, monkeypatch):
+    """Per-base rounds derive their lane scalars on the device (k_setup prog 2) or on the host
+    (KH_HOST_CENTRES): same keys, same first-level candidates, same second-level hits; and a list
+    reaching up to the group order (host path by the engine's own check) still finds its key."""
+    import random
+    import keyhunt_amd as K
+    n, k = (1 << 22, 2) if mode == "list" else (1 << 24, 3)
+    p = oracle.bsgs_params(n, k)
+    keys = [0x2468ACE13579BDF, 0x2468ACE13579BDF + 9 * 2 * p.n + 4321]
+    start = keys[0] - 4 * 2 * p.n - 999
+    res = []
+    for how in ("device", "host"):
+        if how == "host":
+            monkeypatch.setenv("KH_HOST_CENTRES", "1")
+        else:
+            monkeypatch.delenv("KH_HOST_CENTRES", raising=False)
+        with K.Engine(0) as e:
+            e.bsgs_setup(n, k)
+            e.bsgs_build()
+            e.bsgs_set_targets([oracle.pubkey(x) for x in keys])
+            c0 = e.bsgs_candidates()
+            if mode == "list":
+                bases = [start + b * 2 * p.n for b in range(16)]
+                random.Random(5).shuffle(bases)
+                found = e.bsgs_scan_list(bases)
+            else:
+                found = e.bsgs_scan(start, 16)
+            res.append((sorted(found), e.bsgs_candidates() - c0, e.bsgs_refine_stats()[1]))
+    assert res[0] == res[1]
+    assert res[0][0] == [(0, keys[0]), (1, keys[1])]
+    monkeypatch.delenv("KH_HOST_CENTRES", raising=False)
+    with K.Engine(0) as e:
+        e.bsgs_setup(n, k)
+        e.bsgs_build()
+        key = SECP_N - 2 * p.n + 12345
+        e.bsgs_set_targets([oracle.pubkey(key)])
+        bases = [0x1111111111111111, key - 6000, SECP_N - 3 * p.n]
+        assert e.bsgs_scan_list(bases) == [(0, key)]
+
+
+def test_large_calls_use_wide_lanes_same_results(engine, oracle):
+    """A call of >= 2^20 walk groups runs 2^20 lanes (lanes_hb), smaller calls 2^18: one call over
+    2^17 bases, the same bases in four calls, and the same bases as a shuffled list all probe the
+    same points (same first-level candidates) and find the key in the same base."""
+    import random
+    n, k = 1 << 32, 2                      # 32768 giant points per base: 8 groups of 4096
+    p = oracle.bsgs_params(n, k)
+    engine.bsgs_setup(n, k)
+    engine.bsgs_build()
+    nb = 1 << 17
+    start = 0x5A5A5A5A5A000000
+    key = start + (nb - 3) * 2 * p.n + 31337
+    far = start - 12345 * 2 * p.n       # no base of the call holds it: every point is walked
+    bases = [start + b * 2 * p.n for b in range(nb)]
+    random.Random(11).shuffle(bases)
+    runs = []
+    for tgt in (far, key):
+        for plan in ("one", "four", "list"):
+            engine.bsgs_set_targets([oracle.pubkey(tgt)])
+            c0 = engine.bsgs_candidates()
+            if plan == "one":
+                got = engine.bsgs_scan(start, nb)
+            elif plan == "four":
+                got = []
+                for i in range(4):
+                    got += engine.bsgs_scan(start + i * (nb // 4) * 2 * p.n, nb // 4)
+            else:
+                got = engine.bsgs_scan_list(bases)
+            runs.append((tgt, plan, got, engine.bsgs_candidates() - c0))
+    assert [r[2] for r in runs[:3]] == [[], [], []]
+    assert runs[0][3] == runs[1][3] == runs[2][3] > 0
+    assert [r[2] for r in runs[3:]] == [[(0, key)]] * 3
+
+
+@pytest.mark.parametrize("lanes,calls", [(64, [17, 17, 5]), (64, [16, 16, 2]), (32, [9, 9, 9])])
+def test_calls_with_ragged_lane_tiles(oracle, lanes, calls):
+    """Calls whose groups the lanes do not tile exactly (17 bases = 136 groups over 64 lanes: 3
+    groups per lane, 56 unprobed lane-groups past the end) give the same candidates and keys as one
+    call over all the bases: a following call starts its lanes again rather than continuing lanes
+    that ended past its first group."""
+    import keyhunt_amd as K
+    n, k = 1 << 32, 2                      # 8 groups of 4096 giant points per base
+    p = oracle.bsgs_params(n, k)
+    total = sum(calls)
+    start = 0x13579BDF02468000
+    key = start + (calls[0] + calls[1] // 2) * 2 * p.n + 2024   # in the second call
+    far = start - 99 * 2 * p.n
+    with K.Engine(0, lanes, 0) as e:
+        e.bsgs_setup(n, k)
+        e.bsgs_build()
+        res = []
+        for plan in ([total], calls):
+            for tgt in (far, key):
+                e.bsgs_set_targets([oracle.pubkey(tgt)])
+                c0 = e.bsgs_candidates()
+                got, b = [], 0
+                for nb in plan:
+                    got += e.bsgs_scan(start + b * 2 * p.n, nb)
+                    b += nb
+                res.append((got, e.bsgs_candidates() - c0))
+    assert res[0][0] == res[2][0] == []
+    assert res[0][1] == res[2][1]          # the same first-level false positives (often none)
+    assert res[1][0] == res[3][0] == [(0, key)]
+
+
 def test_bsgs_lanes_continue_across_calls(engine, oracle):
     """Continuous mode keeps its (interleaved) lanes across kh_bsgs_scan calls whose bases follow
     on: scanning 8 bases in one call, in 4 calls of 2, or with a jump and a target switch in

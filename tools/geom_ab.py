@@ -27,7 +27,7 @@ DEFAULT = ["xpoint:0:0:1", "xpoint:0:0:2", "xpoint:524288:0:1", "xpoint:1048576:
            "bsgs:0:0:1", "bsgs:524288:0:1"]
 
 
-def run_variant(K, leg: str, lanes: int, gpl: int, ctxs: int, seconds: float, board) -> dict:
+def run_variant(K, leg: str, lanes: int, gpl: int, ctxs: int, seconds: float, board, bsgs_bases: int = 65536) -> dict:
     engs = [K.Engine(0, lanes, gpl) for _ in range(ctxs)]
     try:
         if leg == "bsgs":
@@ -38,7 +38,7 @@ def run_variant(K, leg: str, lanes: int, gpl: int, ctxs: int, seconds: float, bo
                 e.bsgs_set_targets([bench.decompress(C["pub"])])
             two_n = 2 * (1 << 44)
             unit_keys = two_n
-            per_call = 65536
+            per_call = bsgs_bases
             kind = K.engine.TIME_BSGS
             origins = [(1 << 124) + i * (1 << 38) * two_n for i in range(ctxs)]
             pts_per_unit = 32768
@@ -106,6 +106,7 @@ def run_variant(K, leg: str, lanes: int, gpl: int, ctxs: int, seconds: float, bo
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=8.0)
+    ap.add_argument("--bsgs-bases", type=int, default=65536, help="bases per BSGS call (CLI: 2^35 / 32768)")
     ap.add_argument("variants", nargs="*", default=DEFAULT)
     a = ap.parse_args()
     import keyhunt_amd as K
@@ -114,7 +115,7 @@ def main():
     res = []
     for v in a.variants:
         leg, lanes, gpl, ctxs = v.split(":")
-        r = run_variant(K, leg, int(lanes), int(gpl), int(ctxs), a.seconds, board)
+        r = run_variant(K, leg, int(lanes), int(gpl), int(ctxs), a.seconds, board, a.bsgs_bases)
         print(json.dumps(r), file=sys.stderr, flush=True)
         res.append(r)
     board.stop()
