@@ -568,9 +568,10 @@ def bsgs_leg(D: Dist, W: Walks, args, clock):
         run(B0)
         last = time.perf_counter() - t
     B = int(D.max(batch_for(args.seconds, args.steps, last / B0, B0, B0) if args.warmup else B0))
-    # whole tiles of the engine's 2^20 lanes (2^17 bases of 8 groups at k = 128): consecutive steps
+    # whole tiles of the engine's 2^21 lanes (2^18 bases of 8 groups at k = 128): consecutive steps
     # then continue their lanes, and no ragged last round walks unprobed points
-    tile = (1 << 20) // max(1, info.cycles * 1024 // 4096) * S
+    lanes = int(os.environ.get("KH_BSGS_LANES", 1 << 21))
+    tile = lanes // max(1, info.cycles * 1024 // 4096) * S
     if not args.bases and B >= tile:
         B = max(tile, (B + tile // 2) // tile * tile)
     progress(f"BSGS warm-up done; timing {args.steps} steps of {B} bases")

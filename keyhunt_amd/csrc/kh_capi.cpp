@@ -331,6 +331,7 @@ struct kh_ctx {
   // "Launch geometry").  kh_set_geometry(lanes != 0) sets both.
   uint32_t lanes_max = 1u << 18;
   uint32_t lanes_hb = KH_LANES_HB;
+  uint32_t lanes_bsgs = KH_BSGS_LANES;  // the BSGS walk's large calls
   uint32_t groups_per_launch = 0;
   uint32_t lanes_alloc = 0;
   int scratch_h = 0;  // inversion-pad entries per lane in d_scratch
@@ -783,6 +784,7 @@ int kh_set_geometry(kh_ctx *ctx, uint32_t lanes, uint32_t groups_per_launch) {
   if (!ctx) return KH_E_ARG;
   ctx->lanes_max = lanes ? lanes : (1u << 18);
   ctx->lanes_hb = lanes ? lanes : KH_LANES_HB;
+  ctx->lanes_bsgs = lanes ? lanes : KH_BSGS_LANES;
   ctx->groups_per_launch = groups_per_launch;
   return KH_OK;
 }
@@ -1991,16 +1993,22 @@ static int bsgs_scan_impl(kh_ctx *ctx, const u256 &st, const std::vector<u256> *
   // of a group whose first point is t sits at key base_b + M + 2M*(a + H).
   const uint64_t gpb = A_pts / (2 * H);  // walk groups per base
   const uint64_t total_groups = n_bases * gpb;
-  // lanes per launch: lanes_hb (2^20, four waves per SIMD slot) for the large groups when the call
-  // holds that many groups and the device has room for their scratch, else lanes_max (2^18).  At
-  // the CLI's call size (2^35 giant points) 2^20 lanes walk 41.6 G pts/s against 40.1 at 2^18 (and
-  // 38.8 at 2^19), same box, interleaved (profiles/r05n_geom_bsgs_bigcalls.json)
-  uint32_t lanes = ctx->lanes_max;
-  if (H == KH_WALK_HB && ctx->lanes_hb > lanes && total_groups >= ctx->lanes_hb && !getenv("KH_BSGS_NARROW")) {
-    if (ensure_pipeline(ctx, ctx->lanes_hb, H) == KH_OK) {
-      lanes = ctx->lanes_hb;
-    } else {  // out of device memory (other contexts): the smaller geometry
-      (void)hipGetLastError();
+  // lanes per launch: lanes_bsgs (2^21: eight waves per wave slot in turn, kh_kernels.h) for the
+  // large groups when the call holds that many groups and the device has room for their pad, else
+  // the largest power of two below it that fits (down to lanes_max, 2^18: one wave per slot).  The
+  // count must tile the call (below): plan()'s balanced count for a 7274496-base call (1039214
+  // lanes) walked 6 % slower than 2^20 (profiles/r05q_geom_lanes_count.json)
+  uint32_t lanes = ctx->lanes_max, wide = ctx->lanes_bsgs;
+  if (const char *e = getenv("KH_BSGS_LANES")) wide = (uint32_t)strtoul(e, nullptr, 0);  // A/B knob
+  if (getenv("KH_BSGS_NARROW")) wide = lanes;
+  if (H == KH_WALK_HB) {
+    for (uint32_t w = wide; w > lanes; w >>= 1) {
+      if (total_groups < w) continue;
+      if (ensure_pipeline(ctx, w, H) == KH_OK) {
+        lanes = w;
+        break;
+      }
+      (void)hipGetLastError();  // out of device memory (other contexts): a smaller geometry
       ctx->err.clear();
     }
   }

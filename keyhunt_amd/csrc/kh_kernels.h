@@ -28,6 +28,14 @@ static_assert(KH_WALK_H >= 64 && KH_WALK_H <= 512 && (512 % KH_WALK_H) == 0,
 #ifndef KH_LANES_HB
 #define KH_LANES_HB (1u << 20)
 #endif
+// Lanes of the BSGS giant walk's large calls: 2^21, eight waves per wave slot in turn.  The walk
+// waits on its random probes (0.76 of the quad model), and the more batches of waves a launch
+// holds, the further their phases drift apart: in bench.py's BSGS leg, interleaved on one box, 2^21
+// lanes ran 41.9 G giant points/s (spread 0.2 %) against 38.5-40.3 at 2^20 and ~39.7 at 2^18
+// (profiles/r05x_bench_lanes_2m.json).  Pad: 2^21 x 1024 rows x 32 B = 64 GB.
+#ifndef KH_BSGS_LANES
+#define KH_BSGS_LANES (1u << 21)
+#endif
 
 // minimum waves per SIMD requested for the walk kernel: XPOINT/BSGS/BUILD modes (KH_WALK_LB) and
 // the hash160 modes (KH_WALK_LB_HASH).  256 / LB VGPRs per lane at most; see DESIGN.md.

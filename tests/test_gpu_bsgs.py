@@ -381,15 +381,15 @@ def test_device_centres_equal_host_centres(mode, oracle, monkeypatch):
 
 
 def test_large_calls_use_wide_lanes_same_results(engine, oracle):
-    """A call of >= 2^20 walk groups runs 2^20 lanes (lanes_hb), smaller calls 2^18: one call over
-    2^17 bases, the same bases in four calls, and the same bases as a shuffled list all probe the
-    same points (same first-level candidates) and find the key in the same base."""
+    """A call of >= 2^21 walk groups runs 2^21 lanes, >= 2^20 groups 2^20 lanes, smaller calls 2^18:
+    one call over 2^18 bases, the same bases in two and in four calls, and as a shuffled list all
+    probe the same points (same first-level candidates) and find the key in the same base."""
     import random
     n, k = 1 << 32, 2                      # 32768 giant points per base: 8 groups of 4096
     p = oracle.bsgs_params(n, k)
     engine.bsgs_setup(n, k)
     engine.bsgs_build()
-    nb = 1 << 17
+    nb = 1 << 18
     start = 0x5A5A5A5A5A000000
     key = start + (nb - 3) * 2 * p.n + 31337
     far = start - 12345 * 2 * p.n       # no base of the call holds it: every point is walked
@@ -397,21 +397,19 @@ def test_large_calls_use_wide_lanes_same_results(engine, oracle):
     random.Random(11).shuffle(bases)
     runs = []
     for tgt in (far, key):
-        for plan in ("one", "four", "list"):
+        for plan in (1, 2, 4, "list"):
             engine.bsgs_set_targets([oracle.pubkey(tgt)])
             c0 = engine.bsgs_candidates()
-            if plan == "one":
-                got = engine.bsgs_scan(start, nb)
-            elif plan == "four":
-                got = []
-                for i in range(4):
-                    got += engine.bsgs_scan(start + i * (nb // 4) * 2 * p.n, nb // 4)
-            else:
+            if plan == "list":
                 got = engine.bsgs_scan_list(bases)
+            else:
+                got = []
+                for i in range(plan):
+                    got += engine.bsgs_scan(start + i * (nb // plan) * 2 * p.n, nb // plan)
             runs.append((tgt, plan, got, engine.bsgs_candidates() - c0))
-    assert [r[2] for r in runs[:3]] == [[], [], []]
-    assert runs[0][3] == runs[1][3] == runs[2][3] > 0
-    assert [r[2] for r in runs[3:]] == [[(0, key)]] * 3
+    assert [r[2] for r in runs[:4]] == [[]] * 4
+    assert len({r[3] for r in runs[:4]}) == 1 and runs[0][3] > 0
+    assert [r[2] for r in runs[4:]] == [[(0, key)]] * 4
 
 
 @pytest.mark.parametrize("lanes,calls", [(64, [17, 17, 5]), (64, [16, 16, 2]), (32, [9, 9, 9])])
