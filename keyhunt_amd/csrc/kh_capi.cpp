@@ -1954,8 +1954,12 @@ struct bsgs_round {
   bool setup;        // the round (re)started its lanes
 };
 
-// giant points per pipelined round (2^18 lanes x 2 groups of 1024)
-constexpr uint64_t KH_BSGS_ROUND_POINTS = 1ULL << 29;
+// giant points per pipelined round of continuous mode: 2^34 (2^21 lanes x 2 groups of 4096, one
+// launch).  Every launch starts its first batch of waves in phase; two groups per lane per launch
+// walked 41.1 G giant points/s against 40.05 at one (2^33) and 40.7 at four (2^35), three repeats each,
+// spread 0.05 % (profiles/r05ae_round_ab.json); in the bench's BSGS leg four groups ran 43.0 vs 40.1
+// at one on another box (r05ab_bench_round_points.json); eight groups per launch lost 1-14 %
+constexpr uint64_t KH_BSGS_ROUND_POINTS = 1ULL << 34;
 
 }  // namespace
 
@@ -1988,7 +1992,9 @@ static int bsgs_scan_impl(kh_ctx *ctx, const u256 &st, const std::vector<u256> *
     ctx->refine_threads = std::max(1u, std::min(16u, hw ? hw : 4u));
   }
   uint32_t nf = 0;
-  const uint32_t per_launch = ctx->groups_per_launch ? ctx->groups_per_launch : 8;
+  // two groups per lane per launch (KH_BSGS_ROUND_POINTS below): per-base rounds too
+  uint32_t per_launch = ctx->groups_per_launch ? ctx->groups_per_launch : 2;
+  if (const char *e = getenv("KH_BSGS_GROUPS_PER_LAUNCH")) per_launch = std::max(1u, (uint32_t)strtoul(e, nullptr, 0));  // A/B knob
   // giant points of this call: t in [0, n_bases*A); t -> base b = t / A, a = t % A; the centre
   // of a group whose first point is t sits at key base_b + M + 2M*(a + H).
   const uint64_t gpb = A_pts / (2 * H);  // walk groups per base
@@ -2029,7 +2035,9 @@ static int bsgs_scan_impl(kh_ctx *ctx, const u256 &st, const std::vector<u256> *
         jc.gpl = gpl;
       }
     }
-    gpr = std::max<uint64_t>(1, KH_BSGS_ROUND_POINTS / ((uint64_t)jc.L * 2 * H));
+    uint64_t round_pts = KH_BSGS_ROUND_POINTS;
+    if (const char *e = getenv("KH_BSGS_ROUND_POINTS")) round_pts = strtoull(e, nullptr, 0);  // A/B knob
+    gpr = std::max<uint64_t>(1, round_pts / ((uint64_t)jc.L * 2 * H));
     gpr = std::min<uint64_t>(gpr, jc.gpl);
     r = get_table(ctx, sc_neg(u256_u64(2 * I.m)), &tab, H, jc.L);
     if (r) return r;
