@@ -2008,8 +2008,16 @@ static int bsgs_scan_impl(kh_ctx *ctx, const u256 &st, const std::vector<u256> *
   if (const char *e = getenv("KH_BSGS_LANES")) wide = (uint32_t)strtoul(e, nullptr, 0);  // A/B knob
   if (getenv("KH_BSGS_NARROW")) wide = lanes;
   if (H == KH_WALK_HB) {
+    // a wider geometry is taken only if it leaves 32 GB of the device free for other contexts (their
+    // tables are built while this one walks: `-g N` on one GPU)
+    const uint64_t rows = (uint64_t)walk_pad_rows(KM_BSGSB, false, H);
+    const uint64_t have = ctx->lanes_alloc >= lanes ? (uint64_t)ctx->lanes_alloc * ((uint64_t)ctx->scratch_h * 32 + 96) : 0;
+    size_t fr = 0, tot = 0;
+    const bool known = hipMemGetInfo(&fr, &tot) == hipSuccess;
     for (uint32_t w = wide; w > lanes; w >>= 1) {
       if (total_groups < w) continue;
+      const uint64_t need = (uint64_t)w * (rows * 32 + 96);
+      if (known && need > have && fr + have < need + (32ull << 30)) continue;
       if (ensure_pipeline(ctx, w, H) == KH_OK) {
         lanes = w;
         break;
