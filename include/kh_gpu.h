@@ -165,7 +165,8 @@ int kh_bsgs_setup(kh_ctx *ctx, uint64_t n, uint64_t k, kh_bsgs_info *info);
  * (the three layers, the bP rows, the inversion pad of the giant walk, lane state, candidate buffers
  * at their current size, a kh_bsgs_scan_list of up to 2^16 bases), and how many of them it holds
  * already.  A lower bound: longer lists (32 B per base) and candidate buffers grown on overflow come
- * on top */
+ * on top.  The pad counted is the 2^18-lane one (8 GB); a call of >= 2^21 walk groups widens it to
+ * 2^21 lanes (64 GB; 2^20: 32 GB) only while 32 GB of the device stay free after it */
 int kh_bsgs_memory(kh_ctx *ctx, uint64_t *needed_bytes, uint64_t *held_bytes);
 int kh_bsgs_build(kh_ctx *ctx);                  /* baby-step blooms + sorted bP table on the GPU */
 /* -S table files in the reference's formats (keyhunt.cpp:2504-2652 write, 1983-2230 read), in dir
