@@ -471,6 +471,29 @@ namespace {
 
 // lane centres for L lanes and an inversion pad of H rows per lane (walk_pad_rows: half the group for
 // the sparse-pad walks)
+// Device memory for the randomly probed layer-1 filter (which = 1) and the giant walk's inversion pad
+// (which = 2).  KH_CONTIG=<mask> asks for physically contiguous memory (hipDeviceMallocContiguous)
+// for an A/B; the default is an ordinary allocation: contiguous layer 1 + pad walked 35.7 / 34.5 /
+// 36.0 G giant points/s against 40.0 / 39.7 / 37.4 ordinary, interleaved in the bench's BSGS leg
+// (profiles/r05an_bench_contig_ab.json)
+hipError_t dev_alloc(void **p, size_t bytes, int which) {
+  static const int mask = [] {
+    const char *e = getenv("KH_CONTIG");
+    return e ? atoi(e) : 0;
+  }();
+  static const bool log = getenv("KH_DEBUG_ALLOC") != nullptr;  // diagnostics only: stderr
+  if (mask & which) {
+    if (hipExtMallocWithFlags(p, bytes, hipDeviceMallocContiguous) == hipSuccess) {
+      if (log) fprintf(stderr, "[kh] %zu bytes (kind %d): contiguous\n", bytes, which);
+      return hipSuccess;
+    }
+    (void)hipGetLastError();
+    *p = nullptr;
+    if (log) fprintf(stderr, "[kh] %zu bytes (kind %d): contiguous refused\n", bytes, which);
+  }
+  return hipMalloc(p, bytes);
+}
+
 int ensure_lanes(kh_ctx *c, uint32_t L, int H = KH_WALK_H) {
   if (L <= c->lanes_alloc && H <= c->scratch_h) return KH_OK;
   L = std::max(L, c->lanes_alloc);
@@ -487,7 +510,7 @@ int ensure_lanes(kh_ctx *c, uint32_t L, int H = KH_WALK_H) {
   HIPCHK(c, hipMalloc(&c->d_cx, (size_t)L * 32));
   HIPCHK(c, hipMalloc(&c->d_cy, (size_t)L * 32));
   HIPCHK(c, hipMalloc(&c->d_scalars, (size_t)L * 32));
-  HIPCHK(c, hipMalloc(&c->d_scratch, (size_t)L * H * 32));
+  HIPCHK(c, dev_alloc(reinterpret_cast<void **>(&c->d_scratch), (size_t)L * H * 32, 2));
   c->lanes_alloc = L;
   c->scratch_h = H;
   return KH_OK;
@@ -1250,7 +1273,10 @@ int kh_bsgs_setup(kh_ctx *ctx, uint64_t n, uint64_t k, kh_bsgs_info *info) {
     size_t bytes = 256 * ctx->bd[l].stride + 4;
     // (fine-grained and uncached memory types for layer 1 were measured in round 4: no gain, the
     // probes still cost the same power, profiles/r04e_alloc_ab.json)
-    HIPCHK(ctx, hipMalloc(&ctx->d_bl[l], bytes));
+    if (l == 0)
+      HIPCHK(ctx, dev_alloc(reinterpret_cast<void **>(&ctx->d_bl[l]), bytes, 1));
+    else
+      HIPCHK(ctx, hipMalloc(&ctx->d_bl[l], bytes));
     HIPCHK(ctx, hipMemset(ctx->d_bl[l], 0, bytes));
   }
   // AMP2[i] = -(M2 + 2i*M2)G, AMP3[i] = -(M3 + 2i*M3)G  (keyhunt.cpp:1818-1842)

@@ -4,7 +4,8 @@
 continue across them) and reports giant points/s from the engine's walk events and the wall clock.
 
 usage: python tools/round_ab.py [--bases 4194304] [--calls 5] [--repeat 2] VARIANT ...
-VARIANT = ROUND_POINTS_LOG2:GROUPS_PER_LAUNCH, e.g. 35:8 (the default since round 5) 33:8 37:4
+VARIANT = [M x]ROUND_POINTS_LOG2:GROUPS_PER_LAUNCH, e.g. 34:2 (the default since round 5), 33:8,
+3x33:3 (three groups of 2^21 lanes per launch); KH_BSGS_LANES in the environment sets the lanes
 """
 import argparse
 import json
@@ -39,8 +40,11 @@ def main():
     done += 1
     for rep in range(a.repeat):
         for v in a.variants:
-            lg, gpl = (int(x) for x in v.split(":"))
-            os.environ["KH_BSGS_ROUND_POINTS"] = str(1 << lg)
+            rp, gpl = v.split(":")
+            gpl = int(gpl)
+            mult, _, lg = rp.rpartition("x")        # "3x33" = 3 * 2^33 points per round
+            rpts = (int(mult) if mult else 1) << int(lg)
+            os.environ["KH_BSGS_ROUND_POINTS"] = str(rpts)
             e.set_geometry(0, gpl)
             e.kernel_time_reset()
             b0 = board.snapshot()
@@ -52,7 +56,7 @@ def main():
             t1 = time.perf_counter()
             b1 = board.snapshot()
             la, ms, pts = e.kernel_time(K.engine.TIME_BSGS)
-            r = {"variant": v, "repeat": rep, "round_points": 1 << lg, "groups_per_launch": gpl,
+            r = {"variant": v, "repeat": rep, "round_points": rpts, "groups_per_launch": gpl,
                  "giant_points_per_s_wall": a.calls * pts_call / (t1 - t0), "giant_points_per_s_events": pts / (ms / 1e3),
                  "launches": la, "ms_per_launch": ms / la, "board": board.between(b0, b1)}
             rows.append(r)
