@@ -116,6 +116,9 @@ const char *kh_last_error(kh_ctx *ctx);
 int kh_abi_version(void);
 /* lanes per walk launch (0 = automatic); groups (of 1024 points) per lane per launch (0 = auto) */
 int kh_set_geometry(kh_ctx *ctx, uint32_t lanes, uint32_t groups_per_launch);
+/* free the walks' device buffers (lane centres, scalars, inversion pad: up to 64 GB) between jobs;
+ * the next scan allocates them again and starts its lanes afresh.  Tables and targets stay. */
+int kh_release_walk(kh_ctx *ctx);
 int kh_synchronize(kh_ctx *ctx);
 
 /* ---- address / rmd160 / xpoint ------------------------------------------------------------ */

@@ -803,6 +803,22 @@ int kh_close(kh_ctx *ctx) {
   return KH_OK;
 }
 
+int kh_release_walk(kh_ctx *ctx) {
+  if (!ctx) return KH_E_ARG;
+  (void)hipSetDevice(ctx->device);
+  (void)hipDeviceSynchronize();
+  (void)hipFree(ctx->d_cx);
+  (void)hipFree(ctx->d_cy);
+  (void)hipFree(ctx->d_scalars);
+  (void)hipFree(ctx->d_scratch);
+  ctx->d_cx = ctx->d_cy = ctx->d_scalars = nullptr;
+  ctx->d_scratch = nullptr;
+  ctx->lanes_alloc = 0;
+  ctx->scratch_h = 0;
+  ctx->cont_valid = false;
+  return KH_OK;
+}
+
 int kh_set_geometry(kh_ctx *ctx, uint32_t lanes, uint32_t groups_per_launch) {
   if (!ctx) return KH_E_ARG;
   ctx->lanes_max = lanes ? lanes : (1u << 18);

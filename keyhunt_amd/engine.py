@@ -77,6 +77,7 @@ def lib() -> ctypes.CDLL:
     L.kh_open.argtypes = [ctypes.c_int, ctypes.POINTER(P)]
     L.kh_close.argtypes = [P]
     L.kh_set_geometry.argtypes = [P, ctypes.c_uint32, ctypes.c_uint32]
+    L.kh_release_walk.argtypes = [P]
     L.kh_synchronize.argtypes = [P]
     L.kh_scan_memory.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64)]
     L.kh_bsgs_set_bloom_multiplier.argtypes = [P, ctypes.c_uint32]
@@ -170,6 +171,10 @@ class Engine:
 
     def set_geometry(self, lanes: int = 0, groups_per_launch: int = 0) -> None:
         self._chk(lib().kh_set_geometry(self._ctx, lanes, groups_per_launch), "kh_set_geometry")
+
+    def release_walk(self) -> None:
+        """Free the walks' lane arrays and inversion pad (kh_release_walk)."""
+        self._chk(lib().kh_release_walk(self._ctx), "kh_release_walk")
 
     def set_rmd_batch(self, group: int) -> None:
         """-m rmd160 --rmd-batch-size: the reference's clamped group size (1024 = the ordinary walk)."""
