@@ -443,6 +443,27 @@ def test_calls_with_ragged_lane_tiles(oracle, lanes, calls):
     assert res[1][0] == res[3][0] == [(0, key)]
 
 
+def test_release_walk_between_calls(engine, oracle):
+    """kh_release_walk frees the lane arrays and the pad: the next call allocates them again and
+    starts its lanes afresh, with the same candidates and key as one uninterrupted call."""
+    n, k = 1 << 32, 2
+    p = oracle.bsgs_params(n, k)
+    engine.bsgs_setup(n, k)
+    engine.bsgs_build()
+    start = 0x2468ACE0000000
+    key = start + 6 * 2 * p.n + 4242
+    res = []
+    for release in (False, True):
+        engine.bsgs_set_targets([oracle.pubkey(key)])
+        c0 = engine.bsgs_candidates()
+        got = engine.bsgs_scan(start, 4)
+        if release:
+            engine.release_walk()
+        got += engine.bsgs_scan(start + 4 * 2 * p.n, 4)
+        res.append((got, engine.bsgs_candidates() - c0))
+    assert res[0] == res[1] and res[0][0] == [(0, key)]
+
+
 def test_bsgs_lanes_continue_across_calls(engine, oracle):
     """Continuous mode keeps its (interleaved) lanes across kh_bsgs_scan calls whose bases follow
     on: scanning 8 bases in one call, in 4 calls of 2, or with a jump and a target switch in
