@@ -324,10 +324,13 @@ class BoardSampler:
 
     RESIDENCY = ("ppt_residency_acc", "socket_thm_residency_acc", "hbm_thm_residency_acc", "vr_thm_residency_acc",
                  "prochot_residency_acc")
+    # other gpu_metrics fields averaged over a window when the board reports them (MHz / %)
+    EXTRA = ("current_uclk", "current_fclk", "current_socclks", "average_umc_activity", "average_gfx_activity")
 
     def __init__(self, bdf: str | None, period: float = 0.25):
         self.samples: list[tuple[float, float]] = []        # (t, gfx MHz)
         self.power_samples: list[tuple[float, float]] = []  # (t, socket W)
+        self.extra_samples: dict[str, list[tuple[float, float]]] = {}
         self.error = None
         self._stop = threading.Event()
         self._h = None
@@ -389,6 +392,16 @@ class BoardSampler:
                 p = _num(m.get("current_socket_power"))
                 if p:
                     self.power_samples.append((t, p))
+                # memory / fabric clocks and memory-controller activity, where gpu_metrics has them
+                for k in self.EXTRA:
+                    v = m.get(k)
+                    if isinstance(v, list):
+                        v = [x for x in v if isinstance(x, (int, float)) and 0 < x < 65535]
+                        v = sum(v) / len(v) if v else None
+                    else:
+                        v = _num(v)
+                    if v is not None and 0 <= v < 65535:
+                        self.extra_samples.setdefault(k, []).append((t, v))
             except Exception as e:
                 self.error = f"amdsmi read: {e!r}"[:200]
                 return
@@ -436,6 +449,10 @@ class BoardSampler:
         dt = b["t"] - a["t"]
         out = {"seconds": dt, "board_gfxclk_mhz": self.mean(a["t"], b["t"]),
                "socket_power_w_sampled": self.mean_power(a["t"], b["t"])}
+        for k, v in self.extra_samples.items():
+            w = [c for t, c in v if a["t"] <= t <= b["t"]]
+            if w:
+                out[k] = sum(w) / len(w)
         if a.get("energy_j") is not None and b.get("energy_j") is not None and dt > 0:
             out["socket_power_w"] = (b["energy_j"] - a["energy_j"]) / dt
         if a.get("acc") is not None and b.get("acc") is not None and b["acc"] > a["acc"]:
