@@ -579,12 +579,17 @@ def bsgs_leg(D: Dist, W: Walks, args, clock):
         walked += per
         assert not any(found)  # puzzle 125's (130's) key lies far from the start of the range
 
+    # warm-up steps large enough for the engine's lane-count calibration (a context's first call of
+    # >= 2^23 walk groups times 2^21 against 2^20 lanes, DESIGN.md §2 "Placement"), so it happens here
+    # and not in the timed region
+    gpb = max(1, info.cycles * 1024 // 4096)
+    Bw = max(B0, -(-(4 << 21) // gpb) * S) if args.warmup else B0
     last = 0.0
     for s in range(args.warmup):
         t = time.perf_counter()
-        run(B0)
+        run(Bw)
         last = time.perf_counter() - t
-    B = int(D.max(batch_for(args.seconds, args.steps, last / B0, B0, B0) if args.warmup else B0))
+    B = int(D.max(batch_for(args.seconds, args.steps, last / Bw, B0, B0) if args.warmup else B0))
     # whole tiles of the engine's 2^21 lanes (2^18 bases of 8 groups at k = 128): consecutive steps
     # then continue their lanes, and no ragged last round walks unprobed points
     lanes = int(os.environ.get("KH_BSGS_LANES", 1 << 21))
@@ -594,6 +599,7 @@ def bsgs_leg(D: Dist, W: Walks, args, clock):
     progress(f"BSGS warm-up done; timing {args.steps} steps of {B} bases")
     T, t0, t1, recs, board = timed(D, W, args.steps, lambda s: run(B), B, K.engine.TIME_BSGS, clock)
     progress(f"BSGS timed region {T:.1f} s; known-answer window next")
+    lanes_pick, rate_hi, rate_lo = W.engs[0].bsgs_geometry()
     la, ms, pts = W.kernel_time(K.engine.TIME_BSGS)
     my_pts_s = args.steps * B * info.cycles * 1024 / (recs[-1][0] - t0)
     # known answer (outside the timed region, same engine and tables): SURVEY.md 8c
@@ -617,6 +623,8 @@ def bsgs_leg(D: Dist, W: Walks, args, clock):
         "ms_per_step": T / args.steps * 1e3,
         "seconds_timed": T,
         "bases_per_step": B,
+        "lanes_calibration": {"lanes": lanes_pick, "giant_points_per_s_at_2^21": rate_hi,
+                              "giant_points_per_s_at_2^20": rate_lo},
         "giant_points_per_s": D.world * args.steps * B * info.cycles * 1024 / T,
         "rank_giant_points_per_s": my_pts_s,
         "build_seconds": build_s,
@@ -1057,6 +1065,7 @@ def main():
                        "bases_per_step": prim["bases_per_step"],
                        "giant_points_per_step": prim["bases_per_step"] * info.cycles * 1024,
                        "walks_in_flight_per_gpu": args.walks,
+                       "lanes_calibration": prim["lanes_calibration"],
                        "parallelism": f"keyspace split x{D.world} (no collective)"},
             "devices_used": len(devices),
             "rehearsal": len(devices) < D.world,

@@ -119,6 +119,10 @@ int kh_set_geometry(kh_ctx *ctx, uint32_t lanes, uint32_t groups_per_launch);
 /* free the walks' device buffers (lane centres, scalars, inversion pad: up to 64 GB) between jobs;
  * the next scan allocates them again and starts its lanes afresh.  Tables and targets stay. */
 int kh_release_walk(kh_ctx *ctx);
+/* the BSGS walk's lanes per launch for large calls as the context's first large call timed them
+ * (DESIGN.md §2 "Placement"): *lanes = the count kept (0 = not yet timed), rates[0..1] = giant points/s
+ * of the halves walked at 2^21 and at 2^20 lanes (0 when not timed) */
+int kh_bsgs_geometry(kh_ctx *ctx, uint32_t *lanes, double rates[2]);
 int kh_synchronize(kh_ctx *ctx);
 
 /* ---- address / rmd160 / xpoint ------------------------------------------------------------ */

@@ -332,6 +332,11 @@ struct kh_ctx {
   uint32_t lanes_max = 1u << 18;
   uint32_t lanes_hb = KH_LANES_HB;
   uint32_t lanes_bsgs = KH_BSGS_LANES;  // the BSGS walk's large calls
+  // lanes the BSGS walk's large calls use once the context's first large call has timed the two
+  // candidates against each other (bsgs_calibrated); lanes_force: one call's forced count
+  uint32_t lanes_pick = 0, lanes_force = 0;
+  bool bsgs_calibrated = false;
+  double cal_rate[2] = {0, 0};  // giant points/s of the calibration's halves (2^21, 2^20 lanes)
   uint32_t groups_per_launch = 0;
   uint32_t lanes_alloc = 0;
   int scratch_h = 0;  // inversion-pad entries per lane in d_scratch
@@ -816,6 +821,16 @@ int kh_release_walk(kh_ctx *ctx) {
   ctx->lanes_alloc = 0;
   ctx->scratch_h = 0;
   ctx->cont_valid = false;
+  return KH_OK;
+}
+
+int kh_bsgs_geometry(kh_ctx *ctx, uint32_t *lanes, double rates[2]) {
+  if (!ctx) return KH_E_ARG;
+  if (lanes) *lanes = ctx->bsgs_calibrated ? ctx->lanes_pick : 0;
+  if (rates) {
+    rates[0] = ctx->cal_rate[0];
+    rates[1] = ctx->cal_rate[1];
+  }
   return KH_OK;
 }
 
@@ -2006,8 +2021,8 @@ constexpr uint64_t KH_BSGS_ROUND_POINTS = 1ULL << 34;
 }  // namespace
 
 // The giant-step scan behind kh_bsgs_scan (bases start + b*2N) and kh_bsgs_scan_list (any bases).
-static int bsgs_scan_impl(kh_ctx *ctx, const u256 &st, const std::vector<u256> *list, uint64_t n_bases,
-                          kh_bsgs_found *found, uint32_t cap, uint32_t *n_found) {
+static int bsgs_scan_one(kh_ctx *ctx, const u256 &st, const std::vector<u256> *list, uint64_t n_bases,
+                         kh_bsgs_found *found, uint32_t cap, uint32_t *n_found) {
   if (!ctx->bsgs_built) return KH_E_STATE;
   (void)hipSetDevice(ctx->device);
   *n_found = 0;
@@ -2046,7 +2061,7 @@ static int bsgs_scan_impl(kh_ctx *ctx, const u256 &st, const std::vector<u256> *
   // the largest power of two below it that fits (down to lanes_max, 2^18: one wave per slot).  The
   // count must tile the call (below): plan()'s balanced count for a 7274496-base call (1039214
   // lanes) walked 6 % slower than 2^20 (profiles/r05q_geom_lanes_count.json)
-  uint32_t lanes = ctx->lanes_max, wide = ctx->lanes_bsgs;
+  uint32_t lanes = ctx->lanes_max, wide = ctx->lanes_force ? ctx->lanes_force : ctx->lanes_pick ? ctx->lanes_pick : ctx->lanes_bsgs;
   if (const char *e = getenv("KH_BSGS_LANES")) wide = (uint32_t)strtoul(e, nullptr, 0);  // A/B knob
   if (getenv("KH_BSGS_NARROW")) wide = lanes;
   if (H == KH_WALK_HB) {
@@ -2425,6 +2440,55 @@ static int bsgs_scan_impl(kh_ctx *ctx, const u256 &st, const std::vector<u256> *
   }
   *n_found = nf;
   return nf > cap ? KH_E_OVERFLOW : KH_OK;
+}
+
+// The giant walk's rate at 2^21 and at 2^20 lanes differs by up to ~9 % either way from one process
+// (and box) to the next, the state holding for the process (DESIGN.md §2 "Placement").  A context's
+// first continuous call of at least 2^23 walk groups therefore walks its first half at 2^21 lanes and
+// its second at 2^20, times both on the walk's events, and keeps the faster count for its later large
+// calls (KH_BSGS_CALIBRATE=0, KH_BSGS_LANES or kh_set_geometry's lanes switch this off).  Every base
+// is walked once either way, so keys and candidates are those of an uncalibrated call.
+static int bsgs_scan_impl(kh_ctx *ctx, const u256 &st, const std::vector<u256> *list, uint64_t n_bases,
+                          kh_bsgs_found *found, uint32_t cap, uint32_t *n_found) {
+  if (!ctx->bsgs_built) return KH_E_STATE;
+  const kh_bsgs_info &I = ctx->info;
+  const uint64_t A_pts = I.cycles * 1024;
+  const uint64_t gpb = A_pts / (2 * KH_WALK_HB);
+  const uint32_t hi = ctx->lanes_bsgs, lo = ctx->lanes_bsgs / 2;
+  const char *cal = getenv("KH_BSGS_CALIBRATE");
+  const bool calibrate = !ctx->bsgs_calibrated && !list && A_pts == I.aux && A_pts % (2 * KH_WALK_HB) == 0 &&
+                         hi == KH_BSGS_LANES && lo > ctx->lanes_max && !(cal && atoi(cal) == 0) &&
+                         !getenv("KH_BSGS_LANES") && !getenv("KH_BSGS_NARROW") && !getenv("KH_NO_BIG_GROUPS") &&
+                         n_bases * gpb >= 4ull * hi && ctx->targets.size() == 1;
+  if (!calibrate) return bsgs_scan_one(ctx, st, list, n_bases, found, cap, n_found);
+  // halves in whole tiles of the wider count, so both tile exactly
+  const uint64_t tile = std::max<uint64_t>(1, hi / std::max<uint64_t>(1, gpb));
+  const uint64_t nb1 = std::max<uint64_t>(tile, (n_bases / 2) / tile * tile);
+  uint32_t n1 = 0, n2 = 0;
+  double ms[2] = {0, 0}, pts[2] = {0, 0};
+  int r = KH_OK;
+  for (int half = 0; half < 2; half++) {
+    const uint64_t nb = half ? n_bases - nb1 : nb1;
+    if (nb == 0) break;
+    const u256 s = half ? sc_add(st, sc_reduce(u256_from_u128((u128)nb1 * 2 * I.n))) : st;
+    ctx->lanes_force = half ? lo : hi;
+    const timing t0 = ctx->tm[2];
+    uint32_t *nf = half ? &n2 : &n1;
+    r = bsgs_scan_one(ctx, s, nullptr, nb, found ? found + std::min(n1, cap) : nullptr, cap - std::min(n1, cap), nf);
+    ctx->lanes_force = 0;
+    ms[half] = ctx->tm[2].ms - t0.ms;
+    pts[half] = (double)(ctx->tm[2].points - t0.points);
+    if (r && r != KH_E_OVERFLOW) return r;
+    if (half == 0 && ctx->found[0]) break;  // the key ended the call in its first half
+  }
+  *n_found = n1 + n2;
+  if (ms[0] > 0 && ms[1] > 0 && pts[0] > 0 && pts[1] > 0) {
+    ctx->lanes_pick = pts[0] / ms[0] >= pts[1] / ms[1] ? hi : lo;
+    ctx->bsgs_calibrated = true;
+    ctx->cal_rate[0] = pts[0] / ms[0] * 1e3;
+    ctx->cal_rate[1] = pts[1] / ms[1] * 1e3;
+  }
+  return *n_found > cap ? KH_E_OVERFLOW : r;
 }
 
 int kh_bsgs_scan(kh_ctx *ctx, const uint8_t start[32], uint64_t n_bases, kh_bsgs_found *found, uint32_t cap,

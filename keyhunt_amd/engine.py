@@ -78,6 +78,7 @@ def lib() -> ctypes.CDLL:
     L.kh_close.argtypes = [P]
     L.kh_set_geometry.argtypes = [P, ctypes.c_uint32, ctypes.c_uint32]
     L.kh_release_walk.argtypes = [P]
+    L.kh_bsgs_geometry.argtypes = [P, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_double * 2)]
     L.kh_synchronize.argtypes = [P]
     L.kh_scan_memory.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64)]
     L.kh_bsgs_set_bloom_multiplier.argtypes = [P, ctypes.c_uint32]
@@ -171,6 +172,12 @@ class Engine:
 
     def set_geometry(self, lanes: int = 0, groups_per_launch: int = 0) -> None:
         self._chk(lib().kh_set_geometry(self._ctx, lanes, groups_per_launch), "kh_set_geometry")
+
+    def bsgs_geometry(self) -> tuple[int, float, float]:
+        """(lanes kept for large BSGS calls or 0, giant points/s at 2^21 lanes, at 2^20 lanes)."""
+        lanes, rates = ctypes.c_uint32(), (ctypes.c_double * 2)()
+        self._chk(lib().kh_bsgs_geometry(self._ctx, ctypes.byref(lanes), ctypes.byref(rates)), "kh_bsgs_geometry")
+        return lanes.value, rates[0], rates[1]
 
     def release_walk(self) -> None:
         """Free the walks' lane arrays and inversion pad (kh_release_walk)."""

@@ -443,6 +443,43 @@ def test_calls_with_ragged_lane_tiles(oracle, lanes, calls):
     assert res[1][0] == res[3][0] == [(0, key)]
 
 
+def test_lane_calibration_same_results(oracle, monkeypatch):
+    """A context's first call of >= 2^23 walk groups walks its halves at 2^21 and 2^20 lanes and keeps
+    the faster count: the same first-level candidates as an uncalibrated call (KH_BSGS_CALIBRATE=0),
+    the key found in either half, and kh_bsgs_geometry reports both halves' rates."""
+    import keyhunt_amd as K
+    n, k = 1 << 32, 2                      # 8 groups per base: 2^20 bases = 2^23 groups
+    p = oracle.bsgs_params(n, k)
+    nb = 1 << 20
+    start = 0x3C3C3C3C3C000000
+    far = start - 777 * 2 * p.n
+    res = []
+    for calibrate in (True, False):
+        if calibrate:
+            monkeypatch.delenv("KH_BSGS_CALIBRATE", raising=False)
+        else:
+            monkeypatch.setenv("KH_BSGS_CALIBRATE", "0")
+        with K.Engine(0) as e:
+            e.bsgs_setup(n, k)
+            e.bsgs_build()
+            e.bsgs_set_targets([oracle.pubkey(far)])
+            c0 = e.bsgs_candidates()
+            assert e.bsgs_scan(start, nb) == []
+            res.append((e.bsgs_candidates() - c0, e.bsgs_geometry()))
+    assert res[0][0] == res[1][0]
+    lanes, r_hi, r_lo = res[0][1]
+    assert lanes in (1 << 21, 1 << 20) and r_hi > 0 and r_lo > 0
+    assert res[1][1] == (0, 0.0, 0.0)
+    monkeypatch.delenv("KH_BSGS_CALIBRATE", raising=False)
+    for where in (3, nb - 5):              # the key in the first half, then in the second
+        key = start + where * 2 * p.n + 999
+        with K.Engine(0) as e:
+            e.bsgs_setup(n, k)
+            e.bsgs_build()
+            e.bsgs_set_targets([oracle.pubkey(key)])
+            assert e.bsgs_scan(start, nb) == [(0, key)]
+
+
 def test_release_walk_between_calls(engine, oracle):
     """kh_release_walk frees the lane arrays and the pad: the next call allocates them again and
     starts its lanes afresh, with the same candidates and key as one uninterrupted call."""
