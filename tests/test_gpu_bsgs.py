@@ -382,15 +382,17 @@ def test_device_centres_equal_host_centres(mode, oracle, monkeypatch):
 
 def test_large_calls_use_wide_lanes_same_results(engine, oracle):
     """A call of >= 2^21 walk groups runs 2^21 lanes, >= 2^20 groups 2^20 lanes, smaller calls 2^18:
-    one call over 2^18 bases, the same bases in two and in four calls, and as a shuffled list all
+    one call over 2^19 bases, the same bases in two and in four calls, and as a shuffled list all
     probe the same points (same first-level candidates) and find the key in the same base."""
     import random
-    n, k = 1 << 32, 2                      # 32768 giant points per base: 8 groups of 4096
+    # M = 2^22: 16384 entries per shard, past the 10000-entry floor, so layer 1 has false positives
+    # to compare; 16384 giant points per base = 4 groups of 4096
+    n, k = 1 << 36, 16
     p = oracle.bsgs_params(n, k)
-    engine.bsgs_setup(n, k)
+    engine.bsgs_setup(n, k, layer1=1)
     engine.bsgs_build()
-    nb = 1 << 18
-    start = 0x5A5A5A5A5A000000
+    nb = 1 << 19
+    start = 0x5A5A5A5A5A0000000
     key = start + (nb - 3) * 2 * p.n + 31337
     far = start - 12345 * 2 * p.n       # no base of the call holds it: every point is walked
     bases = [start + b * 2 * p.n for b in range(nb)]
