@@ -57,12 +57,16 @@ and traffic = HBM bytes per launch from the PMC counters with the guide's gfx950
 (tools/pmc_summary.py), or null.
 cpu_baseline: rank 0 at N=1 only, on every leg the reference binary built from its own sources with
 its own optimisation flags (oracle/_ref/keyhunt_fast, oracle/Makefile.ref; kind "reference"), run for
---cpu-seconds-primary (BSGS, 60 s) / --cpu-seconds (rmd160, xpoint, 20 s) of its own stats clock twice: on the job's CPU share (cpu_threads: "value", "threads")
-and with -t 1 ("per_core"), its own last stats line parsed each time; the host's sockets, physical
-cores and threads per core come from lscpu.  "long_sample" quotes the newest >= 60-s measurement
-(bench.py --cpu-only --cpu-seconds 60, profiles/r*_cpu_baseline_*.json).  BSGS skips the reference's
+--cpu-seconds-primary (BSGS) / --cpu-seconds (rmd160, xpoint), 60 s each, of its own stats clock on the
+job's CPU share (cpu_threads: "value", "threads"), then for --cpu-seconds-per-core (30 s) with -t 1
+("per_core"), its own last stats line parsed each time; the host's sockets, physical cores and threads
+per core come from lscpu.  BSGS skips the reference's
 baby-step build: the engine writes the -S table files in the reference's format (kh_bsgs_save,
 byte-identical) and the reference reads them (-S -6).
+
+The line ends with "legs": one compact object per leg (value, unit, known-answer match, roofline frac,
+the CPU baseline's value and sample seconds), so the three legs' numbers sit in the last bytes of the
+line, which a runner that keeps only the tail of stdout still holds.
 """
 from __future__ import annotations
 
@@ -953,19 +957,20 @@ def cpu_baseline_xpoint(seconds: float, per_core_seconds: float | None = None):
                          per_core_seconds=per_core_seconds)
 
 
-def long_cpu_baseline() -> dict | None:
-    """The newest profiles/r*_cpu_baseline_*.json (bench.py --cpu-only --cpu-seconds 60 on a GPU box):
-    the reference's rates over >= 60 s of its own clock, at the job's threads and at -t 1 (SURVEY.md
-    8d), quoted beside this run's shorter samples; their per-leg objects, without the host block."""
-    import glob
-    fs = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_cpu_baseline_*.json")), reverse=True)
-    if not fs:
-        return None
-    d = json.load(open(fs[0]))
-    out = {"source": os.path.relpath(fs[0], REPO)}
-    for k in ("bsgs", "rmd160", "xpoint"):
-        if d.get(k):
-            out[k] = {kk: d[k].get(kk) for kk in ("threads", "per_core", "sample")}
+def legs_summary(line: dict) -> dict:
+    """The three legs in a few hundred bytes, for the end of the line: value, unit, the known-answer
+    match, the dominant kernel's roofline frac and the CPU baseline (value, threads, seconds)."""
+    out = {}
+    for name, leg in (("bsgs_b125" if "b 125" in line["config"]["workload"] else "bsgs_b130", line),
+                      ("rmd160_b66", line.get("secondary")), ("xpoint_b63", line.get("tertiary"))):
+        if not leg:
+            continue
+        cb = leg.get("cpu_baseline") or {}
+        th = cb.get("threads") or {}
+        out[name] = {"value": leg["value"], "unit": leg["unit"], "known_answer_match": leg["known_answer"]["match"],
+                     "frac": (leg.get("roofline") or {}).get("frac"),
+                     "cpu_baseline": {"value": cb.get("value"), "threads": th.get("threads"), "seconds": th.get("seconds"),
+                                      "per_core_seconds": (cb.get("per_core") or {}).get("seconds")} if cb else None}
     return out
 
 
@@ -995,11 +1000,13 @@ def main():
                     help="the same for each address-family leg (0: one 2^32-key chunk per step)")
     ap.add_argument("--steps-rmd", type=int, default=None)
     ap.add_argument("--warmup-rmd", type=int, default=None)
-    ap.add_argument("--cpu-seconds", type=float, default=20.0,
-                    help="CPU baseline of the rmd160 / xpoint legs: seconds of the reference's own stats clock per "
-                         "run (threads run, then -t 1)")
+    ap.add_argument("--cpu-seconds", type=float, default=60.0,
+                    help="CPU baseline of the rmd160 / xpoint legs: seconds of the reference's own stats clock on the "
+                         "job's threads (>= 60 s of steady state, SURVEY.md 8d)")
     ap.add_argument("--cpu-seconds-primary", type=float, default=60.0,
-                    help="the same for the BSGS leg (the line's cpu_baseline): >= 60 s of steady state, SURVEY.md 8d")
+                    help="the same for the BSGS leg (the line's cpu_baseline)")
+    ap.add_argument("--cpu-seconds-per-core", type=float, default=30.0,
+                    help="every leg's -t 1 run (the per-core rate beside the baseline's value)")
     ap.add_argument("--cpu-only", action="store_true",
                     help="only the CPU baselines of the three legs (the BSGS one still needs the GPU to write the "
                          "-S tables); prints one JSON object")
@@ -1028,8 +1035,9 @@ def main():
         C = BSGS_CONFIGS[args.config]
         W.engs[0].bsgs_setup(1 << 44, C["k"], layer1=args.layer1)
         W.engs[0].bsgs_build()
-        res = {"bsgs": cpu_baseline_bsgs(W.engs[0], C, args.cpu_seconds),
-               "rmd160": cpu_baseline_rmd160(args.cpu_seconds), "xpoint": cpu_baseline_xpoint(args.cpu_seconds),
+        pc = args.cpu_seconds_per_core
+        res = {"bsgs": cpu_baseline_bsgs(W.engs[0], C, args.cpu_seconds, pc),
+               "rmd160": cpu_baseline_rmd160(args.cpu_seconds, pc), "xpoint": cpu_baseline_xpoint(args.cpu_seconds, pc),
                "cpu_seconds": args.cpu_seconds, "workload": C["workload"]}
         W.close()
         json_out.write(json.dumps(res) + "\n")
@@ -1042,10 +1050,11 @@ def main():
     clock.stop()
     cpu_b = cpu_r = cpu_x = None
     if D.rank == 0 and D.world == 1 and not args.no_cpu_baseline and not args.cpu_only:
-        cpu_b = cpu_baseline_bsgs(W.engs[0], BSGS_CONFIGS[args.config], args.cpu_seconds_primary)
+        pc = args.cpu_seconds_per_core
+        cpu_b = cpu_baseline_bsgs(W.engs[0], BSGS_CONFIGS[args.config], args.cpu_seconds_primary, pc)
         if not args.no_secondary:
-            cpu_r = cpu_baseline_rmd160(args.cpu_seconds)
-            cpu_x = cpu_baseline_xpoint(args.cpu_seconds)
+            cpu_r = cpu_baseline_rmd160(args.cpu_seconds, pc)
+            cpu_x = cpu_baseline_xpoint(args.cpu_seconds, pc)
     W.close()
     ranks = D.gather({"rank": D.rank, "host": os.uname().nodename, "device": dev, "pci_bus_id": bdf,
                       "giant_points_per_s": prim["rank_giant_points_per_s"]})
@@ -1092,24 +1101,7 @@ def main():
                              "known_answer": leg["known_answer"], "sustained": leg["sustained"],
                              "roofline": leg["roofline"],
                              "cpu_baseline": cpu_r if key == "secondary" else cpu_x}
-        long_cpu = long_cpu_baseline()
-        if long_cpu:
-            for k, leg in (("cpu_baseline", line), ("secondary", line.get("secondary")), ("tertiary", line.get("tertiary"))):
-                tgt = leg if k == "cpu_baseline" else (leg or {})
-                cb = tgt.get("cpu_baseline")
-                key = {"cpu_baseline": "bsgs", "secondary": "rmd160", "tertiary": "xpoint"}[k]
-                if cb is not None and long_cpu.get(key):
-                    cb["long_sample"] = dict(long_cpu[key], source=long_cpu["source"])
-                    # this run's rates over the long record's (the spread between boxes and sample lengths)
-                    for kk in ("threads", "per_core"):
-                        mine, rec = cb.get(kk), (long_cpu[key].get(kk) or {})
-                        if mine and rec.get("value"):
-                            cb["long_sample"][kk + "_ratio"] = mine["value"] / rec["value"]
-                    if abs(cb["long_sample"].get("per_core_ratio", 1.0) - 1.0) > 0.1:
-                        cb["long_sample"]["per_core_note"] = (
-                            "the -t 1 rate is the host's single-core boost, which the load of the machine's other "
-                            "tenants sets (the 256-CPU host is shared; this run's host_state gives its load average "
-                            "and the clock of the CPU the reference ran on); both samples are >= 60 s")
+        line["legs"] = legs_summary(line)
         json_out.write(json.dumps(line) + "\n")
         json_out.flush()
     D.close()

@@ -123,6 +123,11 @@ int kh_release_walk(kh_ctx *ctx);
  * (DESIGN.md §2 "Placement"): *lanes = the count kept (0 = not yet timed), rates[0..1] = giant points/s
  * of the halves walked at 2^21 and at 2^20 lanes (0 when not timed) */
 int kh_bsgs_geometry(kh_ctx *ctx, uint32_t *lanes, double rates[2]);
+/* diagnostics (DESIGN.md §2 "Placement"): where the BSGS walk's buffers sit in the device's virtual
+ * address space.  out[0..1] = layer-1 address and bytes, out[2..3] = the inversion pad's, out[4..5] =
+ * layer 2's, out[6] = lanes allocated, out[7] = pad rows per lane.  Engine-only: the reference has no
+ * counterpart. */
+int kh_debug_layout(kh_ctx *ctx, uint64_t out[8]);
 int kh_synchronize(kh_ctx *ctx);
 
 /* ---- address / rmd160 / xpoint ------------------------------------------------------------ */

@@ -335,6 +335,7 @@ struct kh_ctx {
   // lanes the BSGS walk's large calls use once the context's first large call has timed the two
   // candidates against each other (bsgs_calibrated); lanes_force: one call's forced count
   uint32_t lanes_pick = 0, lanes_force = 0;
+  uint32_t lanes_used = 0;  // lanes the last large-group BSGS call walked (the calibration checks it)
   bool bsgs_calibrated = false;
   double cal_rate[2] = {0, 0};  // giant points/s of the calibration's halves (2^21, 2^20 lanes)
   uint32_t groups_per_launch = 0;
@@ -834,12 +835,29 @@ int kh_bsgs_geometry(kh_ctx *ctx, uint32_t *lanes, double rates[2]) {
   return KH_OK;
 }
 
+int kh_debug_layout(kh_ctx *ctx, uint64_t out[8]) {
+  if (!ctx || !out) return KH_E_ARG;
+  out[0] = (uint64_t)(uintptr_t)ctx->d_bl[0];
+  out[1] = ctx->d_bl[0] ? 256 * ctx->bd[0].stride + 4 : 0;
+  out[2] = (uint64_t)(uintptr_t)ctx->d_scratch;
+  out[3] = (uint64_t)ctx->lanes_alloc * ctx->scratch_h * 32;
+  out[4] = (uint64_t)(uintptr_t)ctx->d_bl[1];
+  out[5] = ctx->d_bl[1] ? 256 * ctx->bd[1].stride + 4 : 0;
+  out[6] = ctx->lanes_alloc;
+  out[7] = (uint64_t)ctx->scratch_h;
+  return KH_OK;
+}
+
 int kh_set_geometry(kh_ctx *ctx, uint32_t lanes, uint32_t groups_per_launch) {
   if (!ctx) return KH_E_ARG;
   ctx->lanes_max = lanes ? lanes : (1u << 18);
   ctx->lanes_hb = lanes ? lanes : KH_LANES_HB;
   ctx->lanes_bsgs = lanes ? lanes : KH_BSGS_LANES;
   ctx->groups_per_launch = groups_per_launch;
+  // an explicit geometry overrides an earlier calibration's pick (and a default one calibrates again)
+  ctx->lanes_pick = 0;
+  ctx->bsgs_calibrated = false;
+  ctx->cal_rate[0] = ctx->cal_rate[1] = 0;
   return KH_OK;
 }
 
@@ -906,6 +924,7 @@ int kh_set_targets(kh_ctx *ctx, const uint8_t *rows, uint64_t n, uint64_t bloom_
   for (uint64_t i = 0; i < n; i++) memcpy(&ctx->rows[i * 20], v[i].data(), 20);
   ctx->n_rows = n;
   ctx->vanity = false;
+  ctx->cont_valid = false;  // the next walk may need another pad (dense vs sparse): start its lanes again
   ctx->probe_len = 20;
   ctx->v_ranges.clear();
   ctx->t_entries = bloom_entries(bloom_items ? bloom_items : n);
@@ -926,6 +945,7 @@ int kh_set_vanity(kh_ctx *ctx, const uint8_t *ranges, uint64_t n, uint32_t probe
   ctx->rows.clear();
   ctx->n_rows = 0;
   ctx->vanity = true;
+  ctx->cont_valid = false;  // a vanity walk writes the dense pad: never resume an exact-target walk's lanes
   ctx->probe_len = probe_len;
   (void)hipFree(ctx->d_tblk);  // prefixes probe the reference-layout bloom
   ctx->d_tblk = nullptr;
@@ -1047,8 +1067,14 @@ int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride_be[32], u
   const bool inter = H == KH_WALK_HB && (uint64_t)jg.L * jg.gpl == total_groups;
   r = get_table(ctx, stride, &tab, H, inter ? jg.L : 1);
   if (r) return r;
+  // the pad's rows per lane (the walk below probes the blocked target filter exactly when A.tblk is
+  // set): a resumed walk must find at least that many rows, since the exact-target (sparse) pad is half
+  // the dense one a vanity or reference-bloom walk writes
+  const bool tblk = !(ctx->vanity || getenv("KH_REF_TARGET_BLOOM")) && ctx->d_tblk;
+  const int pad_rows = zg ? H : walk_pad_rows(km, tblk, H);  // km keeps KM_ENDO: as launch_walk sees it
   const bool resume = inter && ctx->cont_valid && ctx->cont_kind == 1 && ctx->cont_km == km &&
-                      ctx->cont_L == jg.L && ctx->cont_H == H && u256_cmp(ctx->cont_next, st) == 0 &&
+                      ctx->cont_L == jg.L && ctx->cont_H == H && ctx->scratch_h >= pad_rows &&
+                      ctx->lanes_alloc >= jg.L && u256_cmp(ctx->cont_next, st) == 0 &&
                       u256_cmp(ctx->cont_stride, stride) == 0;
   ctx->cont_valid = false;
   // lane g's first centre: offset H + g * lane_step, lane_step = 2H (interleaved) or gpl * 2H; the
@@ -1057,10 +1083,7 @@ int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride_be[32], u
   const u256 lane_step = mul_stride(inter ? (u128)(2 * H) : (u128)jg.gpl * (2 * H));
   const u256 s0 = sc_add(st, mul_stride((u128)H));
   if (!resume) {
-    // the pad's rows per lane, before the centres are set (the walk below probes the blocked target
-    // filter exactly when A.tblk is set)
-    const bool tblk = !(ctx->vanity || getenv("KH_REF_TARGET_BLOOM")) && ctx->d_tblk;
-    r = ensure_lanes(ctx, jg.L, zg ? H : walk_pad_rows(km, tblk, H));  // km keeps KM_ENDO: as launch_walk sees it
+    r = ensure_lanes(ctx, jg.L, pad_rows);  // before the centres are set
     if (r) return r;
     r = run_setup_prog(ctx, s0, lane_step, jg.L);
     if (r) return r;
@@ -1079,7 +1102,7 @@ int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride_be[32], u
   A.zhalf = zg ? (uint32_t)H : 0;
   A.bloom = ctx->d_tbloom;
   A.bd = ctx->tbd;
-  A.tblk = ctx->vanity || getenv("KH_REF_TARGET_BLOOM") ? nullptr : ctx->d_tblk;
+  A.tblk = tblk ? ctx->d_tblk : nullptr;
   A.tblocks = ctx->tblocks;
   A.hit_count = ctx->d_hit_count;
   A.hits = ctx->d_hits;
@@ -2083,6 +2106,7 @@ static int bsgs_scan_one(kh_ctx *ctx, const u256 &st, const std::vector<u256> *l
       ctx->err.clear();
     }
   }
+  ctx->lanes_used = H == KH_WALK_HB ? lanes : 0;
   job_geom jc{};
   uint64_t gpr = 0;  // continuous mode: groups per lane per round
   if (cont) {
@@ -2444,10 +2468,12 @@ static int bsgs_scan_one(kh_ctx *ctx, const u256 &st, const std::vector<u256> *l
 
 // The giant walk's rate at 2^21 and at 2^20 lanes differs by up to ~9 % either way from one process
 // (and box) to the next, the state holding for the process (DESIGN.md §2 "Placement").  A context's
-// first continuous call of at least 2^23 walk groups therefore walks its first half at 2^21 lanes and
-// its second at 2^20, times both on the walk's events, and keeps the faster count for its later large
-// calls (KH_BSGS_CALIBRATE=0, KH_BSGS_LANES or kh_set_geometry's lanes switch this off).  Every base
-// is walked once either way, so keys and candidates are those of an uncalibrated call.
+// first continuous call of at least 2^23 walk groups therefore walks its quarters at 2^21, 2^20, 2^20
+// and 2^21 lanes (ABBA, so a linear drift of clock or power between the quarters cancels), times each
+// on the walk's events, and keeps the faster count for its later large calls (KH_BSGS_CALIBRATE=0,
+// KH_BSGS_LANES or kh_set_geometry's lanes switch this off).  A quarter that could not take its count
+// (device memory) leaves the context uncalibrated.  Every base is walked once either way, so keys and
+// candidates are those of an uncalibrated call.
 static int bsgs_scan_impl(kh_ctx *ctx, const u256 &st, const std::vector<u256> *list, uint64_t n_bases,
                           kh_bsgs_found *found, uint32_t cap, uint32_t *n_found) {
   if (!ctx->bsgs_built) return KH_E_STATE;
@@ -2461,28 +2487,36 @@ static int bsgs_scan_impl(kh_ctx *ctx, const u256 &st, const std::vector<u256> *
                          !getenv("KH_BSGS_LANES") && !getenv("KH_BSGS_NARROW") && !getenv("KH_NO_BIG_GROUPS") &&
                          n_bases * gpb >= 4ull * hi && ctx->targets.size() == 1;
   if (!calibrate) return bsgs_scan_one(ctx, st, list, n_bases, found, cap, n_found);
-  // halves in whole tiles of the wider count, so both tile exactly
+  // quarters in whole tiles of the wider count, so each tiles exactly; the last takes the rest
   const uint64_t tile = std::max<uint64_t>(1, hi / std::max<uint64_t>(1, gpb));
-  const uint64_t nb1 = std::max<uint64_t>(tile, (n_bases / 2) / tile * tile);
-  uint32_t n1 = 0, n2 = 0;
+  const uint64_t nbq = std::max<uint64_t>(tile, (n_bases / 4) / tile * tile);
+  static const int side[4] = {0, 1, 1, 0};  // 0: hi lanes, 1: lo lanes
+  uint32_t nf_all = 0;
   double ms[2] = {0, 0}, pts[2] = {0, 0};
+  bool exact = true;
   int r = KH_OK;
-  for (int half = 0; half < 2; half++) {
-    const uint64_t nb = half ? n_bases - nb1 : nb1;
-    if (nb == 0) break;
-    const u256 s = half ? sc_add(st, sc_reduce(u256_from_u128((u128)nb1 * 2 * I.n))) : st;
-    ctx->lanes_force = half ? lo : hi;
+  uint64_t done_b = 0;
+  for (int q = 0; q < 4 && done_b < n_bases; q++) {
+    const uint64_t nb = q == 3 ? n_bases - done_b : std::min(nbq, n_bases - done_b);
+    const u256 s = sc_add(st, sc_reduce(u256_from_u128((u128)done_b * 2 * I.n)));
+    const uint32_t want = side[q] ? lo : hi;
+    ctx->lanes_force = want;
     const timing t0 = ctx->tm[2];
-    uint32_t *nf = half ? &n2 : &n1;
-    r = bsgs_scan_one(ctx, s, nullptr, nb, found ? found + std::min(n1, cap) : nullptr, cap - std::min(n1, cap), nf);
+    uint32_t nf = 0;
+    const uint32_t off = std::min(nf_all, cap);
+    r = bsgs_scan_one(ctx, s, nullptr, nb, found ? found + off : nullptr, cap - off, &nf);
     ctx->lanes_force = 0;
-    ms[half] = ctx->tm[2].ms - t0.ms;
-    pts[half] = (double)(ctx->tm[2].points - t0.points);
+    if (ctx->lanes_used != want) exact = false;
+    ms[side[q]] += ctx->tm[2].ms - t0.ms;
+    pts[side[q]] += (double)(ctx->tm[2].points - t0.points);
+    nf_all += nf;
+    done_b += nb;
     if (r && r != KH_E_OVERFLOW) return r;
-    if (half == 0 && ctx->found[0]) break;  // the key ended the call in its first half
+    if (ctx->found[0]) break;  // the key ended the call
   }
-  *n_found = n1 + n2;
-  if (ms[0] > 0 && ms[1] > 0 && pts[0] > 0 && pts[1] > 0) {
+  // the rest of the call, when the key ended it early, is not walked (as in an uncalibrated call)
+  *n_found = nf_all;
+  if (exact && ms[0] > 0 && ms[1] > 0 && pts[0] > 0 && pts[1] > 0) {
     ctx->lanes_pick = pts[0] / ms[0] >= pts[1] / ms[1] ? hi : lo;
     ctx->bsgs_calibrated = true;
     ctx->cal_rate[0] = pts[0] / ms[0] * 1e3;

@@ -78,12 +78,14 @@ def lib() -> ctypes.CDLL:
     L.kh_close.argtypes = [P]
     L.kh_set_geometry.argtypes = [P, ctypes.c_uint32, ctypes.c_uint32]
     L.kh_release_walk.argtypes = [P]
+    L.kh_debug_layout.argtypes = [P, ctypes.POINTER(ctypes.c_uint64 * 8)]
     L.kh_bsgs_geometry.argtypes = [P, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_double * 2)]
     L.kh_synchronize.argtypes = [P]
     L.kh_scan_memory.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64)]
     L.kh_bsgs_set_bloom_multiplier.argtypes = [P, ctypes.c_uint32]
     L.kh_set_rmd_batch.argtypes = [P, ctypes.c_uint32]
     L.kh_set_targets.argtypes = [P, u8p, ctypes.c_uint64, ctypes.c_uint64]
+    L.kh_set_vanity.argtypes = [P, u8p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64]
     L.kh_scan.argtypes = [P, u8p, u8p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(KhHit),
                           ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]
     L.kh_bsgs_setup.argtypes = [P, ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(KhBsgsInfo)]
@@ -179,6 +181,13 @@ class Engine:
         self._chk(lib().kh_bsgs_geometry(self._ctx, ctypes.byref(lanes), ctypes.byref(rates)), "kh_bsgs_geometry")
         return lanes.value, rates[0], rates[1]
 
+    def debug_layout(self) -> dict:
+        """Device addresses and sizes of layer 1, the inversion pad and layer 2 (kh_debug_layout)."""
+        o = (ctypes.c_uint64 * 8)()
+        self._chk(lib().kh_debug_layout(self._ctx, ctypes.byref(o)), "kh_debug_layout")
+        return {"layer1": [hex(o[0]), o[1]], "pad": [hex(o[2]), o[3]], "layer2": [hex(o[4]), o[5]],
+                "lanes": o[6], "pad_rows": o[7]}
+
     def release_walk(self) -> None:
         """Free the walks' lane arrays and inversion pad (kh_release_walk)."""
         self._chk(lib().kh_release_walk(self._ctx), "kh_release_walk")
@@ -195,6 +204,12 @@ class Engine:
         buf = b"".join(rows)
         assert all(len(r) == 20 for r in rows)
         self._chk(lib().kh_set_targets(self._ctx, buf, len(rows), bloom_items), "kh_set_targets")
+
+    def set_vanity(self, ranges: list[tuple[bytes, bytes]], probe_len: int, bloom_items: int = 0) -> None:
+        """Vanity prefixes (kh_set_vanity): hash160 ranges [A, B], the bloom keyed on A's first probe_len bytes."""
+        assert all(len(a) == 20 and len(b) == 20 for a, b in ranges)
+        buf = b"".join(a + b for a, b in ranges)
+        self._chk(lib().kh_set_vanity(self._ctx, buf, len(ranges), probe_len, bloom_items), "kh_set_vanity")
 
     def targets_save(self, path: str) -> None:
         """Write the -S target file (data_<hex>.dat layout) of the current targets to path."""

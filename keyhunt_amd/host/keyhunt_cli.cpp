@@ -1679,21 +1679,28 @@ int main(int argc, char **argv) {
       }
       FILE *df = fopen(data_file.c_str(), "rb");
       if (df) {
+        fseeko(df, 0, SEEK_END);
+        const off_t size = ftello(df);
         fclose(df);
         have_data = true;
         printf("[+] Reading file %s\n", data_file.c_str());
+        // a file too short for the bloom checksum or its struct bloom fails the reference's first two
+        // reads (readFileAddress, keyhunt.cpp:7068, 7076; the caller's message at 1347): e.g. the empty
+        // data file an -S --mapped-chunks N>1 run leaves behind (below)
+        if (size < 32 + 112) {  // checksum + struct bloom (112 B, kh_mapped.h struct_bloom)
+          fprintf(stderr, "[E] %s reading file, code line %d\n", size < 32 ? "Errore" : "Error", size < 32 ? 7068 : 7076);
+          fprintf(stderr, "[E] Unenexpected error\n");
+          return EXIT_FAILURE;
+        }
       }
     }
     // -S with --mapped and no cache yet: the target filter is the mapped file's (bloom.dat, or the
     // --mapped / --bloom-file name), and that filter -- its struct bloom and bits -- goes into the
     // data file (keyhunt.cpp:7033-7049, 7630-7706, 7756-7855).  With --mapped-chunks above 1 the
-    // reference writes bloom.bytes from its FIRST chunk's mapping, past that mapping's end: refused
+    // reference writes bloom.bytes from its FIRST chunk's mapping (bloom.bf = bf_chunks[0],
+    // bloom.cpp:395), past that mapping's end (handled below)
     const bool mapped_data = opt.mapped && opt.save_read && opt.mode != MODE_VANITY && !have_data;
-    if (mapped_data && opt.mapped_chunks > 1) {
-      fprintf(stderr, "[E] -S with --mapped-chunks above 1: the reference writes the data file from its first chunk's "
-                      "mapping past that mapping's end; not provided\n");
-      return EXIT_FAILURE;
-    }
+    const bool mapped_data_chunked = mapped_data && opt.mapped_chunks > 1;
     mapped::filter tf;
     std::vector<uint8_t> adds;  // the items the reference adds to its (mapped) target bloom
     std::vector<uint8_t> *addp = opt.mapped ? &adds : nullptr;
@@ -1714,9 +1721,23 @@ int main(int argc, char **argv) {
           adds.insert(adds.end(), opt.vanity.ranges.begin() + j, opt.vanity.ranges.begin() + j + L);
         ok = mapped::targets(opt.vanity.total, adds, L);
       } else {
-        ok = mapped::targets(items, adds, 20, mapped_data ? &tf : nullptr);
+        ok = mapped::targets(items, adds, 20, mapped_data && !mapped_data_chunked ? &tf : nullptr);
       }
       if (!ok) return EXIT_FAILURE;
+    }
+    if (mapped_data_chunked) {
+      // The reference maps and fills the chunk files, opens data_<hex>.dat for writing, then hashes
+      // bloom.bytes from the first chunk's mapping and dies of SIGBUS past its end (writeFileIfNeeded,
+      // keyhunt.cpp:7770-7809): the chunk files hold the filter, the data file is left empty, and the next
+      // -S run fails reading it (tests/golden/ref_mapped.json "rmd160_S_mapped_chunks").  This CLI leaves
+      // the same files and exits with an error status instead of the signal.
+      FILE *f = fopen(data_file.c_str(), "wb");
+      if (f) fclose(f);
+      fflush(stdout);
+      fprintf(stderr, "[E] -S with --mapped-chunks %u: the data file would be written from the first chunk's mapping "
+                      "past its end (the reference dies of SIGBUS there); %s left empty\n",
+              (unsigned)opt.mapped_chunks, data_file.c_str());
+      return EXIT_FAILURE;
     }
     if (!have_data)
       printf("[+] Sorting data ... done! %llu values were loaded and sorted\n", (unsigned long long)(rows.size() / 20));

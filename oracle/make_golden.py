@@ -545,6 +545,12 @@ MAPPED_SEQS = [
     ("bsgs_S_mapped_fresh_then_rerun", [BSGS_ARGS + ["-S", "--mapped"], BSGS_ARGS + ["-S", "--mapped"]]),
     ("xpoint_S_mapped_override", [["-m", "xpoint", "-f", "1to63_65.txt", "-r", "1:100000", "-n", "0x100000", "-t", "4",
                                    "-S", "--mapped", "--mapped-size", "1m"]]),
+    # -S with --mapped-chunks 4: the data file is hashed and written from the first chunk's mapping
+    # (bloom.bf = bf_chunks[0], bloom.cpp:395) for bloom.bytes, past that mapping's end
+    # (keyhunt.cpp:7770-7809): SIGBUS (-7) after the chunk files are filled and data_<hex>.dat is opened,
+    # so the data file stays empty; the rerun fails reading it (7068, 1347) with exit 1
+    ("rmd160_S_mapped_chunks", [RMD_ARGS + ["-S", "--mapped", "--mapped-chunks", "4"],
+                                RMD_ARGS + ["-S", "--mapped", "--mapped-chunks", "4"]]),
 ]
 
 
@@ -596,7 +602,10 @@ def gen_mapped(only: list[str] | None = None) -> None:
                         text += open(os.path.join(td, fn)).read()
                         os.remove(os.path.join(td, fn))
                 hits = sorted(parse_keyfound(text), key=lambda h: int(h["key"], 16))
-                steps.append({"argv": argv, "exit": p.returncode, "hits": hits, "files": mapped_files(td)})
+                st = {"argv": argv, "exit": p.returncode, "hits": hits, "files": mapped_files(td)}
+                if p.returncode:  # a failing run: the reference's [E] lines (stdout is lost on a signal)
+                    st["stderr_E"] = [ln for ln in p.stderr.splitlines() if ln.startswith("[E]")]
+                steps.append(st)
                 print(name, argv[-3:], p.returncode, len(hits), {k: v[0] if k.endswith("*") is False else "..." for k, v in steps[-1]["files"].items()}, flush=True)
         res[name] = steps
     with open(out_path, "w") as f:

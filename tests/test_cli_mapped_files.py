@@ -34,6 +34,11 @@ def test_address_family_mapped_files_match_reference(name):
             if "-t" in argv:
                 i = argv.index("-t")
                 del argv[i:i + 2]
-            subprocess.run([CLI] + argv + ["-q", "-s", "0"], cwd=td, capture_output=True, text=True, timeout=120,
-                           env=env)
+            p = subprocess.run([CLI] + argv + ["-q", "-s", "0"], cwd=td, capture_output=True, text=True, timeout=120,
+                               env=env)
             assert mapped_files(td) == step["files"], (k, step["argv"])
+            if step["exit"] < 0:       # the reference died of a signal (-S --mapped-chunks N>1): an error here
+                assert p.returncode != 0 and "[E]" in p.stderr, (k, p.returncode, p.stderr)
+            elif step.get("stderr_E"):  # a clean failure before any device work: the same [E] lines and status
+                assert p.returncode == step["exit"], (k, p.returncode, p.stderr)
+                assert [ln for ln in p.stderr.splitlines() if ln.startswith("[E]")] == step["stderr_E"]

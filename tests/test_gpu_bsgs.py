@@ -414,45 +414,61 @@ def test_large_calls_use_wide_lanes_same_results(engine, oracle):
     assert [r[2] for r in runs[4:]] == [[(0, key)]] * 4
 
 
-@pytest.mark.parametrize("lanes,calls", [(64, [17, 17, 5]), (64, [16, 16, 2]), (32, [9, 9, 9])])
+# Past the 10000-entry floor (keyhunt.cpp:7605-7626): n = 2^36, k = 16 gives M = 2^22, 16384 babies per
+# shard, so layer 1 has false positives at its design rate (~6.6e-7 per giant point, ~0.011 per base of
+# 16384 giant points = 4 groups of 4096).  The tests below walk thousands of bases, so "same first-level
+# candidates" compares dozens of candidates, not zero with zero, and each also checks the giant points
+# the walk counted (kh_kernel_time: n_bases x 16384 for a call that finds nothing), so a group skipped
+# or walked twice fails even where no candidate falls in it.
+N36, K16 = 1 << 36, 16
+
+
+def _walked(e):
+    from keyhunt_amd.engine import TIME_BSGS
+    return e.kernel_time(TIME_BSGS)[2]
+
+
+@pytest.mark.parametrize("lanes,calls", [(1024, [1501, 1501, 333]), (1024, [1536, 1536, 256]), (512, [900, 900, 900])])
 def test_calls_with_ragged_lane_tiles(oracle, lanes, calls):
-    """Calls whose groups the lanes do not tile exactly (17 bases = 136 groups over 64 lanes: 3
-    groups per lane, 56 unprobed lane-groups past the end) give the same candidates and keys as one
-    call over all the bases: a following call starts its lanes again rather than continuing lanes
-    that ended past its first group."""
+    """Calls whose groups the lanes do not tile exactly (1501 bases = 6004 groups over 1024 lanes: 6
+    groups per lane on 1001 lanes, 2 unprobed lane-groups past the end) give the same candidates and keys
+    as one call over all the bases: a following call starts its lanes again rather than continuing lanes
+    that ended past its first group.  The other cases tile exactly (1024 x 6, 512 -> 450 x 8)."""
     import keyhunt_amd as K
-    n, k = 1 << 32, 2                      # 8 groups of 4096 giant points per base
-    p = oracle.bsgs_params(n, k)
+    p = oracle.bsgs_params(N36, K16)
+    assert p.aux == 16384
     total = sum(calls)
     start = 0x13579BDF02468000
     key = start + (calls[0] + calls[1] // 2) * 2 * p.n + 2024   # in the second call
     far = start - 99 * 2 * p.n
     with K.Engine(0, lanes, 0) as e:
-        e.bsgs_setup(n, k)
+        e.bsgs_setup(N36, K16, layer1=K.KH_LAYER1_BLOCKED)
         e.bsgs_build()
         res = []
         for plan in ([total], calls):
             for tgt in (far, key):
                 e.bsgs_set_targets([oracle.pubkey(tgt)])
                 c0 = e.bsgs_candidates()
+                e.kernel_time_reset()
                 got, b = [], 0
                 for nb in plan:
                     got += e.bsgs_scan(start + b * 2 * p.n, nb)
                     b += nb
-                res.append((got, e.bsgs_candidates() - c0))
+                res.append((got, e.bsgs_candidates() - c0, _walked(e)))
     assert res[0][0] == res[2][0] == []
-    assert res[0][1] == res[2][1]          # the same first-level false positives (often none)
+    assert res[0][1] == res[2][1] and res[0][1] > 0    # the same first-level false positives
+    assert res[0][2] == res[2][2] == total * p.aux     # every giant point walked once
     assert res[1][0] == res[3][0] == [(0, key)]
 
 
 def test_lane_calibration_same_results(oracle, monkeypatch):
-    """A context's first call of >= 2^23 walk groups walks its halves at 2^21 and 2^20 lanes and keeps
-    the faster count: the same first-level candidates as an uncalibrated call (KH_BSGS_CALIBRATE=0),
-    the key found in either half, and kh_bsgs_geometry reports both halves' rates."""
+    """A context's first call of >= 2^23 walk groups walks its quarters at 2^21, 2^20, 2^20 and 2^21
+    lanes and keeps the faster count: the same first-level candidates and walked points as an
+    uncalibrated call (KH_BSGS_CALIBRATE=0), the key found in any quarter, and kh_bsgs_geometry reports
+    both counts' rates."""
     import keyhunt_amd as K
-    n, k = 1 << 32, 2                      # 8 groups per base: 2^20 bases = 2^23 groups
-    p = oracle.bsgs_params(n, k)
-    nb = 1 << 20
+    p = oracle.bsgs_params(N36, K16)
+    nb = 1 << 21                           # 4 groups per base: 2^23 groups
     start = 0x3C3C3C3C3C000000
     far = start - 777 * 2 * p.n
     res = []
@@ -462,21 +478,22 @@ def test_lane_calibration_same_results(oracle, monkeypatch):
         else:
             monkeypatch.setenv("KH_BSGS_CALIBRATE", "0")
         with K.Engine(0) as e:
-            e.bsgs_setup(n, k)
+            e.bsgs_setup(N36, K16, layer1=K.KH_LAYER1_BLOCKED)
             e.bsgs_build()
             e.bsgs_set_targets([oracle.pubkey(far)])
             c0 = e.bsgs_candidates()
             assert e.bsgs_scan(start, nb) == []
-            res.append((e.bsgs_candidates() - c0, e.bsgs_geometry()))
-    assert res[0][0] == res[1][0]
-    lanes, r_hi, r_lo = res[0][1]
+            res.append((e.bsgs_candidates() - c0, _walked(e), e.bsgs_geometry()))
+    assert res[0][0] == res[1][0] and res[0][0] > 1000
+    assert res[0][1] == res[1][1] == nb * p.aux
+    lanes, r_hi, r_lo = res[0][2]
     assert lanes in (1 << 21, 1 << 20) and r_hi > 0 and r_lo > 0
-    assert res[1][1] == (0, 0.0, 0.0)
+    assert res[1][2] == (0, 0.0, 0.0)
     monkeypatch.delenv("KH_BSGS_CALIBRATE", raising=False)
-    for where in (3, nb - 5):              # the key in the first half, then in the second
+    for where in (3, nb // 2 - 7, nb - 5):  # the key in the first, the second / third, the last quarter
         key = start + where * 2 * p.n + 999
         with K.Engine(0) as e:
-            e.bsgs_setup(n, k)
+            e.bsgs_setup(N36, K16, layer1=K.KH_LAYER1_BLOCKED)
             e.bsgs_build()
             e.bsgs_set_targets([oracle.pubkey(key)])
             assert e.bsgs_scan(start, nb) == [(0, key)]
@@ -484,58 +501,72 @@ def test_lane_calibration_same_results(oracle, monkeypatch):
 
 def test_release_walk_between_calls(engine, oracle):
     """kh_release_walk frees the lane arrays and the pad: the next call allocates them again and
-    starts its lanes afresh, with the same candidates and key as one uninterrupted call."""
-    n, k = 1 << 32, 2
-    p = oracle.bsgs_params(n, k)
-    engine.bsgs_setup(n, k)
+    starts its lanes afresh, with the same candidates, walked points and key as uninterrupted calls."""
+    import keyhunt_amd as K
+    p = oracle.bsgs_params(N36, K16)
+    engine.bsgs_setup(N36, K16, layer1=K.KH_LAYER1_BLOCKED)
     engine.bsgs_build()
     start = 0x2468ACE0000000
-    key = start + 6 * 2 * p.n + 4242
+    far = start - 4321 * 2 * p.n
+    key = start + 3000 * 2 * p.n + 4242    # in the second call
     res = []
-    for release in (False, True):
-        engine.bsgs_set_targets([oracle.pubkey(key)])
-        c0 = engine.bsgs_candidates()
-        got = engine.bsgs_scan(start, 4)
-        if release:
-            engine.release_walk()
-        got += engine.bsgs_scan(start + 4 * 2 * p.n, 4)
-        res.append((got, engine.bsgs_candidates() - c0))
-    assert res[0] == res[1] and res[0][0] == [(0, key)]
+    for tgt in (far, key):
+        for release in (False, True):
+            engine.bsgs_set_targets([oracle.pubkey(tgt)])
+            c0 = engine.bsgs_candidates()
+            engine.kernel_time_reset()
+            got = engine.bsgs_scan(start, 2048)
+            if release:
+                engine.release_walk()
+            got += engine.bsgs_scan(start + 2048 * 2 * p.n, 2048)
+            res.append((got, engine.bsgs_candidates() - c0, _walked(engine)))
+    assert res[0] == res[1] and res[0][0] == [] and res[0][1] > 0 and res[0][2] == 4096 * p.aux
+    assert res[2][:2] == res[3][:2] and res[2][0] == [(0, key)]
 
 
 def test_bsgs_lanes_continue_across_calls(engine, oracle):
     """Continuous mode keeps its (interleaved) lanes across kh_bsgs_scan calls whose bases follow
-    on: scanning 8 bases in one call, in 4 calls of 2, or with a jump and a target switch in
-    between gives the same first-level candidates and finds the key in the same base."""
-    n, k = 1 << 32, 2                      # M = 2^17, 32768 giant points per base: 4096-point groups
-    p = oracle.bsgs_params(n, k)
-    engine.bsgs_setup(n, k, layer1=1)
+    on: scanning 4096 bases in one call, in 4 calls of 1024, in uneven calls, or with a jump and a
+    target switch in between gives the same first-level candidates and walked points and finds the key
+    in the same base."""
+    import keyhunt_amd as K
+    from keyhunt_amd.engine import TIME_SETUP
+    p = oracle.bsgs_params(N36, K16)
+    engine.bsgs_setup(N36, K16, layer1=K.KH_LAYER1_BLOCKED)
     engine.bsgs_build()
+    total = 4096
     start = 0x1234567890000
-    key = start + 6 * 2 * p.n + 777        # in base 6
-    q = oracle.pubkey(key)
-    engine.bsgs_set_targets([q])
-    c0 = engine.bsgs_candidates()
-    assert engine.bsgs_scan(start, 8) == [(0, key)]
-    one_call = engine.bsgs_candidates() - c0
-    for plan in ([2, 2, 2, 2], [1, 1, 3, 3], "jump"):
+    key = start + 4000 * 2 * p.n + 777     # in the last call of every plan
+    far = start - 5555 * 2 * p.n
+    for tgt in (far, key):
+        q = oracle.pubkey(tgt)
         engine.bsgs_set_targets([q])
         c0 = engine.bsgs_candidates()
-        got, b = [], 0
-        if plan == "jump":                 # an unrelated range, a second target, then back
-            engine.bsgs_scan(start + 1000 * 2 * p.n, 2)
-            engine.bsgs_set_targets([oracle.pubkey(key + 5)])
-            engine.bsgs_scan(start, 2)
+        engine.kernel_time_reset()
+        one = engine.bsgs_scan(start, total)
+        one_call = (engine.bsgs_candidates() - c0, _walked(engine))
+        assert one == ([] if tgt == far else [(0, key)])
+        assert one_call[0] > 0 and one_call[1] == total * p.aux
+        for plan in ([1024] * 4, [512, 512, 1536, 1536], "jump"):
             engine.bsgs_set_targets([q])
             c0 = engine.bsgs_candidates()
-            plan = [3, 5]
-        engine.kernel_time_reset()
-        for nb in plan:
-            got += [(b, f) for f in engine.bsgs_scan(start + b * 2 * p.n, nb)]
-            b += nb
-        assert [f for _, f in got] == [(0, key)]
-        if plan == [2, 2, 2, 2]:           # the lanes were started once, then continued
-            from keyhunt_amd.engine import TIME_SETUP
-            assert engine.kernel_time(TIME_SETUP)[0] == 1
-        assert got[0][0] + plan[-1] == 8 and 6 >= got[0][0]
-        assert engine.bsgs_candidates() - c0 == one_call, plan
+            got, b = [], 0
+            if plan == "jump":                 # an unrelated range, a second target, then back
+                engine.bsgs_scan(start + 100000 * 2 * p.n, 64)
+                engine.bsgs_set_targets([oracle.pubkey(tgt + 5)])
+                engine.bsgs_scan(start, 64)
+                engine.bsgs_set_targets([q])
+                c0 = engine.bsgs_candidates()
+                plan = [1536, 2560]
+            engine.kernel_time_reset()
+            for nb in plan:
+                got += [(b, f) for f in engine.bsgs_scan(start + b * 2 * p.n, nb)]
+                b += nb
+            if tgt == key:
+                assert [f for _, f in got] == [(0, key)]
+                assert got[0][0] + plan[-1] == total
+            else:
+                assert got == []
+            if plan == [1024] * 4:             # the lanes were started once, then continued
+                assert engine.kernel_time(TIME_SETUP)[0] == 1
+            assert (engine.bsgs_candidates() - c0, _walked(engine)) == one_call, plan
