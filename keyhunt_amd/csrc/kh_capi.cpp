@@ -341,6 +341,7 @@ struct kh_ctx {
   uint32_t groups_per_launch = 0;
   uint32_t lanes_alloc = 0;
   int scratch_h = 0;  // inversion-pad entries per lane in d_scratch
+  uint32_t pad_skew = 0;  // lanes of gap after each pad row (KH_PAD_SKEW, read when the pad is allocated)
   // continuous BSGS lanes kept across kh_bsgs_scan calls: valid while the lane centres sit at the
   // first group of the call that would start at cont_next (same target, lanes and group size)
   bool cont_valid = false;
@@ -500,8 +501,15 @@ hipError_t dev_alloc(void **p, size_t bytes, int which) {
   return hipMalloc(p, bytes);
 }
 
+// KH_PAD_SKEW=<lanes>: a gap of that many lane entries after every pad row, so rows sit L + skew
+// entries apart instead of a power of two (A/B knob; 0 by default)
+static uint32_t env_pad_skew() {
+  const char *e = getenv("KH_PAD_SKEW");
+  return e ? (uint32_t)strtoul(e, nullptr, 0) : 0u;
+}
+
 int ensure_lanes(kh_ctx *c, uint32_t L, int H = KH_WALK_H) {
-  if (L <= c->lanes_alloc && H <= c->scratch_h) return KH_OK;
+  if (L <= c->lanes_alloc && H <= c->scratch_h && c->pad_skew == env_pad_skew()) return KH_OK;
   L = std::max(L, c->lanes_alloc);
   H = std::max(H, c->scratch_h);
   c->cont_valid = false;
@@ -513,10 +521,11 @@ int ensure_lanes(kh_ctx *c, uint32_t L, int H = KH_WALK_H) {
   c->d_scratch = nullptr;
   c->lanes_alloc = 0;
   c->scratch_h = 0;
+  c->pad_skew = env_pad_skew();
   HIPCHK(c, hipMalloc(&c->d_cx, (size_t)L * 32));
   HIPCHK(c, hipMalloc(&c->d_cy, (size_t)L * 32));
   HIPCHK(c, hipMalloc(&c->d_scalars, (size_t)L * 32));
-  HIPCHK(c, dev_alloc(reinterpret_cast<void **>(&c->d_scratch), (size_t)L * H * 32, 2));
+  HIPCHK(c, dev_alloc(reinterpret_cast<void **>(&c->d_scratch), ((size_t)L + c->pad_skew) * H * 32, 2));
   c->lanes_alloc = L;
   c->scratch_h = H;
   return KH_OK;
@@ -1096,6 +1105,7 @@ int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride_be[32], u
   A.cy = ctx->d_cy;
   A.scratch = ctx->d_scratch;
   A.L = jg.L;
+  A.pad_skew = ctx->pad_skew;
   A.lane_stride = jg.gpl * 2 * H;
   A.interleave = inter ? 1 : 0;
   A.n_points = n_points;
@@ -1403,6 +1413,7 @@ int build_walk(kh_ctx *ctx, int mode, uint8_t *bl1, const bloom_desc &bd1, uint6
   A.cy = ctx->d_cy;
   A.scratch = ctx->d_scratch;
   A.L = jg.L;
+  A.pad_skew = ctx->pad_skew;
   A.lane_stride = jg.gpl * 2 * H;
   A.n_points = count;
   A.bl1 = bl1;
@@ -2275,6 +2286,7 @@ static int bsgs_scan_one(kh_ctx *ctx, const u256 &st, const std::vector<u256> *l
       Aw.cy = ctx->d_cy;
       Aw.scratch = ctx->d_scratch;
       Aw.L = jg.L;
+      Aw.pad_skew = ctx->pad_skew;
       Aw.lane_stride = jg.gpl * 2 * H;
       Aw.interleave = cont ? 1 : 0;
       Aw.n_points = cont ? total_groups * 2 * H : rg * 2 * H;
@@ -2764,6 +2776,7 @@ int kh_walk_points(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride_be
   A.cy = ctx->d_cy;
   A.scratch = ctx->d_scratch;
   A.L = jg.L;
+  A.pad_skew = ctx->pad_skew;
   A.lane_stride = jg.gpl * 2 * H;
   A.n_points = n_points;
   A.dump_x = dx;

@@ -228,6 +228,8 @@ struct walk_args {
   uint32_t *dump_x, *dump_y;
   // k_walk_zinv: half of the --rmd-batch-size group (groups of 2 * zhalf slots)
   uint32_t zhalf;
+  // inversion pad: lanes of gap after each row (row stride L + pad_skew entries; KH_PAD_SKEW A/B knob)
+  uint32_t pad_skew;
 };
 
 struct setup_args {

@@ -569,6 +569,7 @@ __global__ void __launch_bounds__((walk_threads<MODE, H>()), (walk_blocks_per_cu
   };
   uint4 *__restrict__ scr = A.scratch;
   const size_t L = A.L;
+  const size_t LS = L + A.pad_skew;  // the pad's row stride in lane entries
   fe cx, cy;
   load_soa(cx, A.cx, A.L, g);
   load_soa(cy, A.cy, A.L, g);
@@ -583,12 +584,12 @@ __global__ void __launch_bounds__((walk_threads<MODE, H>()), (walk_blocks_per_cu
   // HBM traffic (outputs wrong)
   auto fold = [&](int m, int which) {
     const int r = SPARSE ? (m >> 1) : m;
-    return (size_t)((KH_TIMING_PAD_FOLD & which) ? (r & ((1 << KH_TIMING_PAD_ROWS_LOG2) - 1)) : r) * L + g;
+    return (size_t)((KH_TIMING_PAD_FOLD & which) ? (r & ((1 << KH_TIMING_PAD_ROWS_LOG2) - 1)) : r) * LS + g;
   };
   auto slot_w = [&](int m) { return fold(m, 1); };
   auto slot = [&](int m) { return fold(m, 2); };
 #else
-  auto slot = [&](int m) { return (size_t)(SPARSE ? (m >> 1) : m) * L + g; };
+  auto slot = [&](int m) { return (size_t)(SPARSE ? (m >> 1) : m) * LS + g; };
   auto slot_w = slot;
 #endif
   // Deferred-probe walks (one 16-B split-block load per point, issued a step ahead): the BSGS giant

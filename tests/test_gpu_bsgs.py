@@ -537,7 +537,7 @@ def test_bsgs_lanes_continue_across_calls(engine, oracle):
     total = 4096
     start = 0x1234567890000
     key = start + 4000 * 2 * p.n + 777     # in the last call of every plan
-    far = start - 5555 * 2 * p.n
+    far = start + 1000000 * 2 * p.n   # past every base these calls walk
     for tgt in (far, key):
         q = oracle.pubkey(tgt)
         engine.bsgs_set_targets([q])
