@@ -583,11 +583,11 @@ def bsgs_leg(D: Dist, W: Walks, args, clock):
         walked += per
         assert not any(found)  # puzzle 125's (130's) key lies far from the start of the range
 
-    # warm-up steps large enough for the engine's lane-count calibration (a context's first call of
-    # >= 2^23 walk groups times 2^21 against 2^20 lanes, DESIGN.md §2 "Placement"), so it happens here
-    # and not in the timed region
+    # warm-up steps large enough for the engine's placement calibration (a context's first call of
+    # >= 2^23 walk groups times two inversion-pad placements against each other in four parts, DESIGN.md
+    # §2 "Placement"), so it happens here and not in the timed region; 2^24 groups: parts of 2^34 points
     gpb = max(1, info.cycles * 1024 // 4096)
-    Bw = max(B0, -(-(4 << 21) // gpb) * S) if args.warmup else B0
+    Bw = max(B0, -(-(8 << 21) // gpb) * S) if args.warmup else B0
     last = 0.0
     for s in range(args.warmup):
         t = time.perf_counter()
@@ -627,8 +627,8 @@ def bsgs_leg(D: Dist, W: Walks, args, clock):
         "ms_per_step": T / args.steps * 1e3,
         "seconds_timed": T,
         "bases_per_step": B,
-        "lanes_calibration": {"lanes": lanes_pick, "giant_points_per_s_at_2^21": rate_hi,
-                              "giant_points_per_s_at_2^20": rate_lo},
+        "placement_calibration": {"lanes": lanes_pick, "giant_points_per_s_kept": rate_hi,
+                                  "giant_points_per_s_other": rate_lo},
         "giant_points_per_s": D.world * args.steps * B * info.cycles * 1024 / T,
         "rank_giant_points_per_s": my_pts_s,
         "build_seconds": build_s,
@@ -1074,7 +1074,7 @@ def main():
                        "bases_per_step": prim["bases_per_step"],
                        "giant_points_per_step": prim["bases_per_step"] * info.cycles * 1024,
                        "walks_in_flight_per_gpu": args.walks,
-                       "lanes_calibration": prim["lanes_calibration"],
+                       "placement_calibration": prim["placement_calibration"],
                        "parallelism": f"keyspace split x{D.world} (no collective)"},
             "devices_used": len(devices),
             "rehearsal": len(devices) < D.world,

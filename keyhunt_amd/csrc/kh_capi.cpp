@@ -337,7 +337,8 @@ struct kh_ctx {
   uint32_t lanes_pick = 0, lanes_force = 0;
   uint32_t lanes_used = 0;  // lanes the last large-group BSGS call walked (the calibration checks it)
   bool bsgs_calibrated = false;
-  double cal_rate[2] = {0, 0};  // giant points/s of the calibration's halves (2^21, 2^20 lanes)
+  // giant points/s of the calibration's candidates: [0] the placement kept, [1] the best other one
+  double cal_rate[2] = {0, 0};
   uint32_t groups_per_launch = 0;
   uint32_t lanes_alloc = 0;
   int scratch_h = 0;  // inversion-pad entries per lane in d_scratch
@@ -353,6 +354,8 @@ struct kh_ctx {
   uint32_t *d_q = nullptr;  // the current BSGS target {x[8], y[8]}
   uint32_t *d_cx = nullptr, *d_cy = nullptr, *d_scalars = nullptr;
   uint4 *d_scratch = nullptr;
+  void *d_scratch_base = nullptr;  // the pad's allocation (d_scratch sits KH_PAD_OFFSET bytes into it)
+  uint64_t pad_offset = 0;
   std::vector<uint32_t> h_scalars;
 
   // walk delta tables: key -> device table ((H+1) x 16 words)
@@ -443,7 +446,7 @@ kh_ctx::~kh_ctx() {
   (void)hipFree(d_cx);
   (void)hipFree(d_cy);
   (void)hipFree(d_scalars);
-  (void)hipFree(d_scratch);
+  (void)hipFree(d_scratch_base);
   (void)hipFree(d_q);
   for (auto &t : tables) (void)hipFree(t.second);
   (void)hipFree(d_hit_count);
@@ -508,24 +511,34 @@ static uint32_t env_pad_skew() {
   return e ? (uint32_t)strtoul(e, nullptr, 0) : 0u;
 }
 
+// KH_PAD_OFFSET=<bytes>: the pad starts that far (rounded down to 256 B) into its allocation (A/B knob)
+static uint64_t env_pad_offset() {
+  const char *e = getenv("KH_PAD_OFFSET");
+  return e ? strtoull(e, nullptr, 0) & ~255ull : 0ull;
+}
+
 int ensure_lanes(kh_ctx *c, uint32_t L, int H = KH_WALK_H) {
-  if (L <= c->lanes_alloc && H <= c->scratch_h && c->pad_skew == env_pad_skew()) return KH_OK;
+  if (L <= c->lanes_alloc && H <= c->scratch_h && c->pad_skew == env_pad_skew() && c->pad_offset == env_pad_offset())
+    return KH_OK;
   L = std::max(L, c->lanes_alloc);
   H = std::max(H, c->scratch_h);
   c->cont_valid = false;
   (void)hipFree(c->d_cx);
   (void)hipFree(c->d_cy);
   (void)hipFree(c->d_scalars);
-  (void)hipFree(c->d_scratch);
+  (void)hipFree(c->d_scratch_base);
   c->d_cx = c->d_cy = c->d_scalars = nullptr;
   c->d_scratch = nullptr;
+  c->d_scratch_base = nullptr;
   c->lanes_alloc = 0;
   c->scratch_h = 0;
   c->pad_skew = env_pad_skew();
   HIPCHK(c, hipMalloc(&c->d_cx, (size_t)L * 32));
   HIPCHK(c, hipMalloc(&c->d_cy, (size_t)L * 32));
   HIPCHK(c, hipMalloc(&c->d_scalars, (size_t)L * 32));
-  HIPCHK(c, dev_alloc(reinterpret_cast<void **>(&c->d_scratch), ((size_t)L + c->pad_skew) * H * 32, 2));
+  c->pad_offset = env_pad_offset();
+  HIPCHK(c, dev_alloc(&c->d_scratch_base, ((size_t)L + c->pad_skew) * H * 32 + c->pad_offset, 2));
+  c->d_scratch = reinterpret_cast<uint4 *>(static_cast<uint8_t *>(c->d_scratch_base) + c->pad_offset);
   c->lanes_alloc = L;
   c->scratch_h = H;
   return KH_OK;
@@ -825,9 +838,10 @@ int kh_release_walk(kh_ctx *ctx) {
   (void)hipFree(ctx->d_cx);
   (void)hipFree(ctx->d_cy);
   (void)hipFree(ctx->d_scalars);
-  (void)hipFree(ctx->d_scratch);
+  (void)hipFree(ctx->d_scratch_base);
   ctx->d_cx = ctx->d_cy = ctx->d_scalars = nullptr;
   ctx->d_scratch = nullptr;
+  ctx->d_scratch_base = nullptr;
   ctx->lanes_alloc = 0;
   ctx->scratch_h = 0;
   ctx->cont_valid = false;
@@ -841,6 +855,19 @@ int kh_bsgs_geometry(kh_ctx *ctx, uint32_t *lanes, double rates[2]) {
     rates[0] = ctx->cal_rate[0];
     rates[1] = ctx->cal_rate[1];
   }
+  return KH_OK;
+}
+
+int kh_debug_replace_layer1(kh_ctx *ctx) {
+  if (!ctx || !ctx->d_bl[0]) return KH_E_STATE;
+  (void)hipSetDevice(ctx->device);
+  HIPCHK(ctx, hipDeviceSynchronize());
+  const size_t bytes = 256 * ctx->bd[0].stride + 4;
+  uint8_t *nb = nullptr;
+  HIPCHK(ctx, dev_alloc(reinterpret_cast<void **>(&nb), bytes, 1));
+  HIPCHK(ctx, hipMemcpy(nb, ctx->d_bl[0], bytes, hipMemcpyDeviceToDevice));
+  (void)hipFree(ctx->d_bl[0]);
+  ctx->d_bl[0] = nb;
   return KH_OK;
 }
 
@@ -2478,14 +2505,27 @@ static int bsgs_scan_one(kh_ctx *ctx, const u256 &st, const std::vector<u256> *l
   return nf > cap ? KH_E_OVERFLOW : KH_OK;
 }
 
-// The giant walk's rate at 2^21 and at 2^20 lanes differs by up to ~9 % either way from one process
-// (and box) to the next, the state holding for the process (DESIGN.md §2 "Placement").  A context's
-// first continuous call of at least 2^23 walk groups therefore walks its quarters at 2^21, 2^20, 2^20
-// and 2^21 lanes (ABBA, so a linear drift of clock or power between the quarters cancels), times each
-// on the walk's events, and keeps the faster count for its later large calls (KH_BSGS_CALIBRATE=0,
-// KH_BSGS_LANES or kh_set_geometry's lanes switch this off).  A quarter that could not take its count
-// (device memory) leaves the context uncalibrated.  Every base is walked once either way, so keys and
-// candidates are those of an uncalibrated call.
+// The giant walk's rate depends on where its 64-GB inversion pad lands in physical memory: the same
+// process walks ~2.5-5 % faster on one allocation than on another, with identical instruction and
+// request counts; the slow placement shows only longer L2 request latencies in cycles at a higher
+// clock (DESIGN.md §2 "Placement", profiles/r06f_state_counters.json).  Re-allocating alternates between
+// placements (r06e_pad_alloc_sweep.json), so a context's first continuous call of at least 2^23 walk
+// groups times candidate placements against each other: the primary pad and KH_PAD_CANDIDATES - 1
+// (default 1) more pads of the same size, allocated while the primary is held (when the device keeps
+// 32 GB free besides), all at 2^21 lanes.  The call is cut into parts walked on the candidates in the
+// order A B B A (A B C C B A ...), so a linear drift of clock or power cancels; each part is timed on the
+// walk's events, the fastest pad becomes the context's pad and the others are freed.  With no room for a
+// second pad the candidates are 2^21 lanes and 2^20 lanes, which walk the first half of the same pad.
+// KH_BSGS_CALIBRATE=0, KH_BSGS_LANES or kh_set_geometry's lanes switch the calibration off.  Every base
+// is walked once either way, so keys and candidates are those of an uncalibrated call.
+struct pad_slot {
+  void *base;
+  uint4 *ptr;
+};
+static void swap_pad(kh_ctx *ctx, pad_slot &p) {
+  std::swap(ctx->d_scratch_base, p.base);
+  std::swap(ctx->d_scratch, p.ptr);
+}
 static int bsgs_scan_impl(kh_ctx *ctx, const u256 &st, const std::vector<u256> *list, uint64_t n_bases,
                           kh_bsgs_found *found, uint32_t cap, uint32_t *n_found) {
   if (!ctx->bsgs_built) return KH_E_STATE;
@@ -2494,45 +2534,105 @@ static int bsgs_scan_impl(kh_ctx *ctx, const u256 &st, const std::vector<u256> *
   const uint64_t gpb = A_pts / (2 * KH_WALK_HB);
   const uint32_t hi = ctx->lanes_bsgs, lo = ctx->lanes_bsgs / 2;
   const char *cal = getenv("KH_BSGS_CALIBRATE");
+  const char *ncand = getenv("KH_PAD_CANDIDATES");
+  // candidates: KH_PAD_CANDIDATES (default 2), as many as the call has pairs of 2^21-group tiles for
+  const uint64_t tiles = n_bases * gpb / std::max<uint32_t>(1, hi);
+  const int want = (int)std::max<uint64_t>(1, std::min<uint64_t>(std::min(4, ncand ? atoi(ncand) : 2), tiles / 2));
   const bool calibrate = !ctx->bsgs_calibrated && !list && A_pts == I.aux && A_pts % (2 * KH_WALK_HB) == 0 &&
                          hi == KH_BSGS_LANES && lo > ctx->lanes_max && !(cal && atoi(cal) == 0) &&
                          !getenv("KH_BSGS_LANES") && !getenv("KH_BSGS_NARROW") && !getenv("KH_NO_BIG_GROUPS") &&
-                         n_bases * gpb >= 4ull * hi && ctx->targets.size() == 1;
+                         tiles >= 4 && ctx->targets.size() == 1 && !ctx->found[0];
   if (!calibrate) return bsgs_scan_one(ctx, st, list, n_bases, found, cap, n_found);
-  // quarters in whole tiles of the wider count, so each tiles exactly; the last takes the rest
+  // the primary pad at 2^21 lanes (bsgs_scan_one would take it too), then the extra candidates
+  struct cand {
+    int pad;
+    uint32_t lanes;
+    double ms, pts;
+  };
+  std::vector<cand> cands;
+  std::vector<pad_slot> pads(1, pad_slot{nullptr, nullptr});  // pads[0]: the primary (lives in ctx)
+  {
+    size_t fr = 0, tot = 0;
+    const uint64_t pad_bytes = ((uint64_t)hi + ctx->pad_skew) * walk_pad_rows(KM_BSGSB, false, KH_WALK_HB) * 32 +
+                               env_pad_offset();
+    const uint64_t lane_bytes = (uint64_t)hi * (walk_pad_rows(KM_BSGSB, false, KH_WALK_HB) * 32 + 96);
+    const bool known = hipMemGetInfo(&fr, &tot) == hipSuccess;
+    const uint64_t have = ctx->lanes_alloc >= hi ? lane_bytes : 0;
+    if (!known || fr + have < lane_bytes + (32ull << 30) || ensure_pipeline(ctx, hi, KH_WALK_HB) != KH_OK) {
+      (void)hipGetLastError();
+      ctx->err.clear();
+      return bsgs_scan_one(ctx, st, list, n_bases, found, cap, n_found);  // no room: its own fallback
+    }
+    cands.push_back({0, hi, 0, 0});
+    for (int k = 1; k < want; k++) {
+      if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr < pad_bytes + (32ull << 30)) break;
+      void *b = nullptr;
+      if (dev_alloc(&b, pad_bytes, 2) != hipSuccess) {
+        (void)hipGetLastError();
+        break;
+      }
+      pads.push_back({b, reinterpret_cast<uint4 *>(static_cast<uint8_t *>(b) + ctx->pad_offset)});
+      cands.push_back({(int)pads.size() - 1, hi, 0, 0});
+    }
+    if (cands.size() == 1) cands.push_back({0, lo, 0, 0});  // one pad: 2^20 lanes walk its first half
+  }
+  const int nc = (int)cands.size();
+  std::vector<int> order;
+  for (int k = 0; k < nc; k++) order.push_back(k);
+  for (int k = nc - 1; k >= 0; k--) order.push_back(k);
+  // parts in whole tiles of the wider count, so each tiles exactly; the last takes the rest
   const uint64_t tile = std::max<uint64_t>(1, hi / std::max<uint64_t>(1, gpb));
-  const uint64_t nbq = std::max<uint64_t>(tile, (n_bases / 4) / tile * tile);
-  static const int side[4] = {0, 1, 1, 0};  // 0: hi lanes, 1: lo lanes
+  const uint64_t nbq = std::max<uint64_t>(tile, (n_bases / order.size()) / tile * tile);
   uint32_t nf_all = 0;
-  double ms[2] = {0, 0}, pts[2] = {0, 0};
   bool exact = true;
-  int r = KH_OK;
+  int r = KH_OK, cur = 0;  // cur: the pads[] entry now in ctx
   uint64_t done_b = 0;
-  for (int q = 0; q < 4 && done_b < n_bases; q++) {
-    const uint64_t nb = q == 3 ? n_bases - done_b : std::min(nbq, n_bases - done_b);
+  for (size_t q = 0; q < order.size() && done_b < n_bases; q++) {
+    cand &c = cands[order[q]];
+    const uint64_t nb = q + 1 == order.size() ? n_bases - done_b : std::min(nbq, n_bases - done_b);
     const u256 s = sc_add(st, sc_reduce(u256_from_u128((u128)done_b * 2 * I.n)));
-    const uint32_t want = side[q] ? lo : hi;
-    ctx->lanes_force = want;
+    if (c.pad != cur) {  // the pad holds no state across launches: swap it under the running lanes
+      (void)hipStreamSynchronize(ctx->stream);
+      (void)hipStreamSynchronize(ctx->side);
+      if (cur) swap_pad(ctx, pads[cur]);    // the primary back into ctx
+      if (c.pad) swap_pad(ctx, pads[c.pad]);
+      cur = c.pad;
+    }
+    ctx->lanes_force = c.lanes;
     const timing t0 = ctx->tm[2];
     uint32_t nf = 0;
     const uint32_t off = std::min(nf_all, cap);
     r = bsgs_scan_one(ctx, s, nullptr, nb, found ? found + off : nullptr, cap - off, &nf);
     ctx->lanes_force = 0;
-    if (ctx->lanes_used != want) exact = false;
-    ms[side[q]] += ctx->tm[2].ms - t0.ms;
-    pts[side[q]] += (double)(ctx->tm[2].points - t0.points);
+    if (ctx->lanes_used != c.lanes) exact = false;
+    c.ms += ctx->tm[2].ms - t0.ms;
+    c.pts += (double)(ctx->tm[2].points - t0.points);
     nf_all += nf;
     done_b += nb;
-    if (r && r != KH_E_OVERFLOW) return r;
-    if (ctx->found[0]) break;  // the key ended the call
+    if ((r && r != KH_E_OVERFLOW) || ctx->found[0]) break;  // an error, or the key ended the call
   }
-  // the rest of the call, when the key ended it early, is not walked (as in an uncalibrated call)
+  // keep the fastest timed candidate's pad (and lane count); free the other pads
+  (void)hipStreamSynchronize(ctx->stream);
+  (void)hipStreamSynchronize(ctx->side);
+  int best = -1;
+  for (int k = 0; k < nc; k++)
+    if (cands[k].ms > 0 && cands[k].pts > 0 &&
+        (best < 0 || cands[k].pts / cands[k].ms > cands[best].pts / cands[best].ms))
+      best = k;
+  int timed = 0;
+  for (int k = 0; k < nc; k++) timed += cands[k].ms > 0 && cands[k].pts > 0;
+  const int keep_pad = best >= 0 && timed == nc && exact && r == KH_OK ? cands[best].pad : cur;
+  if (cur) swap_pad(ctx, pads[cur]);          // primary back in ctx
+  if (keep_pad) swap_pad(ctx, pads[keep_pad]);  // the kept pad into ctx, the primary into its slot
+  for (size_t k = 1; k < pads.size(); k++) (void)hipFree(pads[k].base);
   *n_found = nf_all;
-  if (exact && ms[0] > 0 && ms[1] > 0 && pts[0] > 0 && pts[1] > 0) {
-    ctx->lanes_pick = pts[0] / ms[0] >= pts[1] / ms[1] ? hi : lo;
+  if (best >= 0 && timed == nc && exact) {
+    ctx->lanes_pick = cands[best].lanes;
     ctx->bsgs_calibrated = true;
-    ctx->cal_rate[0] = pts[0] / ms[0] * 1e3;
-    ctx->cal_rate[1] = pts[1] / ms[1] * 1e3;
+    ctx->cal_rate[0] = cands[best].pts / cands[best].ms * 1e3;
+    ctx->cal_rate[1] = 0;
+    for (int k = 0; k < nc; k++)
+      if (k != best) ctx->cal_rate[1] = std::max(ctx->cal_rate[1], cands[k].pts / cands[k].ms * 1e3);
   }
   return *n_found > cap ? KH_E_OVERFLOW : r;
 }

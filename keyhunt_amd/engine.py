@@ -79,6 +79,7 @@ def lib() -> ctypes.CDLL:
     L.kh_set_geometry.argtypes = [P, ctypes.c_uint32, ctypes.c_uint32]
     L.kh_release_walk.argtypes = [P]
     L.kh_debug_layout.argtypes = [P, ctypes.POINTER(ctypes.c_uint64 * 8)]
+    L.kh_debug_replace_layer1.argtypes = [P]
     L.kh_bsgs_geometry.argtypes = [P, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_double * 2)]
     L.kh_synchronize.argtypes = [P]
     L.kh_scan_memory.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64)]
@@ -176,7 +177,8 @@ class Engine:
         self._chk(lib().kh_set_geometry(self._ctx, lanes, groups_per_launch), "kh_set_geometry")
 
     def bsgs_geometry(self) -> tuple[int, float, float]:
-        """(lanes kept for large BSGS calls or 0, giant points/s at 2^21 lanes, at 2^20 lanes)."""
+        """(lanes kept for large BSGS calls or 0, giant points/s of the pad placement kept, of the best
+        other candidate) -- the context's placement calibration (kh_bsgs_geometry)."""
         lanes, rates = ctypes.c_uint32(), (ctypes.c_double * 2)()
         self._chk(lib().kh_bsgs_geometry(self._ctx, ctypes.byref(lanes), ctypes.byref(rates)), "kh_bsgs_geometry")
         return lanes.value, rates[0], rates[1]
@@ -187,6 +189,10 @@ class Engine:
         self._chk(lib().kh_debug_layout(self._ctx, ctypes.byref(o)), "kh_debug_layout")
         return {"layer1": [hex(o[0]), o[1]], "pad": [hex(o[2]), o[3]], "layer2": [hex(o[4]), o[5]],
                 "lanes": o[6], "pad_rows": o[7]}
+
+    def debug_replace_layer1(self) -> None:
+        """Move the BSGS layer-1 filter to a fresh allocation (kh_debug_replace_layer1; diagnostics)."""
+        self._chk(lib().kh_debug_replace_layer1(self._ctx), "kh_debug_replace_layer1")
 
     def release_walk(self) -> None:
         """Free the walks' lane arrays and inversion pad (kh_release_walk)."""

@@ -461,16 +461,19 @@ def test_calls_with_ragged_lane_tiles(oracle, lanes, calls):
     assert res[1][0] == res[3][0] == [(0, key)]
 
 
-def test_lane_calibration_same_results(oracle, monkeypatch):
-    """A context's first call of >= 2^23 walk groups walks its quarters at 2^21, 2^20, 2^20 and 2^21
-    lanes and keeps the faster count: the same first-level candidates and walked points as an
-    uncalibrated call (KH_BSGS_CALIBRATE=0), the key found in any quarter, and kh_bsgs_geometry reports
-    both counts' rates."""
+@pytest.mark.parametrize("cands", [2, 3])
+def test_placement_calibration_same_results(oracle, monkeypatch, cands):
+    """A context's first call of >= 2^23 walk groups walks its parts on candidate pad placements (the
+    primary pad and KH_PAD_CANDIDATES - 1 more, in the order A B B A / A B C C B A, or 2^21 and 2^20 lanes
+    on one pad when the device has no room) and keeps the fastest: the same first-level candidates and
+    walked points as an uncalibrated call (KH_BSGS_CALIBRATE=0), the key found in any part, and
+    kh_bsgs_geometry reports the kept and the best other candidate's rates."""
     import keyhunt_amd as K
     p = oracle.bsgs_params(N36, K16)
-    nb = 1 << 21                           # 4 groups per base: 2^23 groups
+    nb = 3 << 20                           # 4 groups per base: 6 x 2^21 groups (six parts for 3 pads)
     start = 0x3C3C3C3C3C000000
     far = start - 777 * 2 * p.n
+    monkeypatch.setenv("KH_PAD_CANDIDATES", str(cands))
     res = []
     for calibrate in (True, False):
         if calibrate:
@@ -486,11 +489,11 @@ def test_lane_calibration_same_results(oracle, monkeypatch):
             res.append((e.bsgs_candidates() - c0, _walked(e), e.bsgs_geometry()))
     assert res[0][0] == res[1][0] and res[0][0] > 1000
     assert res[0][1] == res[1][1] == nb * p.aux
-    lanes, r_hi, r_lo = res[0][2]
-    assert lanes in (1 << 21, 1 << 20) and r_hi > 0 and r_lo > 0
+    lanes, r_kept, r_other = res[0][2]
+    assert lanes in (1 << 21, 1 << 20) and r_kept >= r_other > 0
     assert res[1][2] == (0, 0.0, 0.0)
     monkeypatch.delenv("KH_BSGS_CALIBRATE", raising=False)
-    for where in (3, nb // 2 - 7, nb - 5):  # the key in the first, the second / third, the last quarter
+    for where in (3, nb // 2 - 7, nb - 5):  # the key in the first, a middle and the last part
         key = start + where * 2 * p.n + 999
         with K.Engine(0) as e:
             e.bsgs_setup(N36, K16, layer1=K.KH_LAYER1_BLOCKED)
@@ -570,3 +573,33 @@ def test_bsgs_lanes_continue_across_calls(engine, oracle):
             if plan == [1024] * 4:             # the lanes were started once, then continued
                 assert engine.kernel_time(TIME_SETUP)[0] == 1
             assert (engine.bsgs_candidates() - c0, _walked(engine)) == one_call, plan
+
+
+def test_pad_skew_and_offset_same_results(oracle, monkeypatch):
+    """The pad layout knobs (KH_PAD_SKEW: a gap of lanes after every pad row; KH_PAD_OFFSET: the pad's
+    start inside its allocation) move only where the inversion pad sits: the same first-level candidates,
+    walked points and key as the default layout, for the BSGS walk and an xpoint chunk."""
+    import keyhunt_amd as K
+    p = oracle.bsgs_params(N36, K16)
+    start = 0x7777777700000
+    key = start + 3000 * 2 * p.n + 31
+    xkeys = [(1 << 61) + 12345 + 99991 * j for j in range(5)]
+    xrows = [oracle.pubkey(k)[0].to_bytes(32, "big")[:20] for k in xkeys]
+    res = []
+    for skew, off in ((None, None), ("37", "4096"), ("3000", "65792")):
+        for var, val in (("KH_PAD_SKEW", skew), ("KH_PAD_OFFSET", off)):
+            if val is None:
+                monkeypatch.delenv(var, raising=False)
+            else:
+                monkeypatch.setenv(var, val)
+        with K.Engine(0) as e:
+            e.bsgs_setup(N36, K16, layer1=K.KH_LAYER1_BLOCKED)
+            e.bsgs_build()
+            e.bsgs_set_targets([oracle.pubkey(key)])
+            got = e.bsgs_scan(start, 4096)
+            walked = _walked(e)
+            e.set_targets(xrows)
+            xs = sorted(h.key for h in e.scan(1 << 61, 1 << 24, mode=K.KH_MODE_XPOINT, search=0))
+            res.append((got, e.bsgs_candidates(), walked, xs))
+    assert res[0][0] == [(0, key)] and res[0][1] > 0 and res[0][3] == sorted(xkeys)
+    assert res[1] == res[0] and res[2] == res[0]

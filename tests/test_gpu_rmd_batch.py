@@ -155,6 +155,42 @@ def test_engine_rmd_batch_near_the_order_without_a_zero_centre(engine, oracle):
     assert sorted((h.key, h.compressed, h.kind) for h in got) == sorted(ref)
 
 
+def test_engine_rmd_batch_chunk_over_the_order_equals_oracle(engine, oracle):
+    """The whole 4-group chunk from n - 1000: group 1 holds the key 0 mod n at a
+    non-centre slot, whose zero difference would collapse a full batch inversion -- with G < 1024 every
+    inverse of the reference's IntGroup is 0 anyway (oracle walk_group_n), so that group's points follow
+    the same s = 0 formulas.  Targets are planted on both sides of groups 0 and 1 (and their centres);
+    the engine's hits over the whole chunk, keys past the order included, equal the oracle's.  The
+    oracle is pinned by the reference CLI away from the order; for keys past it (which the reference
+    keeps unreduced) parity with the reference itself is unpinned: no reference fixture crosses the order
+    with --rmd-batch-size."""
+    G, half = 512, 256
+    start = ORDER_N - 1000
+    rng = random.Random(79)
+    pts = []
+    for off in (0, 100, 255, 256, 257, 500, 511, 512, 600, 767, 768, 769, 900, 999):
+        g, t = divmod(off, G)
+        c = start + g * G + half
+        if t == half:
+            pts.append(oracle.pubkey(c))
+            continue
+        cx, _ = oracle.pubkey(c)
+        i = t - half - 1 if t > half else half - t - 1
+        tx, ty = oracle.pubkey(i + 1)
+        pts.append(((-(cx + tx)) % P, (P - ty) % P if t > half else ty))
+    rows = _point_rows(oracle, pts, rng)
+    engine.set_targets(rows)
+    engine.set_rmd_batch(G)
+    try:
+        r, got = engine.scan_status(start, 4 * G, mode=0, search=2)
+    finally:
+        engine.set_rmd_batch(1024)
+    assert r == 0
+    ref = oracle.scan_chunk(0, 2, start, 4 * G, rows, group=G)
+    assert len(ref) >= 8
+    assert sorted((h.key, h.compressed, h.kind) for h in got) == sorted(ref)
+
+
 def test_engine_rmd_batch_wrapping_stride(engine, oracle):
     """-I strides that wrap the order many times per chunk (every such chunk was
     refused).  Centres are real points: a centre planted as a target is found with its key

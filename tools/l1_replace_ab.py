@@ -1,0 +1,72 @@
+"""Which buffer's placement sets the BSGS walk's state?  One process on the bench geometry (n = 2^44,
+k = 128, 2^21 lanes, no calibration): --l1 times, move layer 1 to a fresh allocation
+(kh_debug_replace_layer1) and time --calls calls of --bases bases; then --pad times, re-allocate the
+pad instead (kh_release_walk) and time the same.  Prints one JSON object with every step's rate and
+the board's clock and power.
+
+usage: python tools/l1_replace_ab.py [--l1 6] [--pad 4] [--calls 1] [--bases 4194304]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+os.environ.setdefault("KH_BSGS_CALIBRATE", "0")
+os.environ.setdefault("KH_BSGS_LANES", str(1 << 21))
+import bench  # noqa: E402
+import keyhunt_amd as K  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--l1", type=int, default=6)
+    ap.add_argument("--pad", type=int, default=4)
+    ap.add_argument("--calls", type=int, default=1)
+    ap.add_argument("--bases", type=int, default=1 << 22)
+    a = ap.parse_args()
+    board = bench.BoardSampler(bench.pci_bus_id(0)).start()
+    e = K.Engine(0)
+    info = e.bsgs_setup(1 << 44, 128)
+    e.bsgs_build()
+    e.bsgs_set_targets([bench.decompress(bench.PUZZLE125)])
+    two_n = 2 * info.n
+    pts_call = a.bases * info.cycles * 1024
+    origin, done = 1 << 124, 0
+    rows = []
+
+    def timed(what, k):
+        nonlocal done
+        assert not e.bsgs_scan(origin + done * a.bases * two_n, a.bases)  # warm (after a re-allocation)
+        done += 1
+        e.synchronize()
+        b0 = board.snapshot()
+        t0 = time.perf_counter()
+        for _ in range(a.calls):
+            assert not e.bsgs_scan(origin + done * a.bases * two_n, a.bases)
+            done += 1
+        e.synchronize()
+        t1 = time.perf_counter()
+        bw = board.between(b0, board.snapshot()) or {}
+        r = {"moved": what, "step": k, "giant_points_per_s": a.calls * pts_call / (t1 - t0),
+             "mhz": bw.get("board_gfxclk_mhz"), "w": bw.get("socket_power_w"), "layout": e.debug_layout()}
+        rows.append(r)
+        print(json.dumps({"moved": what, "k": k, "G": round(r["giant_points_per_s"] / 1e9, 3),
+                          "mhz": round(r["mhz"] or 0), "w": round(r["w"] or 0)}), file=sys.stderr, flush=True)
+
+    timed("none", 0)
+    for k in range(a.l1):
+        e.debug_replace_layer1()
+        timed("layer1", k)
+    for k in range(a.pad):
+        e.release_walk()
+        timed("pad", k)
+    board.stop()
+    e.close()
+    print(json.dumps({"bases_per_call": a.bases, "calls": a.calls, "rows": rows}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
