@@ -604,6 +604,7 @@ def bsgs_leg(D: Dist, W: Walks, args, clock):
     T, t0, t1, recs, board = timed(D, W, args.steps, lambda s: run(B), B, K.engine.TIME_BSGS, clock)
     progress(f"BSGS timed region {T:.1f} s; known-answer window next")
     lanes_pick, rate_hi, rate_lo = W.engs[0].bsgs_geometry()
+    cal_done, cal_rates = W.engs[0].bsgs_placement()
     la, ms, pts = W.kernel_time(K.engine.TIME_BSGS)
     my_pts_s = args.steps * B * info.cycles * 1024 / (recs[-1][0] - t0)
     # known answer (outside the timed region, same engine and tables): SURVEY.md 8c
@@ -627,8 +628,9 @@ def bsgs_leg(D: Dist, W: Walks, args, clock):
         "ms_per_step": T / args.steps * 1e3,
         "seconds_timed": T,
         "bases_per_step": B,
-        "placement_calibration": {"lanes": lanes_pick, "giant_points_per_s_kept": rate_hi,
-                                  "giant_points_per_s_other": rate_lo},
+        "placement_calibration": {"complete": cal_done, "lanes": lanes_pick,
+                                  "pad_giant_points_per_s_kept": cal_rates[0], "pad_other": cal_rates[1],
+                                  "layer1_giant_points_per_s_kept": cal_rates[2], "layer1_other": cal_rates[3]},
         "giant_points_per_s": D.world * args.steps * B * info.cycles * 1024 / T,
         "rank_giant_points_per_s": my_pts_s,
         "build_seconds": build_s,

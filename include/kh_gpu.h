@@ -119,19 +119,25 @@ int kh_set_geometry(kh_ctx *ctx, uint32_t lanes, uint32_t groups_per_launch);
 /* free the walks' device buffers (lane centres, scalars, inversion pad: up to 64 GB) between jobs;
  * the next scan allocates them again and starts its lanes afresh.  Tables and targets stay. */
 int kh_release_walk(kh_ctx *ctx);
-/* the BSGS walk's placement calibration (DESIGN.md §2 "Placement"): a context's first large call walks
- * its parts on candidate inversion-pad placements (a second pad of the same size, or 2^20 lanes when
- * the device has no room for one) and keeps the fastest.  *lanes = the lane count kept (0 = not yet
- * calibrated), rates[0] = giant points/s of the placement kept, rates[1] = of the best other one */
+/* the BSGS walk's placement calibration (DESIGN.md §2 "Placement"): a context's first large calls walk
+ * their parts on candidate placements of the inversion pad (a second pad of the same size, or 2^20
+ * lanes when the device has no room for one), then of layer 1 (a copy), keeping the fastest of each.
+ * *lanes = the lane count kept (0 = the pad stage not yet run), rates[0] = giant points/s of the pad
+ * placement kept, rates[1] = of the best other one */
 int kh_bsgs_geometry(kh_ctx *ctx, uint32_t *lanes, double rates[2]);
+/* both stages of the placement calibration: rates[0..1] = the pad placement kept / the best other one,
+ * rates[2..3] = the layer-1 placement kept / the other one (0 = stage not run).  Returns 1 when the
+ * calibration is complete, 0 while stages remain. */
+int kh_bsgs_placement(kh_ctx *ctx, double rates[4]);
 /* diagnostics (DESIGN.md §2 "Placement"): where the BSGS walk's buffers sit in the device's virtual
  * address space.  out[0..1] = layer-1 address and bytes, out[2..3] = the inversion pad's, out[4..5] =
  * layer 2's, out[6] = lanes allocated, out[7] = pad rows per lane.  Engine-only: the reference has no
  * counterpart. */
 int kh_debug_layout(kh_ctx *ctx, uint64_t out[8]);
-/* diagnostics: move the BSGS layer-1 filter to a new allocation (copy, then free the old one); the
- * tables' contents are unchanged */
-int kh_debug_replace_layer1(kh_ctx *ctx);
+/* diagnostics (DESIGN.md §2 "Placement"): give device buffers fresh allocations, taken while the old
+ * ones are held, contents copied: which = 1 layer 1, 2 the inversion pad, 4 the lane centres and scalars,
+ * 8 the walks' delta tables, 16 layers 2 and 3 (bits may be combined).  Results are unchanged. */
+int kh_debug_replace(kh_ctx *ctx, uint32_t which);
 int kh_synchronize(kh_ctx *ctx);
 
 /* ---- address / rmd160 / xpoint ------------------------------------------------------------ */

@@ -337,8 +337,10 @@ struct kh_ctx {
   uint32_t lanes_pick = 0, lanes_force = 0;
   uint32_t lanes_used = 0;  // lanes the last large-group BSGS call walked (the calibration checks it)
   bool bsgs_calibrated = false;
-  // giant points/s of the calibration's candidates: [0] the placement kept, [1] the best other one
-  double cal_rate[2] = {0, 0};
+  // giant points/s of the placement calibration's candidates (stage 0: the pad, 1: layer 1):
+  // [2s] the one kept, [2s + 1] the best other one; cal_stage: stages decided so far
+  double cal_rate[4] = {0, 0, 0, 0};
+  int cal_stage = 0;
   uint32_t groups_per_launch = 0;
   uint32_t lanes_alloc = 0;
   int scratch_h = 0;  // inversion-pad entries per lane in d_scratch
@@ -850,7 +852,7 @@ int kh_release_walk(kh_ctx *ctx) {
 
 int kh_bsgs_geometry(kh_ctx *ctx, uint32_t *lanes, double rates[2]) {
   if (!ctx) return KH_E_ARG;
-  if (lanes) *lanes = ctx->bsgs_calibrated ? ctx->lanes_pick : 0;
+  if (lanes) *lanes = ctx->cal_stage >= 1 ? ctx->lanes_pick : 0;
   if (rates) {
     rates[0] = ctx->cal_rate[0];
     rates[1] = ctx->cal_rate[1];
@@ -858,17 +860,59 @@ int kh_bsgs_geometry(kh_ctx *ctx, uint32_t *lanes, double rates[2]) {
   return KH_OK;
 }
 
-int kh_debug_replace_layer1(kh_ctx *ctx) {
-  if (!ctx || !ctx->d_bl[0]) return KH_E_STATE;
+int kh_bsgs_placement(kh_ctx *ctx, double rates[4]) {
+  if (!ctx || !rates) return KH_E_ARG;
+  for (int k = 0; k < 4; k++) rates[k] = ctx->cal_rate[k];
+  return ctx->bsgs_calibrated ? 1 : 0;
+}
+
+// a fresh allocation for one device buffer: the new one is taken while the old is held, the contents
+// copied, then the old one freed
+static int move_buffer(kh_ctx *ctx, void **p, size_t bytes, int which) {
+  if (!*p) return KH_OK;
+  void *nb = nullptr;
+  HIPCHK(ctx, which ? dev_alloc(&nb, bytes, which) : hipMalloc(&nb, bytes));
+  HIPCHK(ctx, hipMemcpy(nb, *p, bytes, hipMemcpyDeviceToDevice));
+  (void)hipFree(*p);
+  *p = nb;
+  return KH_OK;
+}
+
+int kh_debug_replace(kh_ctx *ctx, uint32_t which) {
+  if (!ctx) return KH_E_ARG;
   (void)hipSetDevice(ctx->device);
   HIPCHK(ctx, hipDeviceSynchronize());
-  const size_t bytes = 256 * ctx->bd[0].stride + 4;
-  uint8_t *nb = nullptr;
-  HIPCHK(ctx, dev_alloc(reinterpret_cast<void **>(&nb), bytes, 1));
-  HIPCHK(ctx, hipMemcpy(nb, ctx->d_bl[0], bytes, hipMemcpyDeviceToDevice));
-  (void)hipFree(ctx->d_bl[0]);
-  ctx->d_bl[0] = nb;
-  return KH_OK;
+  int r = KH_OK;
+  if ((which & 1) && ctx->d_bl[0])
+    r = move_buffer(ctx, reinterpret_cast<void **>(&ctx->d_bl[0]), 256 * ctx->bd[0].stride + 4, 1);
+  if (!r && (which & 2) && ctx->d_scratch_base) {  // the pad (no contents to keep)
+    const size_t bytes = ((size_t)ctx->lanes_alloc + ctx->pad_skew) * ctx->scratch_h * 32 + ctx->pad_offset;
+    void *nb = nullptr;
+    HIPCHK(ctx, dev_alloc(&nb, bytes, 2));
+    (void)hipFree(ctx->d_scratch_base);
+    ctx->d_scratch_base = nb;
+    ctx->d_scratch = reinterpret_cast<uint4 *>(static_cast<uint8_t *>(nb) + ctx->pad_offset);
+  }
+  if (!r && (which & 4)) {  // lane centres and scalars (the centres are kept: lanes may continue)
+    const size_t bytes = (size_t)ctx->lanes_alloc * 32;
+    r = move_buffer(ctx, reinterpret_cast<void **>(&ctx->d_cx), bytes, 0);
+    if (!r) r = move_buffer(ctx, reinterpret_cast<void **>(&ctx->d_cy), bytes, 0);
+    if (!r) r = move_buffer(ctx, reinterpret_cast<void **>(&ctx->d_scalars), bytes, 0);
+  }
+  if (!r && (which & 8)) {  // the walks' delta tables
+    for (auto &t : ctx->tables) {
+      const size_t H = (size_t)atoi(t.first.c_str() + 32);  // key: 32 scalar bytes, then "H/jump"
+      void *q = t.second;
+      r = move_buffer(ctx, &q, (H + 1) * 16 * 4, 0);
+      if (r) break;
+      t.second = static_cast<uint32_t *>(q);
+    }
+  }
+  if (!r && (which & 16)) {  // layers 2 and 3
+    for (int l = 1; l < 3 && !r; l++)
+      r = move_buffer(ctx, reinterpret_cast<void **>(&ctx->d_bl[l]), 256 * ctx->bd[l].stride + 4, 0);
+  }
+  return r;
 }
 
 int kh_debug_layout(kh_ctx *ctx, uint64_t out[8]) {
@@ -893,7 +937,8 @@ int kh_set_geometry(kh_ctx *ctx, uint32_t lanes, uint32_t groups_per_launch) {
   // an explicit geometry overrides an earlier calibration's pick (and a default one calibrates again)
   ctx->lanes_pick = 0;
   ctx->bsgs_calibrated = false;
-  ctx->cal_rate[0] = ctx->cal_rate[1] = 0;
+  ctx->cal_stage = 0;
+  for (double &x : ctx->cal_rate) x = 0;
   return KH_OK;
 }
 
@@ -2505,98 +2550,106 @@ static int bsgs_scan_one(kh_ctx *ctx, const u256 &st, const std::vector<u256> *l
   return nf > cap ? KH_E_OVERFLOW : KH_OK;
 }
 
-// The giant walk's rate depends on where its 64-GB inversion pad lands in physical memory: the same
-// process walks ~2.5-5 % faster on one allocation than on another, with identical instruction and
-// request counts; the slow placement shows only longer L2 request latencies in cycles at a higher
-// clock (DESIGN.md §2 "Placement", profiles/r06f_state_counters.json).  Re-allocating alternates between
-// placements (r06e_pad_alloc_sweep.json), so a context's first continuous call of at least 2^23 walk
-// groups times candidate placements against each other: the primary pad and KH_PAD_CANDIDATES - 1
-// (default 1) more pads of the same size, allocated while the primary is held (when the device keeps
-// 32 GB free besides), all at 2^21 lanes.  The call is cut into parts walked on the candidates in the
-// order A B B A (A B C C B A ...), so a linear drift of clock or power cancels; each part is timed on the
-// walk's events, the fastest pad becomes the context's pad and the others are freed.  With no room for a
-// second pad the candidates are 2^21 lanes and 2^20 lanes, which walk the first half of the same pad.
-// KH_BSGS_CALIBRATE=0, KH_BSGS_LANES or kh_set_geometry's lanes switch the calibration off.  Every base
-// is walked once either way, so keys and candidates are those of an uncalibrated call.
-struct pad_slot {
-  void *base;
-  uint4 *ptr;
+// The giant walk's rate depends on where its two big buffers land in physical memory: the same process
+// walks ~1-5 % faster on one allocation of the 64-GB inversion pad than on another, and ~1.5 % faster on
+// one allocation of layer 1 than on another, with identical instruction and request counts; the slow
+// placements show only longer L2 request latencies in cycles at a higher clock (DESIGN.md §2
+// "Placement", profiles/r06f_state_counters.json, r06h_layer1_vs_pad.json).  Re-allocating alternates
+// between placements, so a context's first continuous calls of at least 2^23 walk groups calibrate in
+// two stages of four parts each, one candidate pair per stage:
+//   stage 0, the pad: the primary pad and KH_PAD_CANDIDATES - 1 (default 1) more pads of the same size,
+//            allocated while the primary is held (when the device keeps 32 GB free besides), all at 2^21
+//            lanes; with no room for a second pad, 2^21 and 2^20 lanes (which walk the first half of the
+//            one pad: other physical pages);
+//   stage 1, layer 1: the primary layer 1 and a copy of it in a new allocation.
+// A stage walks its parts on the candidates in the order A B B A (A B C C B A, ...), so a linear drift of
+// clock or power cancels, times each part on the walk's events, keeps the faster candidate and frees the
+// other.  Neither buffer holds state across launches that the swap could break: the pad is rewritten by
+// every group, and the copies of layer 1 are identical, so the lanes run on through the swaps.  A call
+// runs as many stages as it has 4 tiles of 2^21 groups for; the bases after them walk normally.
+// KH_BSGS_CALIBRATE=0, KH_BSGS_LANES or kh_set_geometry's lanes switch it off.  Every base is walked once
+// either way, so keys and candidates are those of an uncalibrated call.
+static constexpr int KH_CAL_SKIP = 1000;  // cal_stage: nothing walked, no candidate fits
+struct cal_slot {
+  void *base;  // the allocation (freed when the slot loses)
+  void *ptr;   // what the walk reads (the pad: base + KH_PAD_OFFSET)
 };
-static void swap_pad(kh_ctx *ctx, pad_slot &p) {
-  std::swap(ctx->d_scratch_base, p.base);
-  std::swap(ctx->d_scratch, p.ptr);
+static void cal_swap(kh_ctx *ctx, int stage, cal_slot &c) {
+  if (stage == 0) {
+    std::swap(ctx->d_scratch_base, c.base);
+    void *p = ctx->d_scratch;
+    ctx->d_scratch = static_cast<uint4 *>(c.ptr);
+    c.ptr = p;
+  } else {
+    void *p = ctx->d_bl[0];
+    ctx->d_bl[0] = static_cast<uint8_t *>(c.ptr);
+    c.ptr = p;
+    c.base = p;
+  }
 }
-static int bsgs_scan_impl(kh_ctx *ctx, const u256 &st, const std::vector<u256> *list, uint64_t n_bases,
-                          kh_bsgs_found *found, uint32_t cap, uint32_t *n_found) {
-  if (!ctx->bsgs_built) return KH_E_STATE;
+// one calibration stage over the n_bases bases from st; returns the walk's status, hits in found
+static int cal_stage(kh_ctx *ctx, int stage, const u256 &st, uint64_t n_bases, kh_bsgs_found *found, uint32_t cap,
+                     uint32_t *n_found) {
   const kh_bsgs_info &I = ctx->info;
-  const uint64_t A_pts = I.cycles * 1024;
-  const uint64_t gpb = A_pts / (2 * KH_WALK_HB);
   const uint32_t hi = ctx->lanes_bsgs, lo = ctx->lanes_bsgs / 2;
-  const char *cal = getenv("KH_BSGS_CALIBRATE");
-  const char *ncand = getenv("KH_PAD_CANDIDATES");
-  // candidates: KH_PAD_CANDIDATES (default 2), as many as the call has pairs of 2^21-group tiles for
-  const uint64_t tiles = n_bases * gpb / std::max<uint32_t>(1, hi);
-  const int want = (int)std::max<uint64_t>(1, std::min<uint64_t>(std::min(4, ncand ? atoi(ncand) : 2), tiles / 2));
-  const bool calibrate = !ctx->bsgs_calibrated && !list && A_pts == I.aux && A_pts % (2 * KH_WALK_HB) == 0 &&
-                         hi == KH_BSGS_LANES && lo > ctx->lanes_max && !(cal && atoi(cal) == 0) &&
-                         !getenv("KH_BSGS_LANES") && !getenv("KH_BSGS_NARROW") && !getenv("KH_NO_BIG_GROUPS") &&
-                         tiles >= 4 && ctx->targets.size() == 1 && !ctx->found[0];
-  if (!calibrate) return bsgs_scan_one(ctx, st, list, n_bases, found, cap, n_found);
-  // the primary pad at 2^21 lanes (bsgs_scan_one would take it too), then the extra candidates
+  const uint64_t gpb = I.cycles * 1024 / (2 * KH_WALK_HB);
+  const uint64_t rows = walk_pad_rows(KM_BSGSB, false, KH_WALK_HB);
   struct cand {
-    int pad;
+    int slot;  // 0: the primary (in ctx), k: slots[k]
     uint32_t lanes;
     double ms, pts;
   };
-  std::vector<cand> cands;
-  std::vector<pad_slot> pads(1, pad_slot{nullptr, nullptr});  // pads[0]: the primary (lives in ctx)
-  {
-    size_t fr = 0, tot = 0;
-    const uint64_t pad_bytes = ((uint64_t)hi + ctx->pad_skew) * walk_pad_rows(KM_BSGSB, false, KH_WALK_HB) * 32 +
-                               env_pad_offset();
-    const uint64_t lane_bytes = (uint64_t)hi * (walk_pad_rows(KM_BSGSB, false, KH_WALK_HB) * 32 + 96);
-    const bool known = hipMemGetInfo(&fr, &tot) == hipSuccess;
-    const uint64_t have = ctx->lanes_alloc >= hi ? lane_bytes : 0;
-    if (!known || fr + have < lane_bytes + (32ull << 30) || ensure_pipeline(ctx, hi, KH_WALK_HB) != KH_OK) {
-      (void)hipGetLastError();
-      ctx->err.clear();
-      return bsgs_scan_one(ctx, st, list, n_bases, found, cap, n_found);  // no room: its own fallback
-    }
-    cands.push_back({0, hi, 0, 0});
+  std::vector<cand> cands{{0, hi, 0, 0}};
+  std::vector<cal_slot> slots(1, cal_slot{nullptr, nullptr});
+  size_t fr = 0, tot = 0;
+  if (stage == 0) {
+    const char *ncand = getenv("KH_PAD_CANDIDATES");
+    const int want = std::max(1, std::min(4, ncand ? atoi(ncand) : 2));
+    const uint64_t pad_bytes = ((uint64_t)hi + ctx->pad_skew) * rows * 32 + ctx->pad_offset;
     for (int k = 1; k < want; k++) {
-      if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr < pad_bytes + (32ull << 30)) break;
       void *b = nullptr;
-      if (dev_alloc(&b, pad_bytes, 2) != hipSuccess) {
+      if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr < pad_bytes + (32ull << 30) ||
+          dev_alloc(&b, pad_bytes, 2) != hipSuccess) {
         (void)hipGetLastError();
         break;
       }
-      pads.push_back({b, reinterpret_cast<uint4 *>(static_cast<uint8_t *>(b) + ctx->pad_offset)});
-      cands.push_back({(int)pads.size() - 1, hi, 0, 0});
+      slots.push_back({b, static_cast<uint8_t *>(b) + ctx->pad_offset});
+      cands.push_back({(int)slots.size() - 1, hi, 0, 0});
     }
     if (cands.size() == 1) cands.push_back({0, lo, 0, 0});  // one pad: 2^20 lanes walk its first half
+  } else {
+    const size_t bytes = 256 * ctx->bd[0].stride + 4;
+    void *b = nullptr;
+    if (hipMemGetInfo(&fr, &tot) == hipSuccess && fr >= bytes + (32ull << 30) && dev_alloc(&b, bytes, 1) == hipSuccess &&
+        hipMemcpy(b, ctx->d_bl[0], bytes, hipMemcpyDeviceToDevice) == hipSuccess) {
+      slots.push_back({b, b});
+      cands.push_back({1, hi, 0, 0});
+    } else {
+      (void)hipGetLastError();
+      if (b) (void)hipFree(b);
+      return KH_CAL_SKIP;  // no room for a copy: the stage is skipped
+    }
   }
   const int nc = (int)cands.size();
   std::vector<int> order;
   for (int k = 0; k < nc; k++) order.push_back(k);
   for (int k = nc - 1; k >= 0; k--) order.push_back(k);
-  // parts in whole tiles of the wider count, so each tiles exactly; the last takes the rest
   const uint64_t tile = std::max<uint64_t>(1, hi / std::max<uint64_t>(1, gpb));
   const uint64_t nbq = std::max<uint64_t>(tile, (n_bases / order.size()) / tile * tile);
   uint32_t nf_all = 0;
   bool exact = true;
-  int r = KH_OK, cur = 0;  // cur: the pads[] entry now in ctx
+  int r = KH_OK, cur = 0;
   uint64_t done_b = 0;
   for (size_t q = 0; q < order.size() && done_b < n_bases; q++) {
     cand &c = cands[order[q]];
     const uint64_t nb = q + 1 == order.size() ? n_bases - done_b : std::min(nbq, n_bases - done_b);
     const u256 s = sc_add(st, sc_reduce(u256_from_u128((u128)done_b * 2 * I.n)));
-    if (c.pad != cur) {  // the pad holds no state across launches: swap it under the running lanes
+    if (c.slot != cur) {  // swap the buffer under the running lanes (the walk is idle between calls)
       (void)hipStreamSynchronize(ctx->stream);
       (void)hipStreamSynchronize(ctx->side);
-      if (cur) swap_pad(ctx, pads[cur]);    // the primary back into ctx
-      if (c.pad) swap_pad(ctx, pads[c.pad]);
-      cur = c.pad;
+      if (cur) cal_swap(ctx, stage, slots[cur]);  // the primary back
+      if (c.slot) cal_swap(ctx, stage, slots[c.slot]);
+      cur = c.slot;
     }
     ctx->lanes_force = c.lanes;
     const timing t0 = ctx->tm[2];
@@ -2611,29 +2664,89 @@ static int bsgs_scan_impl(kh_ctx *ctx, const u256 &st, const std::vector<u256> *
     done_b += nb;
     if ((r && r != KH_E_OVERFLOW) || ctx->found[0]) break;  // an error, or the key ended the call
   }
-  // keep the fastest timed candidate's pad (and lane count); free the other pads
   (void)hipStreamSynchronize(ctx->stream);
   (void)hipStreamSynchronize(ctx->side);
-  int best = -1;
-  for (int k = 0; k < nc; k++)
-    if (cands[k].ms > 0 && cands[k].pts > 0 &&
-        (best < 0 || cands[k].pts / cands[k].ms > cands[best].pts / cands[best].ms))
-      best = k;
-  int timed = 0;
-  for (int k = 0; k < nc; k++) timed += cands[k].ms > 0 && cands[k].pts > 0;
-  const int keep_pad = best >= 0 && timed == nc && exact && r == KH_OK ? cands[best].pad : cur;
-  if (cur) swap_pad(ctx, pads[cur]);          // primary back in ctx
-  if (keep_pad) swap_pad(ctx, pads[keep_pad]);  // the kept pad into ctx, the primary into its slot
-  for (size_t k = 1; k < pads.size(); k++) (void)hipFree(pads[k].base);
-  *n_found = nf_all;
-  if (best >= 0 && timed == nc && exact) {
-    ctx->lanes_pick = cands[best].lanes;
-    ctx->bsgs_calibrated = true;
-    ctx->cal_rate[0] = cands[best].pts / cands[best].ms * 1e3;
-    ctx->cal_rate[1] = 0;
-    for (int k = 0; k < nc; k++)
-      if (k != best) ctx->cal_rate[1] = std::max(ctx->cal_rate[1], cands[k].pts / cands[k].ms * 1e3);
+  int best = -1, timed = 0;
+  for (int k = 0; k < nc; k++) {
+    if (!(cands[k].ms > 0 && cands[k].pts > 0)) continue;
+    timed++;
+    if (best < 0 || cands[k].pts / cands[k].ms > cands[best].pts / cands[best].ms) best = k;
   }
+  const bool decided = best >= 0 && timed == nc && exact && (r == KH_OK || r == KH_E_OVERFLOW);
+  const int keep = decided ? cands[best].slot : cur;
+  if (cur) cal_swap(ctx, stage, slots[cur]);     // the primary back in ctx
+  if (keep) cal_swap(ctx, stage, slots[keep]);   // the kept one into ctx, the primary into its slot
+  for (size_t k = 1; k < slots.size(); k++) (void)hipFree(slots[k].base);
+  *n_found = nf_all;
+  if (decided) {
+    if (stage == 0) ctx->lanes_pick = cands[best].lanes;
+    ctx->cal_rate[2 * stage] = cands[best].pts / cands[best].ms * 1e3;
+    ctx->cal_rate[2 * stage + 1] = 0;
+    for (int k = 0; k < nc; k++)
+      if (k != best) ctx->cal_rate[2 * stage + 1] = std::max(ctx->cal_rate[2 * stage + 1], cands[k].pts / cands[k].ms * 1e3);
+    ctx->cal_stage = stage + 1;
+  }
+  return r;
+}
+static int bsgs_scan_impl(kh_ctx *ctx, const u256 &st, const std::vector<u256> *list, uint64_t n_bases,
+                          kh_bsgs_found *found, uint32_t cap, uint32_t *n_found) {
+  if (!ctx->bsgs_built) return KH_E_STATE;
+  const kh_bsgs_info &I = ctx->info;
+  const uint64_t A_pts = I.cycles * 1024;
+  const uint64_t gpb = A_pts / (2 * KH_WALK_HB);
+  const uint32_t hi = ctx->lanes_bsgs, lo = ctx->lanes_bsgs / 2;
+  const uint64_t tile = std::max<uint64_t>(1, hi / std::max<uint64_t>(1, gpb));  // bases per 2^21 groups
+  const char *cal = getenv("KH_BSGS_CALIBRATE");
+  const bool calibrate = !ctx->bsgs_calibrated && !list && A_pts == I.aux && A_pts % (2 * KH_WALK_HB) == 0 &&
+                         hi == KH_BSGS_LANES && lo > ctx->lanes_max && !(cal && atoi(cal) == 0) &&
+                         !getenv("KH_BSGS_LANES") && !getenv("KH_BSGS_NARROW") && !getenv("KH_NO_BIG_GROUPS") &&
+                         n_bases * gpb >= 4ull * hi && ctx->targets.size() == 1 && !ctx->found[0];
+  if (!calibrate) return bsgs_scan_one(ctx, st, list, n_bases, found, cap, n_found);
+  // the primary pad at 2^21 lanes first (bsgs_scan_one would take it too): with no room, no calibration
+  {
+    size_t fr = 0, tot = 0;
+    const uint64_t lane_bytes = (uint64_t)hi * (walk_pad_rows(KM_BSGSB, false, KH_WALK_HB) * 32 + 96);
+    const uint64_t have = ctx->lanes_alloc >= hi ? lane_bytes : 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr + have < lane_bytes + (32ull << 30) ||
+        ensure_pipeline(ctx, hi, KH_WALK_HB) != KH_OK) {
+      (void)hipGetLastError();
+      ctx->err.clear();
+      return bsgs_scan_one(ctx, st, list, n_bases, found, cap, n_found);
+    }
+  }
+  uint32_t nf_all = 0;
+  uint64_t done_b = 0;
+  int r = KH_OK;
+  // stages while the call has 4 tiles left for one (the last stage of the call takes the rest of it)
+  while (ctx->cal_stage < 2 && (n_bases - done_b) >= 4 * tile && !ctx->found[0]) {
+    const uint64_t left = n_bases - done_b;
+    const uint64_t nb = ctx->cal_stage == 0 && left >= 8 * tile ? left / 2 / tile * tile : left;
+    const u256 s = sc_add(st, sc_reduce(u256_from_u128((u128)done_b * 2 * I.n)));
+    uint32_t nf = 0;
+    const uint32_t off = std::min(nf_all, cap);
+    const int stage = ctx->cal_stage;
+    r = cal_stage(ctx, stage, s, nb, found ? found + off : nullptr, cap - off, &nf);
+    if (r == KH_CAL_SKIP) {  // no room for the stage's candidate: calibration ends here
+      r = KH_OK;
+      ctx->cal_stage = 2;
+      break;
+    }
+    nf_all += nf;
+    done_b += nb;
+    if (r && r != KH_E_OVERFLOW) return r;
+    if (ctx->cal_stage == stage) break;  // undecided (the key ended the call): try again next call
+  }
+  if (ctx->cal_stage >= 2) ctx->bsgs_calibrated = true;
+  if (done_b < n_bases && !ctx->found[0] && (r == KH_OK || r == KH_E_OVERFLOW)) {
+    const u256 s = sc_add(st, sc_reduce(u256_from_u128((u128)done_b * 2 * I.n)));
+    uint32_t nf = 0;
+    const uint32_t off = std::min(nf_all, cap);
+    const int r2 = bsgs_scan_one(ctx, s, nullptr, n_bases - done_b, found ? found + off : nullptr, cap - off, &nf);
+    nf_all += nf;
+    if (r2 && r2 != KH_E_OVERFLOW) return r2;
+    if (r2) r = r2;
+  }
+  *n_found = nf_all;
   return *n_found > cap ? KH_E_OVERFLOW : r;
 }
 

@@ -79,7 +79,8 @@ def lib() -> ctypes.CDLL:
     L.kh_set_geometry.argtypes = [P, ctypes.c_uint32, ctypes.c_uint32]
     L.kh_release_walk.argtypes = [P]
     L.kh_debug_layout.argtypes = [P, ctypes.POINTER(ctypes.c_uint64 * 8)]
-    L.kh_debug_replace_layer1.argtypes = [P]
+    L.kh_bsgs_placement.argtypes = [P, ctypes.POINTER(ctypes.c_double * 4)]
+    L.kh_debug_replace.argtypes = [P, ctypes.c_uint32]
     L.kh_bsgs_geometry.argtypes = [P, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_double * 2)]
     L.kh_synchronize.argtypes = [P]
     L.kh_scan_memory.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64)]
@@ -190,9 +191,21 @@ class Engine:
         return {"layer1": [hex(o[0]), o[1]], "pad": [hex(o[2]), o[3]], "layer2": [hex(o[4]), o[5]],
                 "lanes": o[6], "pad_rows": o[7]}
 
+    def debug_replace(self, which: int) -> None:
+        """Give device buffers fresh allocations (kh_debug_replace; diagnostics): 1 layer 1, 2 the pad,
+        4 the lane arrays, 8 the delta tables, 16 layers 2 and 3."""
+        self._chk(lib().kh_debug_replace(self._ctx, which), "kh_debug_replace")
+
     def debug_replace_layer1(self) -> None:
-        """Move the BSGS layer-1 filter to a fresh allocation (kh_debug_replace_layer1; diagnostics)."""
-        self._chk(lib().kh_debug_replace_layer1(self._ctx), "kh_debug_replace_layer1")
+        self.debug_replace(1)
+
+    def bsgs_placement(self) -> tuple[bool, list[float]]:
+        """(calibration complete, [pad kept, pad other, layer-1 kept, layer-1 other] giant points/s)."""
+        rates = (ctypes.c_double * 4)()
+        r = lib().kh_bsgs_placement(self._ctx, ctypes.byref(rates))
+        if r < 0:
+            self._chk(r, "kh_bsgs_placement")
+        return r == 1, list(rates)
 
     def release_walk(self) -> None:
         """Free the walks' lane arrays and inversion pad (kh_release_walk)."""

@@ -463,14 +463,15 @@ def test_calls_with_ragged_lane_tiles(oracle, lanes, calls):
 
 @pytest.mark.parametrize("cands", [2, 3])
 def test_placement_calibration_same_results(oracle, monkeypatch, cands):
-    """A context's first call of >= 2^23 walk groups walks its parts on candidate pad placements (the
-    primary pad and KH_PAD_CANDIDATES - 1 more, in the order A B B A / A B C C B A, or 2^21 and 2^20 lanes
-    on one pad when the device has no room) and keeps the fastest: the same first-level candidates and
-    walked points as an uncalibrated call (KH_BSGS_CALIBRATE=0), the key found in any part, and
-    kh_bsgs_geometry reports the kept and the best other candidate's rates."""
+    """A context's first call of >= 2^23 walk groups walks its parts on candidate placements -- first of
+    the pad (the primary and KH_PAD_CANDIDATES - 1 more, in the order A B B A / A B C C B A, or 2^21 and
+    2^20 lanes on one pad when the device has no room), then of layer 1 (a copy) -- and keeps the fastest
+    of each: the same first-level candidates and walked points as an uncalibrated call
+    (KH_BSGS_CALIBRATE=0), the key found in any part, and kh_bsgs_geometry / kh_bsgs_placement report
+    the kept and the best other candidates' rates."""
     import keyhunt_amd as K
     p = oracle.bsgs_params(N36, K16)
-    nb = 3 << 20                           # 4 groups per base: 6 x 2^21 groups (six parts for 3 pads)
+    nb = 1 << 22                           # 4 groups per base: 8 x 2^21 groups, both stages in one call
     start = 0x3C3C3C3C3C000000
     far = start - 777 * 2 * p.n
     monkeypatch.setenv("KH_PAD_CANDIDATES", str(cands))
@@ -486,12 +487,14 @@ def test_placement_calibration_same_results(oracle, monkeypatch, cands):
             e.bsgs_set_targets([oracle.pubkey(far)])
             c0 = e.bsgs_candidates()
             assert e.bsgs_scan(start, nb) == []
-            res.append((e.bsgs_candidates() - c0, _walked(e), e.bsgs_geometry()))
+            res.append((e.bsgs_candidates() - c0, _walked(e), e.bsgs_geometry(), e.bsgs_placement()))
     assert res[0][0] == res[1][0] and res[0][0] > 1000
     assert res[0][1] == res[1][1] == nb * p.aux
     lanes, r_kept, r_other = res[0][2]
     assert lanes in (1 << 21, 1 << 20) and r_kept >= r_other > 0
-    assert res[1][2] == (0, 0.0, 0.0)
+    done, rates = res[0][3]
+    assert done and rates[0] == r_kept and rates[2] >= rates[3] > 0
+    assert res[1][2] == (0, 0.0, 0.0) and res[1][3] == (False, [0.0] * 4)
     monkeypatch.delenv("KH_BSGS_CALIBRATE", raising=False)
     for where in (3, nb // 2 - 7, nb - 5):  # the key in the first, a middle and the last part
         key = start + where * 2 * p.n + 999

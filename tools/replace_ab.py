@@ -1,10 +1,11 @@
 """Which buffer's placement sets the BSGS walk's state?  One process on the bench geometry (n = 2^44,
-k = 128, 2^21 lanes, no calibration): --l1 times, move layer 1 to a fresh allocation
-(kh_debug_replace_layer1) and time --calls calls of --bases bases; then --pad times, re-allocate the
-pad instead (kh_release_walk) and time the same.  Prints one JSON object with every step's rate and
-the board's clock and power.
+k = 128, 2^21 lanes, no calibration): for each entry of --seq, give the buffers it names fresh
+allocations (kh_debug_replace: 1 layer 1, 2 the pad, 4 the lane arrays, 8 the delta tables, 16 layers
+2/3; "r" = kh_release_walk) and time --calls calls of --bases bases after one warm call.  Prints one
+JSON object with every step's rate and the board's clock and power.  (Round-6 r06h ran it as
+--seq 1,1,1,1,1,1,r,r,r,r.)
 
-usage: python tools/l1_replace_ab.py [--l1 6] [--pad 4] [--calls 1] [--bases 4194304]
+usage: python tools/replace_ab.py [--seq 8,8,4,4,1,1,2,2] [--calls 1] [--bases 4194304]
 """
 import argparse
 import json
@@ -22,8 +23,7 @@ import keyhunt_amd as K  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--l1", type=int, default=6)
-    ap.add_argument("--pad", type=int, default=4)
+    ap.add_argument("--seq", default="8,8,4,4,1,1,2,2")
     ap.add_argument("--calls", type=int, default=1)
     ap.add_argument("--bases", type=int, default=1 << 22)
     a = ap.parse_args()
@@ -56,13 +56,15 @@ def main():
         print(json.dumps({"moved": what, "k": k, "G": round(r["giant_points_per_s"] / 1e9, 3),
                           "mhz": round(r["mhz"] or 0), "w": round(r["w"] or 0)}), file=sys.stderr, flush=True)
 
+    names = {1: "layer1", 2: "pad", 4: "lanes", 8: "tables", 16: "layers23"}
     timed("none", 0)
-    for k in range(a.l1):
-        e.debug_replace_layer1()
-        timed("layer1", k)
-    for k in range(a.pad):
-        e.release_walk()
-        timed("pad", k)
+    for k, w in enumerate(a.seq.split(",")):
+        if w == "r":
+            e.release_walk()
+            timed("release_walk", k)
+        else:
+            e.debug_replace(int(w))
+            timed("+".join(v for b, v in names.items() if int(w) & b), k)
     board.stop()
     e.close()
     print(json.dumps({"bases_per_call": a.bases, "calls": a.calls, "rows": rows}, indent=1))
