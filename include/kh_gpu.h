@@ -136,7 +136,8 @@ int kh_bsgs_placement(kh_ctx *ctx, double rates[4]);
 int kh_debug_layout(kh_ctx *ctx, uint64_t out[8]);
 /* diagnostics (DESIGN.md §2 "Placement"): give device buffers fresh allocations, taken while the old
  * ones are held, contents copied: which = 1 layer 1, 2 the inversion pad, 4 the lane centres and scalars,
- * 8 the walks' delta tables, 16 layers 2 and 3 (bits may be combined).  Results are unchanged. */
+ * 8 the walks' delta tables, 16 layers 2 and 3, 32 a new walk stream (bits may be combined).  Results
+ * are unchanged. */
 int kh_debug_replace(kh_ctx *ctx, uint32_t which);
 int kh_synchronize(kh_ctx *ctx);
 

@@ -341,6 +341,8 @@ struct kh_ctx {
   // [2s] the one kept, [2s + 1] the best other one; cal_stage: stages decided so far
   double cal_rate[4] = {0, 0, 0, 0};
   int cal_stage = 0;
+  uint64_t cal_moved_bases = 0;  // bases the last KH_CAL_MOVE stage walked
+  uint32_t cal_deferred = 0;      // eligible calls walked uncalibrated (KH_CAL_DEFER)
   uint32_t groups_per_launch = 0;
   uint32_t lanes_alloc = 0;
   int scratch_h = 0;  // inversion-pad entries per lane in d_scratch
@@ -511,6 +513,12 @@ hipError_t dev_alloc(void **p, size_t bytes, int which) {
 static uint32_t env_pad_skew() {
   const char *e = getenv("KH_PAD_SKEW");
   return e ? (uint32_t)strtoul(e, nullptr, 0) : 0u;
+}
+
+// KH_PAD_SWZ=1: rotate each pad row's columns by workgroup (walk_args::pad_swz), when the lanes allow
+static uint32_t pad_swizzle(uint32_t L) {
+  const char *e = getenv("KH_PAD_SWZ");  // read per launch: A/B tools switch it inside one process
+  return e && atoi(e) && L % 2048 == 0 ? 1u : 0u;
 }
 
 // KH_PAD_OFFSET=<bytes>: the pad starts that far (rounded down to 256 B) into its allocation (A/B knob)
@@ -908,6 +916,12 @@ int kh_debug_replace(kh_ctx *ctx, uint32_t which) {
       t.second = static_cast<uint32_t *>(q);
     }
   }
+  if (!r && (which & 32)) {  // the walk's stream: a new one (another hardware queue), then the old one destroyed
+    hipStream_t ns = nullptr;
+    HIPCHK(ctx, hipStreamCreateWithFlags(&ns, hipStreamNonBlocking));
+    (void)hipStreamDestroy(ctx->stream);
+    ctx->stream = ns;
+  }
   if (!r && (which & 16)) {  // layers 2 and 3
     for (int l = 1; l < 3 && !r; l++)
       r = move_buffer(ctx, reinterpret_cast<void **>(&ctx->d_bl[l]), 256 * ctx->bd[l].stride + 4, 0);
@@ -1178,6 +1192,7 @@ int kh_scan(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride_be[32], u
   A.scratch = ctx->d_scratch;
   A.L = jg.L;
   A.pad_skew = ctx->pad_skew;
+  A.pad_swz = pad_swizzle(A.L);
   A.lane_stride = jg.gpl * 2 * H;
   A.interleave = inter ? 1 : 0;
   A.n_points = n_points;
@@ -1486,6 +1501,7 @@ int build_walk(kh_ctx *ctx, int mode, uint8_t *bl1, const bloom_desc &bd1, uint6
   A.scratch = ctx->d_scratch;
   A.L = jg.L;
   A.pad_skew = ctx->pad_skew;
+  A.pad_swz = pad_swizzle(A.L);
   A.lane_stride = jg.gpl * 2 * H;
   A.n_points = count;
   A.bl1 = bl1;
@@ -2359,6 +2375,7 @@ static int bsgs_scan_one(kh_ctx *ctx, const u256 &st, const std::vector<u256> *l
       Aw.scratch = ctx->d_scratch;
       Aw.L = jg.L;
       Aw.pad_skew = ctx->pad_skew;
+      Aw.pad_swz = pad_swizzle(Aw.L);
       Aw.lane_stride = jg.gpl * 2 * H;
       Aw.interleave = cont ? 1 : 0;
       Aw.n_points = cont ? total_groups * 2 * H : rg * 2 * H;
@@ -2550,25 +2567,23 @@ static int bsgs_scan_one(kh_ctx *ctx, const u256 &st, const std::vector<u256> *l
   return nf > cap ? KH_E_OVERFLOW : KH_OK;
 }
 
-// The giant walk's rate depends on where its two big buffers land in physical memory: the same process
-// walks ~1-5 % faster on one allocation of the 64-GB inversion pad than on another, and ~1.5 % faster on
-// one allocation of layer 1 than on another, with identical instruction and request counts; the slow
-// placements show only longer L2 request latencies in cycles at a higher clock (DESIGN.md §2
-// "Placement", profiles/r06f_state_counters.json, r06h_layer1_vs_pad.json).  Re-allocating alternates
-// between placements, so a context's first continuous calls of at least 2^23 walk groups calibrate in
-// two stages of four parts each, one candidate pair per stage:
-//   stage 0, the pad: the primary pad and KH_PAD_CANDIDATES - 1 (default 1) more pads of the same size,
-//            allocated while the primary is held (when the device keeps 32 GB free besides), all at 2^21
-//            lanes; with no room for a second pad, 2^21 and 2^20 lanes (which walk the first half of the
-//            one pad: other physical pages);
-//   stage 1, layer 1: the primary layer 1 and a copy of it in a new allocation.
-// A stage walks its parts on the candidates in the order A B B A (A B C C B A, ...), so a linear drift of
-// clock or power cancels, times each part on the walk's events, keeps the faster candidate and frees the
-// other.  Neither buffer holds state across launches that the swap could break: the pad is rewritten by
-// every group, and the copies of layer 1 are identical, so the lanes run on through the swaps.  A call
-// runs as many stages as it has 4 tiles of 2^21 groups for; the bases after them walk normally.
-// KH_BSGS_CALIBRATE=0, KH_BSGS_LANES or kh_set_geometry's lanes switch it off.  Every base is walked once
-// either way, so keys and candidates are those of an uncalibrated call.
+// The giant walk's rate depends on where its 64-GB inversion pad (and on some boxes its layer 1) land in
+// physical memory and on the box: the same process walks 1-8 % faster on one allocation of the pad than
+// on another, with identical instruction and request counts; the slow placements show only longer L2
+// request latencies in cycles at a higher clock (DESIGN.md §2 "Placement", profiles/r06f_state_counters.json,
+// r06j_buffer_replacement.json).  A context's first continuous call of at least 2^23 walk groups therefore
+// calibrates: it walks the call's parts on candidate placements in the order A B B A (A B C C B A, ...),
+// so a linear drift of clock or power cancels, times each part on the walk's events and keeps the faster.
+// The default candidates are 2^21 and 2^20 lanes on the one pad (2^20 lanes walk its first half: other
+// physical pages) -- the form that measured best over five boxes (profiles/r06n..r06q_calibration_ab.json:
+// 41.2 G giant points/s mean against 40.7 uncalibrated, never below 39.4).  Opt-in stages, measured no
+// better: KH_PAD_CANDIDATES=N (N pads of the same size held at once, each at 2^21 lanes; with
+// KH_CAL_LANES=1 the primary at 2^20 lanes too), KH_CAL_STAGES=2 (then a stage over layer 1: a copy in a
+// new allocation), KH_CAL_MOVE=1 (the pad moved once or twice instead), KH_CAL_DEFER=N (the first N calls
+// uncalibrated).  Neither buffer holds state across launches that a swap could break: the pad is
+// rewritten by every group and the layer-1 copies are identical, so the lanes run on through the swaps.
+// KH_BSGS_CALIBRATE=0, KH_BSGS_LANES or kh_set_geometry's lanes switch the calibration off.  Every base
+// is walked once either way, so keys and candidates are those of an uncalibrated call.
 static constexpr int KH_CAL_SKIP = 1000;  // cal_stage: nothing walked, no candidate fits
 struct cal_slot {
   void *base;  // the allocation (freed when the slot loses)
@@ -2604,7 +2619,7 @@ static int cal_stage(kh_ctx *ctx, int stage, const u256 &st, uint64_t n_bases, k
   size_t fr = 0, tot = 0;
   if (stage == 0) {
     const char *ncand = getenv("KH_PAD_CANDIDATES");
-    const int want = std::max(1, std::min(4, ncand ? atoi(ncand) : 2));
+    const int want = std::max(1, std::min(4, ncand ? atoi(ncand) : 1));
     const uint64_t pad_bytes = ((uint64_t)hi + ctx->pad_skew) * rows * 32 + ctx->pad_offset;
     for (int k = 1; k < want; k++) {
       void *b = nullptr;
@@ -2616,7 +2631,9 @@ static int cal_stage(kh_ctx *ctx, int stage, const u256 &st, uint64_t n_bases, k
       slots.push_back({b, static_cast<uint8_t *>(b) + ctx->pad_offset});
       cands.push_back({(int)slots.size() - 1, hi, 0, 0});
     }
-    if (cands.size() == 1) cands.push_back({0, lo, 0, 0});  // one pad: 2^20 lanes walk its first half
+    // one pad (or KH_CAL_LANES=1): 2^20 lanes, which walk the first half of the primary pad
+    const char *cl = getenv("KH_CAL_LANES");
+    if (cands.size() == 1 || (cl && atoi(cl))) cands.push_back({0, lo, 0, 0});
   } else {
     const size_t bytes = 256 * ctx->bd[0].stride + 4;
     void *b = nullptr;
@@ -2688,6 +2705,53 @@ static int cal_stage(kh_ctx *ctx, int stage, const u256 &st, uint64_t n_bases, k
   }
   return r;
 }
+// KH_CAL_MOVE=1 (pad stage variant): walk a part on the current pad, move the pad (a new allocation
+// taken while the old one is held, then the old one freed), walk a part; if that was slower, move once
+// more and keep the third placement.  Parts of n_bases / 3 (whole tiles).
+static int cal_move(kh_ctx *ctx, const u256 &st, uint64_t n_bases, kh_bsgs_found *found, uint32_t cap,
+                    uint32_t *n_found) {
+  const kh_bsgs_info &I = ctx->info;
+  const uint32_t hi = ctx->lanes_bsgs;
+  const uint64_t gpb = I.cycles * 1024 / (2 * KH_WALK_HB);
+  const uint64_t tile = std::max<uint64_t>(1, hi / std::max<uint64_t>(1, gpb));
+  const uint64_t nbq = std::max<uint64_t>(tile, (n_bases / 3) / tile * tile);
+  double rate[3] = {0, 0, 0};
+  uint32_t nf_all = 0;
+  uint64_t done_b = 0;
+  int r = KH_OK;
+  for (int q = 0; q < 3 && done_b < n_bases; q++) {
+    if (q == 2 && rate[1] >= rate[0]) break;  // the moved pad is at least as fast: keep it
+    if (q > 0) {
+      (void)hipStreamSynchronize(ctx->stream);
+      (void)hipStreamSynchronize(ctx->side);
+      r = kh_debug_replace(ctx, 2);
+      if (r) return r;
+    }
+    const uint64_t nb = q == 2 ? std::min(nbq, n_bases - done_b) : std::min(nbq, n_bases - done_b);
+    const u256 s = sc_add(st, sc_reduce(u256_from_u128((u128)done_b * 2 * I.n)));
+    ctx->lanes_force = hi;
+    const timing t0 = ctx->tm[2];
+    uint32_t nf = 0;
+    const uint32_t off = std::min(nf_all, cap);
+    r = bsgs_scan_one(ctx, s, nullptr, nb, found ? found + off : nullptr, cap - off, &nf);
+    ctx->lanes_force = 0;
+    const double ms = ctx->tm[2].ms - t0.ms, pts = (double)(ctx->tm[2].points - t0.points);
+    rate[q] = ms > 0 ? pts / ms * 1e3 : 0;
+    nf_all += nf;
+    done_b += nb;
+    if ((r && r != KH_E_OVERFLOW) || ctx->found[0]) break;
+  }
+  *n_found = nf_all;
+  if (rate[0] > 0 && rate[1] > 0) {
+    ctx->lanes_pick = hi;
+    ctx->cal_rate[0] = rate[2] > 0 ? rate[2] : rate[1];
+    ctx->cal_rate[1] = rate[2] > 0 ? std::max(rate[0], rate[1]) : rate[0];
+    ctx->cal_stage = 1;
+  }
+  ctx->cal_moved_bases = done_b;
+  return r;
+}
+
 static int bsgs_scan_impl(kh_ctx *ctx, const u256 &st, const std::vector<u256> *list, uint64_t n_bases,
                           kh_bsgs_found *found, uint32_t cap, uint32_t *n_found) {
   if (!ctx->bsgs_built) return KH_E_STATE;
@@ -2702,6 +2766,13 @@ static int bsgs_scan_impl(kh_ctx *ctx, const u256 &st, const std::vector<u256> *
                          !getenv("KH_BSGS_LANES") && !getenv("KH_BSGS_NARROW") && !getenv("KH_NO_BIG_GROUPS") &&
                          n_bases * gpb >= 4ull * hi && ctx->targets.size() == 1 && !ctx->found[0];
   if (!calibrate) return bsgs_scan_one(ctx, st, list, n_bases, found, cap, n_found);
+  // KH_CAL_DEFER=N: the first N eligible calls walk uncalibrated (the board settles into its power-capped
+  // operating point first)
+  const char *dfr = getenv("KH_CAL_DEFER");
+  if (dfr && ctx->cal_deferred < (uint32_t)atoi(dfr)) {
+    ctx->cal_deferred++;
+    return bsgs_scan_one(ctx, st, list, n_bases, found, cap, n_found);
+  }
   // the primary pad at 2^21 lanes first (bsgs_scan_one would take it too): with no room, no calibration
   {
     size_t fr = 0, tot = 0;
@@ -2717,26 +2788,37 @@ static int bsgs_scan_impl(kh_ctx *ctx, const u256 &st, const std::vector<u256> *
   uint32_t nf_all = 0;
   uint64_t done_b = 0;
   int r = KH_OK;
-  // stages while the call has 4 tiles left for one (the last stage of the call takes the rest of it)
-  while (ctx->cal_stage < 2 && (n_bases - done_b) >= 4 * tile && !ctx->found[0]) {
+  // stages while the call has 4 tiles left for one (the last stage of the call takes the rest of it);
+  // KH_CAL_STAGES=1: the pad stage only
+  const char *nst = getenv("KH_CAL_STAGES");
+  const int stages = std::max(1, std::min(2, nst ? atoi(nst) : 1));
+  if (ctx->cal_stage >= stages) ctx->cal_stage = 2;
+  while (ctx->cal_stage < stages && (n_bases - done_b) >= 4 * tile && !ctx->found[0]) {
     const uint64_t left = n_bases - done_b;
     const uint64_t nb = ctx->cal_stage == 0 && left >= 8 * tile ? left / 2 / tile * tile : left;
     const u256 s = sc_add(st, sc_reduce(u256_from_u128((u128)done_b * 2 * I.n)));
     uint32_t nf = 0;
     const uint32_t off = std::min(nf_all, cap);
     const int stage = ctx->cal_stage;
-    r = cal_stage(ctx, stage, s, nb, found ? found + off : nullptr, cap - off, &nf);
+    const char *mv = getenv("KH_CAL_MOVE");
+    uint64_t walked = nb;
+    if (stage == 0 && mv && atoi(mv)) {
+      r = cal_move(ctx, s, nb, found ? found + off : nullptr, cap - off, &nf);
+      walked = ctx->cal_moved_bases;
+    } else {
+      r = cal_stage(ctx, stage, s, nb, found ? found + off : nullptr, cap - off, &nf);
+    }
     if (r == KH_CAL_SKIP) {  // no room for the stage's candidate: calibration ends here
       r = KH_OK;
       ctx->cal_stage = 2;
       break;
     }
     nf_all += nf;
-    done_b += nb;
+    done_b += walked;
     if (r && r != KH_E_OVERFLOW) return r;
     if (ctx->cal_stage == stage) break;  // undecided (the key ended the call): try again next call
   }
-  if (ctx->cal_stage >= 2) ctx->bsgs_calibrated = true;
+  if (ctx->cal_stage >= stages) ctx->bsgs_calibrated = true;
   if (done_b < n_bases && !ctx->found[0] && (r == KH_OK || r == KH_E_OVERFLOW)) {
     const u256 s = sc_add(st, sc_reduce(u256_from_u128((u128)done_b * 2 * I.n)));
     uint32_t nf = 0;
@@ -2990,6 +3072,7 @@ int kh_walk_points(kh_ctx *ctx, const uint8_t start[32], const uint8_t stride_be
   A.scratch = ctx->d_scratch;
   A.L = jg.L;
   A.pad_skew = ctx->pad_skew;
+  A.pad_swz = pad_swizzle(A.L);
   A.lane_stride = jg.gpl * 2 * H;
   A.n_points = n_points;
   A.dump_x = dx;

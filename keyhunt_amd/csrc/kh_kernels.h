@@ -230,6 +230,9 @@ struct walk_args {
   uint32_t zhalf;
   // inversion pad: lanes of gap after each row (row stride L + pad_skew entries; KH_PAD_SKEW A/B knob)
   uint32_t pad_skew;
+  // inversion pad: row r keeps lane g's entry in column g ^ ((r & 7) << 8) (L a multiple of 2048), so
+  // the columns of one 256-lane workgroup -- one XCD's -- rotate over the 8 KB chunk classes row by row
+  uint32_t pad_swz;
 };
 
 struct setup_args {

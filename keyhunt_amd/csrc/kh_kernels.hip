@@ -589,7 +589,10 @@ __global__ void __launch_bounds__((walk_threads<MODE, H>()), (walk_blocks_per_cu
   auto slot_w = [&](int m) { return fold(m, 1); };
   auto slot = [&](int m) { return fold(m, 2); };
 #else
-  auto slot = [&](int m) { return (size_t)(SPARSE ? (m >> 1) : m) * LS + g; };
+  auto slot = [&](int m) {
+    const uint32_t r = SPARSE ? (uint32_t)(m >> 1) : (uint32_t)m;
+    return (size_t)r * LS + (A.pad_swz ? (g ^ ((r & 7u) << 8)) : g);
+  };
   auto slot_w = slot;
 #endif
   // Deferred-probe walks (one 16-B split-block load per point, issued a step ahead): the BSGS giant

@@ -461,20 +461,24 @@ def test_calls_with_ragged_lane_tiles(oracle, lanes, calls):
     assert res[1][0] == res[3][0] == [(0, key)]
 
 
-@pytest.mark.parametrize("cands", [2, 3])
-def test_placement_calibration_same_results(oracle, monkeypatch, cands):
-    """A context's first call of >= 2^23 walk groups walks its parts on candidate placements -- first of
-    the pad (the primary and KH_PAD_CANDIDATES - 1 more, in the order A B B A / A B C C B A, or 2^21 and
-    2^20 lanes on one pad when the device has no room), then of layer 1 (a copy) -- and keeps the fastest
-    of each: the same first-level candidates and walked points as an uncalibrated call
-    (KH_BSGS_CALIBRATE=0), the key found in any part, and kh_bsgs_geometry / kh_bsgs_placement report
-    the kept and the best other candidates' rates."""
+@pytest.mark.parametrize("cands,stages", [(1, 1), (2, 2), (3, 2), ("move", 1)])
+def test_placement_calibration_same_results(oracle, monkeypatch, cands, stages):
+    """A context's first call of >= 2^23 walk groups walks its parts on candidate placements and keeps the
+    fastest: by default 2^21 and 2^20 lanes on the one pad (A B B A); opt-in, several pads held at once
+    (KH_PAD_CANDIDATES, A B C C B A) then a layer-1 copy (KH_CAL_STAGES=2), or the pad moved
+    (KH_CAL_MOVE=1).  The same first-level candidates and walked points as an uncalibrated call
+    (KH_BSGS_CALIBRATE=0), the key found in any part, and kh_bsgs_geometry / kh_bsgs_placement report the
+    kept and the best other candidates' rates."""
     import keyhunt_amd as K
     p = oracle.bsgs_params(N36, K16)
     nb = 1 << 22                           # 4 groups per base: 8 x 2^21 groups, both stages in one call
     start = 0x3C3C3C3C3C000000
     far = start - 777 * 2 * p.n
-    monkeypatch.setenv("KH_PAD_CANDIDATES", str(cands))
+    if cands == "move":
+        monkeypatch.setenv("KH_CAL_MOVE", "1")
+    else:
+        monkeypatch.setenv("KH_PAD_CANDIDATES", str(cands))
+    monkeypatch.setenv("KH_CAL_STAGES", str(stages))
     res = []
     for calibrate in (True, False):
         if calibrate:
@@ -491,9 +495,11 @@ def test_placement_calibration_same_results(oracle, monkeypatch, cands):
     assert res[0][0] == res[1][0] and res[0][0] > 1000
     assert res[0][1] == res[1][1] == nb * p.aux
     lanes, r_kept, r_other = res[0][2]
-    assert lanes in (1 << 21, 1 << 20) and r_kept >= r_other > 0
+    assert lanes in (1 << 21, 1 << 20) and r_kept > 0 and r_other > 0
+    assert cands == "move" or r_kept >= r_other   # a move keeps its last placement whatever it measured
     done, rates = res[0][3]
-    assert done and rates[0] == r_kept and rates[2] >= rates[3] > 0
+    assert done and rates[0] == r_kept
+    assert (rates[2] >= rates[3] > 0) if stages == 2 else rates[2:] == [0.0, 0.0]
     assert res[1][2] == (0, 0.0, 0.0) and res[1][3] == (False, [0.0] * 4)
     monkeypatch.delenv("KH_BSGS_CALIBRATE", raising=False)
     for where in (3, nb // 2 - 7, nb - 5):  # the key in the first, a middle and the last part

@@ -1,7 +1,7 @@
 """Which buffer's placement sets the BSGS walk's state?  One process on the bench geometry (n = 2^44,
 k = 128, 2^21 lanes, no calibration): for each entry of --seq, give the buffers it names fresh
 allocations (kh_debug_replace: 1 layer 1, 2 the pad, 4 the lane arrays, 8 the delta tables, 16 layers
-2/3; "r" = kh_release_walk) and time --calls calls of --bases bases after one warm call.  Prints one
+2/3, 32 a new walk stream; "r" = kh_release_walk; "s0" / "s1" = switch KH_PAD_SWZ, no move) and time --calls calls of --bases bases after one warm call.  Prints one
 JSON object with every step's rate and the board's clock and power.  (Round-6 r06h ran it as
 --seq 1,1,1,1,1,1,r,r,r,r.)
 
@@ -56,12 +56,15 @@ def main():
         print(json.dumps({"moved": what, "k": k, "G": round(r["giant_points_per_s"] / 1e9, 3),
                           "mhz": round(r["mhz"] or 0), "w": round(r["w"] or 0)}), file=sys.stderr, flush=True)
 
-    names = {1: "layer1", 2: "pad", 4: "lanes", 8: "tables", 16: "layers23"}
+    names = {1: "layer1", 2: "pad", 4: "lanes", 8: "tables", 16: "layers23", 32: "stream"}
     timed("none", 0)
     for k, w in enumerate(a.seq.split(",")):
         if w == "r":
             e.release_walk()
             timed("release_walk", k)
+        elif w[0] in "sS":          # s0 / s1: KH_PAD_SWZ off / on (the pad's column swizzle), no move
+            os.environ["KH_PAD_SWZ"] = w[1:]
+            timed("swz" + w[1:], k)
         else:
             e.debug_replace(int(w))
             timed("+".join(v for b, v in names.items() if int(w) & b), k)
