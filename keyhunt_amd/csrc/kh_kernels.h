@@ -141,6 +141,9 @@ KH_HD void kh_blk_masks(uint32_t s0, uint32_t s1, uint32_t s2, uint32_t m[4]) {
 #ifndef KH_PAD_PLANES
 #define KH_PAD_PLANES 0
 #endif
+#ifndef KH_PAD_KNOBS
+#define KH_PAD_KNOBS 0  // kernel side of the KH_PAD_SKEW / KH_PAD_SWZ pad-layout A/B knobs
+#endif
 //   KH_PAD_NT      the inversion pad's stores (bit 0) / loads (bit 1) with the nontemporal hint
 #ifndef KH_PAD_NT
 #define KH_PAD_NT 0

@@ -569,7 +569,10 @@ __global__ void __launch_bounds__((walk_threads<MODE, H>()), (walk_blocks_per_cu
   };
   uint4 *__restrict__ scr = A.scratch;
   const size_t L = A.L;
-  const size_t LS = L + A.pad_skew;  // the pad's row stride in lane entries
+  // the pad's row stride in lane entries; the row-skew and column-swizzle A/B knobs (KH_PAD_SKEW,
+  // KH_PAD_SWZ: no effect on the rate, DESIGN.md §2 "Placement") cost ~1 VALU per point, so they are
+  // compiled in only with -DKH_PAD_KNOBS=1
+  const size_t LS = KH_PAD_KNOBS ? L + A.pad_skew : L;
   fe cx, cy;
   load_soa(cx, A.cx, A.L, g);
   load_soa(cy, A.cy, A.L, g);
@@ -591,7 +594,7 @@ __global__ void __launch_bounds__((walk_threads<MODE, H>()), (walk_blocks_per_cu
 #else
   auto slot = [&](int m) {
     const uint32_t r = SPARSE ? (uint32_t)(m >> 1) : (uint32_t)m;
-    return (size_t)r * LS + (A.pad_swz ? (g ^ ((r & 7u) << 8)) : g);
+    return (size_t)r * LS + (KH_PAD_KNOBS && A.pad_swz ? (g ^ ((r & 7u) << 8)) : g);
   };
   auto slot_w = slot;
 #endif

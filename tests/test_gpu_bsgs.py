@@ -585,9 +585,10 @@ def test_bsgs_lanes_continue_across_calls(engine, oracle):
 
 
 def test_pad_skew_and_offset_same_results(oracle, monkeypatch):
-    """The pad layout knobs (KH_PAD_SKEW: a gap of lanes after every pad row; KH_PAD_OFFSET: the pad's
-    start inside its allocation) move only where the inversion pad sits: the same first-level candidates,
-    walked points and key as the default layout, for the BSGS walk and an xpoint chunk."""
+    """The pad layout knobs (KH_PAD_SKEW: a gap of lanes after every pad row, honoured by the kernels of
+    a -DKH_PAD_KNOBS=1 build; KH_PAD_OFFSET: the pad's start inside its allocation) move only where the
+    inversion pad sits: the same first-level candidates, walked points and key as the default layout, for
+    the BSGS walk and an xpoint chunk."""
     import keyhunt_amd as K
     p = oracle.bsgs_params(N36, K16)
     start = 0x7777777700000
