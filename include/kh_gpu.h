@@ -139,6 +139,9 @@ int kh_debug_layout(kh_ctx *ctx, uint64_t out[8]);
  * 8 the walks' delta tables, 16 layers 2 and 3, 32 a new walk stream (bits may be combined).  Results
  * are unchanged. */
 int kh_debug_replace(kh_ctx *ctx, uint32_t which);
+/* diagnostics: enqueue about `ms` milliseconds of a VALU-dense load (no memory traffic) on the walk's
+ * stream, left in flight (the board's clock/power operating point study, DESIGN.md §2 "Placement") */
+int kh_debug_burn(kh_ctx *ctx, double ms);
 int kh_synchronize(kh_ctx *ctx);
 
 /* ---- address / rmd160 / xpoint ------------------------------------------------------------ */

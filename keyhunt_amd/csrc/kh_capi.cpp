@@ -343,6 +343,8 @@ struct kh_ctx {
   int cal_stage = 0;
   uint64_t cal_moved_bases = 0;  // bases the last KH_CAL_MOVE stage walked
   uint32_t cal_deferred = 0;      // eligible calls walked uncalibrated (KH_CAL_DEFER)
+  bool burned = false;            // KH_BURN_MS ran before this context's first large BSGS call
+  double burn_ms = 0;
   uint32_t groups_per_launch = 0;
   uint32_t lanes_alloc = 0;
   int scratch_h = 0;  // inversion-pad entries per lane in d_scratch
@@ -927,6 +929,23 @@ int kh_debug_replace(kh_ctx *ctx, uint32_t which) {
       r = move_buffer(ctx, reinterpret_cast<void **>(&ctx->d_bl[l]), 256 * ctx->bd[l].stride + 4, 0);
   }
   return r;
+}
+
+int kh_debug_burn(kh_ctx *ctx, double ms) {
+  if (!ctx || !(ms > 0)) return KH_E_ARG;
+  (void)hipSetDevice(ctx->device);
+  uint32_t *sink = ctx->d_zero_flag;
+  const uint32_t iters = 1u << 16;
+  HIPCHK(ctx, hipEventRecord(ctx->ev_a, ctx->stream));
+  HIPCHK(ctx, launch_burn(iters, sink, ctx->stream));
+  HIPCHK(ctx, hipEventRecord(ctx->ev_b, ctx->stream));
+  HIPCHK(ctx, hipEventSynchronize(ctx->ev_b));
+  float one = 0;
+  (void)hipEventElapsedTime(&one, ctx->ev_a, ctx->ev_b);
+  const int more = one > 0 ? (int)std::min(10000.0, ms / one) : 0;
+  for (int k = 1; k < more; k++) HIPCHK(ctx, launch_burn(iters, sink, ctx->stream));  // left in flight
+  ctx->burn_ms = one * std::max(1, more);
+  return KH_OK;
 }
 
 int kh_debug_layout(kh_ctx *ctx, uint64_t out[8]) {
@@ -2760,6 +2779,17 @@ static int bsgs_scan_impl(kh_ctx *ctx, const u256 &st, const std::vector<u256> *
   const uint64_t gpb = A_pts / (2 * KH_WALK_HB);
   const uint32_t hi = ctx->lanes_bsgs, lo = ctx->lanes_bsgs / 2;
   const uint64_t tile = std::max<uint64_t>(1, hi / std::max<uint64_t>(1, gpb));  // bases per 2^21 groups
+  // KH_BURN_MS=<ms>: before the context's first large call, that long a VALU-dense load on the walk's
+  // stream, enqueued right ahead of the walk (A/B knob for the clock/latency operating point)
+  if (!ctx->burned && n_bases * gpb >= hi) {
+    ctx->burned = true;
+    const char *bm = getenv("KH_BURN_MS");
+    const double want_ms = bm ? atof(bm) : 0.0;
+    if (want_ms > 0) {
+      const int rb = kh_debug_burn(ctx, want_ms);
+      if (rb) return rb;
+    }
+  }
   const char *cal = getenv("KH_BSGS_CALIBRATE");
   const bool calibrate = !ctx->bsgs_calibrated && !list && A_pts == I.aux && A_pts % (2 * KH_WALK_HB) == 0 &&
                          hi == KH_BSGS_LANES && lo > ctx->lanes_max && !(cal && atoi(cal) == 0) &&

@@ -293,6 +293,7 @@ inline int walk_pad_rows(int mode, bool tblk, int H) {
 }
 hipError_t launch_walk_zinv(int mode, const walk_args &A, hipStream_t st);
 hipError_t launch_refine(const refine_args &A, hipStream_t st);
+hipError_t launch_burn(uint32_t iters, uint32_t *sink, hipStream_t st);
 hipError_t launch_setup(const setup_args &A, hipStream_t st);
 hipError_t launch_test_hash160(const uint32_t *xs, const uint32_t *ys, uint32_t n, uint32_t *out, hipStream_t st);
 hipError_t launch_test_field(const uint32_t *a, const uint32_t *b, uint32_t n, uint32_t *out, hipStream_t st);

@@ -1359,6 +1359,29 @@ hipError_t launch_walk_zinv(int mode, const walk_args &A, hipStream_t st) {
 #endif
 }
 
+// A VALU-dense load (multiply-add chains, no memory traffic) run right before a BSGS job's first walk
+// launch (KH_BURN_MS, kh_capi.cpp): it drives the board's clock down to its power cap before the walk
+// starts, so the walk settles into the low-clock operating point (DESIGN.md §2 "Placement")
+__global__ void __launch_bounds__(256) k_burn(uint32_t iters, uint32_t *sink) {
+  uint64_t a[8];
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < 8; k++) a[k] = (uint64_t)(g * 2654435761u + k) | 1;
+  for (uint32_t i = 0; i < iters; i++) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) a[k] = (uint64_t)(uint32_t)a[k] * (uint32_t)(a[k] >> 17) + a[(k + 1) & 7];
+  }
+  uint64_t x = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) x ^= a[k];
+  if (x == 0x0123456789ABCDEFull) sink[0] = g;  // never in practice: keeps the chains live
+}
+
+hipError_t launch_burn(uint32_t iters, uint32_t *sink, hipStream_t st) {
+  hipLaunchKernelGGL(k_burn, dim3(256 * 8), dim3(256), 0, st, iters, sink);
+  return hipGetLastError();
+}
+
 hipError_t launch_refine(const refine_args &A, hipStream_t st) {
   hipLaunchKernelGGL(k_refine, dim3((A.cap + 63) / 64), dim3(64), 0, st, A);
   return hipGetLastError();

@@ -81,6 +81,7 @@ def lib() -> ctypes.CDLL:
     L.kh_debug_layout.argtypes = [P, ctypes.POINTER(ctypes.c_uint64 * 8)]
     L.kh_bsgs_placement.argtypes = [P, ctypes.POINTER(ctypes.c_double * 4)]
     L.kh_debug_replace.argtypes = [P, ctypes.c_uint32]
+    L.kh_debug_burn.argtypes = [P, ctypes.c_double]
     L.kh_bsgs_geometry.argtypes = [P, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_double * 2)]
     L.kh_synchronize.argtypes = [P]
     L.kh_scan_memory.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64)]
@@ -195,6 +196,10 @@ class Engine:
         """Give device buffers fresh allocations (kh_debug_replace; diagnostics): 1 layer 1, 2 the pad,
         4 the lane arrays, 8 the delta tables, 16 layers 2 and 3."""
         self._chk(lib().kh_debug_replace(self._ctx, which), "kh_debug_replace")
+
+    def debug_burn(self, ms: float) -> None:
+        """Enqueue ~ms of VALU-dense load on the walk's stream (kh_debug_burn; diagnostics)."""
+        self._chk(lib().kh_debug_burn(self._ctx, ms), "kh_debug_burn")
 
     def debug_replace_layer1(self) -> None:
         self.debug_replace(1)

@@ -1,7 +1,7 @@
 """Which buffer's placement sets the BSGS walk's state?  One process on the bench geometry (n = 2^44,
 k = 128, 2^21 lanes, no calibration): for each entry of --seq, give the buffers it names fresh
 allocations (kh_debug_replace: 1 layer 1, 2 the pad, 4 the lane arrays, 8 the delta tables, 16 layers
-2/3, 32 a new walk stream; "r" = kh_release_walk; "s0" / "s1" = switch KH_PAD_SWZ, no move) and time --calls calls of --bases bases after one warm call.  Prints one
+2/3, 32 a new walk stream; "r" = kh_release_walk; "s0" / "s1" = switch KH_PAD_SWZ, no move; "bN" = N ms of VALU burn first; "iN" = N ms idle first) and time --calls calls of --bases bases after one warm call.  Prints one
 JSON object with every step's rate and the board's clock and power.  (Round-6 r06h ran it as
 --seq 1,1,1,1,1,1,r,r,r,r.)
 
@@ -62,6 +62,13 @@ def main():
         if w == "r":
             e.release_walk()
             timed("release_walk", k)
+        elif w[0] == "b":           # bN: N ms of VALU burn right before the timed calls
+            e.debug_burn(float(w[1:]))
+            timed("burn" + w[1:], k)
+        elif w[0] == "i":           # iN: N ms idle (the board's clock rises), then the timed calls
+            e.synchronize()
+            time.sleep(float(w[1:]) / 1e3)
+            timed("idle" + w[1:], k)
         elif w[0] in "sS":          # s0 / s1: KH_PAD_SWZ off / on (the pad's column swizzle), no move
             os.environ["KH_PAD_SWZ"] = w[1:]
             timed("swz" + w[1:], k)
