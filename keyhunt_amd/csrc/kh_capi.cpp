@@ -2746,7 +2746,7 @@ static int cal_move(kh_ctx *ctx, const u256 &st, uint64_t n_bases, kh_bsgs_found
       r = kh_debug_replace(ctx, 2);
       if (r) return r;
     }
-    const uint64_t nb = q == 2 ? std::min(nbq, n_bases - done_b) : std::min(nbq, n_bases - done_b);
+    const uint64_t nb = std::min(nbq, n_bases - done_b);
     const u256 s = sc_add(st, sc_reduce(u256_from_u128((u128)done_b * 2 * I.n)));
     ctx->lanes_force = hi;
     const timing t0 = ctx->tm[2];
@@ -2846,7 +2846,10 @@ static int bsgs_scan_impl(kh_ctx *ctx, const u256 &st, const std::vector<u256> *
     nf_all += nf;
     done_b += walked;
     if (r && r != KH_E_OVERFLOW) return r;
-    if (ctx->cal_stage == stage) break;  // undecided (the key ended the call): try again next call
+    if (ctx->cal_stage == stage) {  // undecided: the key ended the call (try again next call), or a
+      if (!ctx->found[0]) ctx->cal_stage = 2;  // part could not take its lane count (give up)
+      break;
+    }
   }
   if (ctx->cal_stage >= stages) ctx->bsgs_calibrated = true;
   if (done_b < n_bases && !ctx->found[0] && (r == KH_OK || r == KH_E_OVERFLOW)) {
