@@ -2825,7 +2825,8 @@ static int bsgs_scan_impl(kh_ctx *ctx, const u256 &st, const std::vector<u256> *
   if (ctx->cal_stage >= stages) ctx->cal_stage = 2;
   while (ctx->cal_stage < stages && (n_bases - done_b) >= 4 * tile && !ctx->found[0]) {
     const uint64_t left = n_bases - done_b;
-    const uint64_t nb = ctx->cal_stage == 0 && left >= 8 * tile ? left / 2 / tile * tile : left;
+    // with a second stage to come, the first takes half of a call that holds both
+    const uint64_t nb = ctx->cal_stage == 0 && stages > 1 && left >= 8 * tile ? left / 2 / tile * tile : left;
     const u256 s = sc_add(st, sc_reduce(u256_from_u128((u128)done_b * 2 * I.n)));
     uint32_t nf = 0;
     const uint32_t off = std::min(nf_all, cap);
