@@ -151,6 +151,17 @@ def test_bench_config_k128_known_answer():
     assert [h["key"] for h in hits] == ["1c533b6bb7f0804e09960225e44877ac"]
 
 
+def test_cli_first_call_calibrates_and_finds_the_key():
+    """The CLI's first 2^35-point call (2^20 bases at k = 128) holds the placement calibration's four
+    parts; puzzle 125's key placed in the third part (2^19 + 1000 bases after the range start) is found,
+    the same key as in the reference-verified window above."""
+    start = 0x1c533b6bb7f0804e0995fe0000000000 - ((1 << 19) + 1000) * (1 << 45)
+    end = start + (1 << 20) * (1 << 45)
+    p, hits = run_cli(["-m", "bsgs", "-f", "125.txt", "-k", "128", "-r", f"{start:x}:{end:x}"], timeout=900)
+    assert p.returncode == 1, p.stdout[-2000:] + p.stderr[-2000:]
+    assert [h["key"] for h in hits] == ["1c533b6bb7f0804e09960225e44877ac"]
+
+
 def test_config5_geometry_k512_known_answer():
     """configs[4] geometry (-k 512: M = 2^31, 7.36 GB layer-1 bloom per GPU) on the window that holds
     puzzle 130's key (verified by the reference)."""
