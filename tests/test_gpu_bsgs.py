@@ -162,6 +162,17 @@ def test_cli_first_call_calibrates_and_finds_the_key():
     assert [h["key"] for h in hits] == ["1c533b6bb7f0804e09960225e44877ac"]
 
 
+def test_cli_two_contexts_calibrate_and_find_the_key():
+    """-g 2 on one GPU over two calls' worth of bases: each context's first 2^35-point call calibrates
+    (each holds its own 2^21-lane pad), and the key, placed in the second call, is found once."""
+    start = 0x1c533b6bb7f0804e0995fe0000000000 - ((1 << 20) + (1 << 19) + 77) * (1 << 45)
+    end = start + (1 << 21) * (1 << 45)
+    p, hits = run_cli(["-m", "bsgs", "-f", "125.txt", "-k", "128", "-g", "2", "-r", f"{start:x}:{end:x}"],
+                      timeout=900)
+    assert p.returncode == 1, p.stdout[-2000:] + p.stderr[-2000:]
+    assert sorted({h["key"] for h in hits}) == ["1c533b6bb7f0804e09960225e44877ac"]
+
+
 def test_config5_geometry_k512_known_answer():
     """configs[4] geometry (-k 512: M = 2^31, 7.36 GB layer-1 bloom per GPU) on the window that holds
     puzzle 130's key (verified by the reference)."""
